@@ -1,0 +1,335 @@
+"""CPU oracle for the reference's compat hot path (TEST INFRASTRUCTURE -- never shipped).
+
+Restates, function by function, what the reference computes on the path that
+BASELINE.json's north_star names, with the same numerics:
+
+  SignalProcessor  /root/reference/tetraear/signal/processor.py:18-273
+  TetraDecoder     /root/reference/tetraear/core/decoder.py:140-295, 835-888 (lower-MAC part)
+  TetraProtocolParser.parse_burst/_check_crc/_calculate_crc16
+                   /root/reference/tetraear/core/protocol.py:192-347
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module.
+It is pinned bit-exact against golden vectors produced by running the reference itself
+(tests/golden/make_golden.py; tests/test_oracle_golden.py checks the pin).
+
+Heavy loops live in compat_oracle.c (liboracle.so, built by oracle/Makefile); vector math
+uses the same numpy/scipy calls the reference makes, so third-party numerics (scipy 1.15.3
+filter design, numpy's SIMD complex kernels) are inherited, not re-derived.
+"""
+import ctypes
+import os
+
+import numpy as np
+from scipy import signal as _ss
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            import subprocess
+            subprocess.check_call(["make", "-s", "-C", _HERE])
+        L = ctypes.CDLL(path)
+        f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+        f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+        u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+        i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
+        L.orc_sosfilt_f32.argtypes = [f32p, ctypes.c_int, f32p, f32p, ctypes.c_long]
+        L.orc_sosfilt_f64.argtypes = [f64p, ctypes.c_int, f64p, f64p, ctypes.c_long]
+        L.orc_lfilter_f64.argtypes = [f64p, f64p, ctypes.c_int, f64p, f64p, ctypes.c_long]
+        L.orc_sync_counts.argtypes = [u8p, ctypes.c_long, u8p, u8p]
+        L.orc_find_sync_greedy.argtypes = [u8p, u8p, ctypes.c_long, ctypes.c_int, i64p, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_int)]
+        L.orc_find_sync_greedy.restype = ctypes.c_int
+        L.orc_crc16.argtypes = [u8p, ctypes.c_long, ctypes.c_int]
+        L.orc_crc16.restype = ctypes.c_uint32
+        L.orc_check_crc.argtypes = [u8p, ctypes.c_long]
+        L.orc_check_crc.restype = ctypes.c_int
+        _LIB = L
+    return _LIB
+
+
+# ----------------------------------------------------------------------------- filters
+
+def _odd_ext(x, n):
+    """scipy.signal._arraytools.odd_ext along the last axis, in x's own dtype."""
+    left = 2 * x[0:1] - x[n:0:-1]
+    right = 2 * x[-1:] - x[-2:-(n + 2):-1]
+    return np.concatenate((left, x, right))
+
+
+def _components(v):
+    return (v.real, v.imag) if np.iscomplexobj(v) else (v,)
+
+
+def _run_per_component(ext, dtype, init_state, step):
+    """Run a real recursion `step(comp, state)` over each component of ext (forward+reverse)."""
+    real_t = np.float32 if dtype in (np.float32, np.complex64) else np.float64
+    outs = []
+    for comp in _components(ext.astype(dtype)):
+        c = np.ascontiguousarray(comp, dtype=real_t)
+        step(c, init_state(c[0]))
+        c = np.ascontiguousarray(c[::-1])
+        step(c, init_state(c[0]))
+        outs.append(c[::-1])
+    if np.iscomplexobj(np.zeros(0, dtype)):
+        return (outs[0] + 1j * outs[1]).astype(dtype)
+    return outs[0].astype(dtype)
+
+
+def sosfiltfilt(sos, x):
+    """scipy.signal.sosfiltfilt(sos, x) with default odd padding (scipy 1.15.3)."""
+    ns = sos.shape[0]
+    ntaps = 2 * ns + 1 - min(int((sos[:, 2] == 0).sum()), int((sos[:, 5] == 0).sum()))
+    edge = 3 * ntaps
+    if x.shape[0] <= edge:
+        raise ValueError(f"The length of the input vector x must be greater than padlen, which is {edge}.")
+    dtype = np.result_type(sos, x)
+    zi = _ss.sosfilt_zi(sos)
+    real_t = np.float32 if dtype in (np.float32, np.complex64) else np.float64
+    zr = np.ascontiguousarray(zi.real, dtype=real_t)
+    coef = np.ascontiguousarray(np.asarray(sos).real, dtype=real_t)
+    fn = lib().orc_sosfilt_f32 if real_t is np.float32 else lib().orc_sosfilt_f64
+    ext = _odd_ext(x, edge)
+    y = _run_per_component(ext, dtype, lambda x0: np.ascontiguousarray(zr * x0, dtype=real_t),
+                           lambda c, st: fn(coef, ns, st, c, len(c)))
+    return y[edge:-edge]
+
+
+def decimate(x, q):
+    """scipy.signal.decimate(x, q) (IIR, zero phase), scipy 1.15.3 _signaltools.decimate."""
+    x = np.asarray(x)
+    rt = x.dtype
+    if not np.issubdtype(rt, np.inexact) or rt.type == np.float16:
+        rt = np.float64
+    sos = np.asarray(_ss.cheby1(8, 0.05, 0.8 / q, output="sos"), dtype=rt)
+    return sosfiltfilt(sos, x)[::q]
+
+
+def filtfilt(b, a, x):
+    """scipy.signal.filtfilt(b, a, x) with default odd padding, a[0] == 1."""
+    assert a[0] == 1.0
+    edge = 3 * max(len(a), len(b))
+    if x.shape[0] <= edge:
+        raise ValueError(f"The length of the input vector x must be greater than padlen, which is {edge}.")
+    zi = np.ascontiguousarray(_ss.lfilter_zi(b, a), dtype=np.float64)
+    ext = _odd_ext(x, edge)
+    dtype = np.result_type(b, a, ext, zi[:1] * ext[:1])
+    bb = np.ascontiguousarray(b, np.float64)
+    aa = np.ascontiguousarray(a, np.float64)
+    y = _run_per_component(ext, dtype, lambda x0: np.ascontiguousarray(zi * x0),
+                           lambda c, st: lib().orc_lfilter_f64(bb, aa, len(bb), st, c, len(c)))
+    return y[edge:-edge]
+
+
+# ----------------------------------------------------------------------------- demod
+
+def _pairwise_sum(v):
+    """numpy's pairwise summation for float64 (np.add.reduce on a contiguous 1-D array)."""
+    return np.add.reduce(v)
+
+
+class SignalProcessor:
+    """Restatement of processor.py:18-273."""
+
+    def __init__(self, sample_rate=2.4e6):
+        self.sample_rate = sample_rate
+        self.symbol_rate = 18000
+        self.samples_per_symbol = int(sample_rate / self.symbol_rate)
+        self.symbols = None
+
+    def filter_signal(self, samples, bandwidth=25000, sample_rate=None):
+        if len(samples) == 0:
+            return samples
+        fs = sample_rate if sample_rate is not None else self.sample_rate
+        cutoff = min(0.99, max(0.01, (bandwidth / 2) / (fs / 2)))
+        try:
+            b, a = _ss.butter(4, cutoff, btype="low")
+            return filtfilt(b, a, np.asarray(samples))
+        except Exception:
+            return samples
+
+    def frequency_shift(self, samples, freq_offset, sample_rate=None):
+        fs = sample_rate if sample_rate is not None else self.sample_rate
+        t = np.arange(len(samples)) / fs
+        return samples * np.exp(-1j * 2 * np.pi * freq_offset * t)
+
+    def demodulate_dqpsk(self, samples):
+        if len(samples) < 2:
+            return np.array([], dtype=np.uint8)
+        samples = np.asarray(samples)
+        m = np.max(np.abs(samples))
+        if m > 0:
+            samples = samples / m
+        s = samples[1:]
+        p = samples[:-1]
+        if np.iscomplexobj(samples):
+            sr, si, pr, pi = s.real, s.imag, p.real, -p.imag
+            # numpy scalar complex multiply (no FMA): (sr*pr - si*pi, sr*pi + si*pr)
+            dr = sr * pr - si * pi
+            di = sr * pi + si * pr
+        else:
+            dr = s * p
+            di = np.zeros_like(dr)
+        ph = np.arctan2(di, dr)
+        out = np.full(len(ph), 3, np.uint8)
+        out[ph < 5 * np.pi / 8] = 1
+        out[ph < 3 * np.pi / 8] = 0
+        out[ph < -3 * np.pi / 8] = 2
+        out[ph < -5 * np.pi / 8] = 3
+        return out
+
+    def extract_symbols(self, samples, sample_rate=None):
+        if len(samples) == 0:
+            return np.array([], dtype=complex)
+        fs = sample_rate if sample_rate is not None else self.sample_rate
+        sps = int(fs / self.symbol_rate)
+        if sps <= 1:
+            return samples
+        best, maxp = 0, -1
+        for ph in range(0, sps, max(1, sps // 8)):
+            ns = (len(samples) - ph) // sps
+            if ns <= 0:
+                continue
+            p = np.mean(np.abs(samples[ph + np.arange(ns) * sps]) ** 2)
+            if p > maxp:
+                maxp, best = p, ph
+        ns = (len(samples) - best) // sps
+        return samples[best + np.arange(ns) * sps]
+
+    def process(self, samples, freq_offset=0):
+        if len(samples) == 0:
+            self.symbols = np.array([], dtype=complex)
+            return np.array([], dtype=np.uint8)
+        rate = self.sample_rate
+        if rate > 240000 * 2:
+            q = int(rate / 240000)
+            if q > 1:
+                try:
+                    samples = decimate(samples, q)
+                    rate = rate / q
+                except Exception:
+                    pass
+        if freq_offset != 0:
+            samples = self.frequency_shift(samples, freq_offset, sample_rate=rate)
+        filtered = self.filter_signal(samples, bandwidth=25000, sample_rate=rate)
+        sym = self.extract_symbols(filtered, sample_rate=rate)
+        self.symbols = sym
+        return self.demodulate_dqpsk(sym)
+
+
+# ----------------------------------------------------------------------------- lower MAC
+
+SYNC_CONT = np.array([1, 1, 0, 1, 0, 0, 0, 0, 1, 1, 1, 0, 1, 0, 0, 1, 1, 1, 0, 1, 0, 0], np.uint8)
+SYNC_DISC = np.array([0, 0, 1, 1, 1, 0, 1, 0, 0, 1, 0, 0, 0, 0, 1, 1, 0, 1, 0, 0, 1, 1], np.uint8)
+
+
+def count_threshold(thr):
+    """Least integer count c with c/22 >= thr (the float comparison of decoder.py:240-245)."""
+    for c in range(23):
+        if c / 22 >= thr:
+            return c
+    return 23
+
+
+def symbols_to_bits(symbols):
+    """decoder.py:140-169 (returns int64 arrays like np.array(list_of_ints))."""
+    symbols = np.asarray(symbols)
+    if len(symbols) == 0:
+        return np.array([]), np.array([])
+    if np.max(symbols) <= 3:
+        val = symbols.astype(np.int64) & 0x3
+    else:
+        lut = np.array([0, 0, 0, 1, 1, 3, 2, 2], np.int64)
+        s = symbols.astype(np.int64)
+        val = np.where((s >= 0) & (s <= 7), lut[np.clip(s, 0, 7)], 0)
+    bits = np.stack([val >> 1, val & 1], axis=1).reshape(-1)
+    return bits, val
+
+
+def find_sync(bits, threshold=0.85, return_max_corr=False):
+    """decoder.py:171-295."""
+    bits = np.ascontiguousarray(np.asarray(bits), dtype=np.uint8) if len(bits) else np.zeros(0, np.uint8)
+    if len(bits) < 22:
+        return ([], 0.0) if return_max_corr else []
+    nw = len(bits) - 21
+    c1 = np.empty(nw, np.uint8)
+    c2 = np.empty(nw, np.uint8)
+    lib().orc_sync_counts(bits, len(bits), c1, c2)
+    pos = np.zeros(nw // 250 + 2, np.int64)
+    mc = ctypes.c_int(0)
+    n = lib().orc_find_sync_greedy(c1, c2, nw, count_threshold(threshold), pos, len(pos), ctypes.byref(mc))
+    sync = [int(p) for p in pos[:n]]
+    max_corr = mc.value / 22
+    if not sync and max_corr > 0.75 and max_corr >= (threshold - 0.15):
+        adaptive = max(0.75, max_corr - 0.02)
+        if adaptive < threshold:
+            m = np.maximum(c1, c2)
+            k = count_threshold(adaptive)
+            last = -10 ** 9
+            for i in np.nonzero(m >= k)[0]:
+                if i >= last + 250:
+                    sync.append(int(i))
+                    last = int(i)
+    return (sync, max_corr) if return_max_corr else sync
+
+
+def decode_syncs(bits):
+    """The threshold cascade of decoder.py:845-857."""
+    sp, mc = find_sync(bits, threshold=0.90, return_max_corr=True)
+    if not sp:
+        sp, mc = find_sync(bits, threshold=0.85, return_max_corr=True)
+        if not sp:
+            sp, mc = find_sync(bits, threshold=0.80, return_max_corr=True)
+            if not sp and mc >= 0.75:
+                sp, _ = find_sync(bits, threshold=max(0.75, mc - 0.02), return_max_corr=True)
+    return sp
+
+
+def calculate_crc16(bits):
+    b = np.ascontiguousarray(np.asarray(bits) & 1, dtype=np.uint8)
+    c = lib().orc_crc16(b, len(b), 0)
+    return np.array([(c >> i) & 1 for i in range(15, -1, -1)])
+
+
+def check_crc(bits):
+    b = np.ascontiguousarray(np.asarray(bits) & 1, dtype=np.uint8)
+    return bool(lib().orc_check_crc(b, len(b)))
+
+
+def parse_burst_fields(symbols):
+    """parse_burst (protocol.py:192-244) -> (burst_type value, training_sequence, data_bits, crc_ok)."""
+    if len(symbols) < 255:
+        return None
+    s = np.asarray(symbols)[:255].astype(np.int64)
+    bits = np.stack([(s >> 1) & 1, s & 1], axis=1).reshape(-1)
+    w = bits[255:277]
+    corr = max(np.sum(w == SYNC_CONT) / 22, np.sum(w == SYNC_DISC) / 22)
+    if corr > 0.8:
+        btype, ts, data = 5, bits[108:130], bits
+    else:
+        btype, ts, data = 2, bits[108:122], np.concatenate([bits[0:108], bits[122:230]])
+    return btype, ts, data, check_crc(data)
+
+
+def decode_frames(symbols):
+    """Lower-MAC part of decode()/decode_frame() (decoder.py:835-888, 890-992)."""
+    bits, mapped = symbols_to_bits(symbols)
+    frames = []
+    for pos in decode_syncs(bits):
+        start = pos - 216
+        if start < 0 or start // 2 + 255 > len(mapped):
+            continue
+        fb = bits[start:start + 510]
+        f = dict(pos=pos, start=start, number=start // 510, nbits=len(fb))
+        if len(fb) >= 510:
+            btype, ts, data, ok = parse_burst_fields(mapped[start // 2:start // 2 + 255])
+            f.update(burst_type=btype, ts=ts, data=data, crc_ok=ok,
+                     header="".join(str(int(v)) for v in fb[:32]), pdu_type=int(fb[0] * 2 + fb[1]),
+                     enc_mode=int(fb[2] * 2 + fb[3]))
+        frames.append(f)
+    return frames

@@ -1,0 +1,308 @@
+#!/usr/bin/env python3
+"""Generate golden fixtures by running the REFERENCE itself (TEST INFRASTRUCTURE).
+
+Run in the build container only (the reference does not exist on the GPU box):
+
+    python tests/golden/make_golden.py            # writes tests/golden/*.npz
+
+The reference (/root/reference, read-only) is imported in this process with the oracle's
+``bitstring`` shim (oracle/shim/bitstring.py) on sys.path, because ``bitstring``
+(/root/reference/requirements.txt:5) is not installed.  Only inputs/outputs are stored.
+
+Fixtures:
+  g1_demod.npz   SignalProcessor.process + every intermediate (processor.py:221-273)
+  g2_decode.npz  symbols_to_bits / find_sync / decode cascade + frame slices (decoder.py:140-295,835-888)
+  g3_burst.npz   parse_burst / _check_crc / _calculate_crc16 (protocol.py:192-347)
+"""
+import json
+import os
+import sys
+import warnings
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = os.environ.get("TETRA_REFERENCE", "/root/reference")
+sys.path.insert(0, os.path.join(REPO, "oracle", "shim"))
+sys.path.insert(0, REF)
+sys.path.insert(0, HERE)
+
+import numpy as np  # noqa: E402
+import scipy  # noqa: E402
+from scipy import signal as ss  # noqa: E402
+
+from tetraear.signal.processor import SignalProcessor  # noqa: E402  (the reference)
+from tetraear.core.decoder import TetraDecoder  # noqa: E402
+from tetraear.core.protocol import TetraProtocolParser, BurstType  # noqa: E402
+
+import _signals  # noqa: E402
+
+warnings.simplefilter("ignore")
+AFC = 2.4e6 / 2048  # 1171.875 Hz, the AFC bin of /root/reference/tetraear/ui/modern.py:1956-1974
+
+
+def run_chain(fs, x, freq_offset):
+    """Reference process() with every intermediate (mirrors processor.py:239-273 call by call)."""
+    proc = SignalProcessor(sample_rate=fs)
+    out = {}
+    hard = proc.process(x, freq_offset=freq_offset)
+    out["hard"] = hard
+    out["symbols"] = proc.symbols
+    # intermediates, recomputed with the reference's own calls in the same order
+    samples = x
+    rate = fs
+    q = 0
+    dec_ok = 0
+    if len(samples) and rate > 240000 * 2:
+        q = int(rate / 240000)
+        if q > 1:
+            try:
+                samples = ss.decimate(samples, q)
+                rate = rate / q
+                dec_ok = 1
+            except Exception:
+                dec_ok = 0
+    out["decimated"] = samples
+    if freq_offset != 0 and len(x):
+        samples = proc.frequency_shift(samples, freq_offset, sample_rate=rate)
+    out["shifted"] = samples
+    filt = proc.filter_signal(samples, bandwidth=25000, sample_rate=rate) if len(x) else samples
+    out["filtered"] = filt
+    if len(x):   # process() short-circuits on empty input (processor.py:239-241)
+        sym = proc.extract_symbols(filt, sample_rate=rate)
+        assert np.array_equal(sym, out["symbols"]) and sym.dtype == out["symbols"].dtype, (fs, len(x))
+    else:
+        sym = out["symbols"]
+    assert np.array_equal(proc.demodulate_dqpsk(sym), hard)
+    out["q"] = q
+    out["dec_ok"] = dec_ok
+    return out
+
+
+def g1():
+    rng = np.random.default_rng(20260130)
+    cases = []
+    # full-size GUI chunks (modern.py:1919) at 2.4 MSps
+    for fam, off in (("tetra", 2 * AFC), ("noise", 0.0)):
+        cases.append((fam, 2.4e6, 131072, off))
+    for k, fam in enumerate(("tetra", "tetra_clean", "noise", "tone", "stress", "tetra", "tetra", "noise")):
+        cases.append((fam, 2.4e6, 16384, (k - 4) * AFC if k % 2 else 0.0))
+    cases += [("tetra", 1.8e6, 16384, 0.0), ("tetra", 1.8e6, 16384, -AFC),
+              ("tetra", 1.0e6, 16384, 3 * AFC), ("tetra", 240000.0, 4096, 0.0),
+              ("tetra", 240000.0, 4096, AFC), ("tetra", 20e6, 100000, 0.0)]
+    # edge cases: empty, 1 sample, decimate padlen failure (N<=27), filtfilt padlen failure
+    for n in (0, 1, 2, 27, 28, 150, 151, 152, 200, 1000, 1331, 1340):
+        cases.append(("noise", 2.4e6, n, 0.0 if n % 2 else AFC))
+    cases += [("noise", 240000.0, 15, 0.0), ("noise", 240000.0, 16, 0.0), ("noise", 240000.0, 40, AFC)]
+    arrays = {}
+    meta = []
+    for i, (fam, fs, n, off) in enumerate(cases):
+        x, iq = _signals.family(fam, rng, n, fs)
+        r = run_chain(fs, x, off)
+        arrays[f"c{i}_iq"] = iq
+        # full-size chunks keep only the stage boundaries that bound the fixture size
+        keys = ("hard", "symbols", "decimated") if n > 20000 else ("hard", "symbols", "decimated", "shifted", "filtered")
+        for key in keys:
+            arrays[f"c{i}_{key}"] = np.asarray(r[key])
+        meta.append(dict(family=fam, fs=fs, n=n, freq_offset=off, q=r["q"], dec_ok=r["dec_ok"],
+                         dtypes={k: str(np.asarray(r[k]).dtype) for k in
+                                 ("hard", "symbols", "decimated", "shifted", "filtered")}))
+    # direct method calls as the reference tests make them (test_signal_processor.py)
+    proc = SignalProcessor()
+    x128 = np.exp(1j * 0 * np.arange(6000)) + 0.1 * (rng.standard_normal(6000) + 1j * rng.standard_normal(6000))
+    arrays["direct_x128"] = x128
+    arrays["direct_filter_25k"] = proc.filter_signal(x128, bandwidth=25000)
+    arrays["direct_filter_50k"] = proc.filter_signal(x128, bandwidth=50000)
+    arrays["direct_demod"] = proc.demodulate_dqpsk(x128)
+    arrays["direct_extract"] = proc.extract_symbols(x128)
+    arrays["direct_extract_1M"] = proc.extract_symbols(x128, sample_rate=1.0e6)
+    arrays["direct_shift_1k"] = proc.frequency_shift(x128, 1000)
+    return arrays, meta
+
+
+def crafted_streams(rng):
+    """Hard-symbol streams with training sequences planted at chosen quality levels."""
+    streams = []
+    for level in (22, 21, 20, 19, 18, 17, 16, 15):
+        for k in range(3):
+            n = int(rng.integers(600, 2200))
+            sym = rng.integers(0, 4, n).astype(np.uint8)
+            bits = np.stack([(sym >> 1) & 1, sym & 1], axis=1).reshape(-1)
+            npl = int(rng.integers(1, 6))
+            for _ in range(npl):
+                pos = int(rng.integers(0, len(bits) - 22))
+                pat = _signals.TS_N if rng.integers(0, 2) else _signals.TS_P
+                w = pat.copy()
+                flip = rng.choice(22, 22 - level, replace=False)
+                w[flip] ^= 1
+                bits[pos:pos + 22] = w
+            sym = (bits[0::2] << 1 | bits[1::2]).astype(np.uint8)
+            streams.append(sym)
+    # regular burst-aligned stream: TS at bit 216 of each 510-bit slot (decoder.py:863-865)
+    n = 4 * 255 + 40
+    bits = rng.integers(0, 2, 2 * n).astype(np.uint8)
+    for s in range(4):
+        bits[s * 510 + 216 + 40:s * 510 + 216 + 40 + 22] = _signals.TS_N
+    streams.append((bits[0::2] << 1 | bits[1::2]).astype(np.uint8))
+    # odd start position (start//2 misalignment, decoder.py:870-877)
+    bits = rng.integers(0, 2, 2 * n).astype(np.uint8)
+    bits[217 + 101:217 + 101 + 22] = _signals.TS_N
+    streams.append((bits[0::2] << 1 | bits[1::2]).astype(np.uint8))
+    # start+510 == 2S+1 edge: 509 frame bits -> decode_frame returns None (decoder.py:894)
+    S = 400
+    bits = rng.integers(0, 2, 2 * S).astype(np.uint8)
+    start = 2 * S + 1 - 510
+    bits[start + 216:start + 238] = _signals.TS_N
+    streams.append((bits[0::2] << 1 | bits[1::2]).astype(np.uint8))
+    streams.append(np.zeros(0, np.uint8))
+    streams.append(rng.integers(0, 4, 10).astype(np.uint8))
+    streams.append(rng.integers(0, 8, 700).astype(np.uint8))  # 8-PSK branch (decoder.py:158-164)
+    return streams
+
+
+def decode_record(dec, sym):
+    """decode() with its internal cascade exposed (decoder.py:835-888)."""
+    rec = {}
+    bits, mapped = dec.symbols_to_bits(sym)
+    rec["bits"] = bits
+    rec["mapped"] = mapped
+    for thr in (0.9, 0.85, 0.8, 0.75, 0.7):
+        p, mc = dec.find_sync(bits, threshold=thr, return_max_corr=True)
+        rec[f"fs_{thr}"] = (list(map(int, p)), float(mc))
+    sp, mc = dec.find_sync(bits, threshold=0.90, return_max_corr=True)
+    if not sp:
+        sp, mc = dec.find_sync(bits, threshold=0.85, return_max_corr=True)
+        if not sp:
+            sp, mc = dec.find_sync(bits, threshold=0.80, return_max_corr=True)
+            if not sp and mc >= 0.75:
+                sp, _ = dec.find_sync(bits, threshold=max(0.75, mc - 0.02), return_max_corr=True)
+    rec["syncs"] = list(map(int, sp))
+    frames = []
+    parser = TetraProtocolParser()
+    for pos in sp:
+        start = pos - 216
+        if start < 0:
+            continue
+        if start // 2 + 255 > len(mapped):
+            continue
+        fb = bits[start:start + 510]
+        fsym = mapped[start // 2:start // 2 + 255]
+        f = dict(pos=int(pos), start=int(start), number=int(start // 510), nbits=int(len(fb)))
+        if len(fb) >= 510:
+            b = parser.parse_burst(fsym, slot_number=(start // 510) % 4)
+            f.update(burst_type=b.burst_type.name, crc_ok=bool(b.crc_ok),
+                     ts=b.training_sequence.astype(np.uint8).tolist(),
+                     data=np.asarray(b.data_bits).astype(np.uint8).tolist(),
+                     header="".join(str(int(v)) for v in fb[:32]))
+        frames.append(f)
+    rec["frames"] = frames
+    out = dec.decode(sym)
+    rec["decoded"] = [dict(number=f["number"], timeslot=f["timeslot"], type=f["type"], header=f["header"],
+                           position=f["position"], burst_crc=f.get("burst_crc")) for f in out]
+    rec["stats"] = dict(dec.protocol_parser.stats)
+    return rec
+
+
+def g2(g1_arrays, g1_meta):
+    rng = np.random.default_rng(7)
+    streams = crafted_streams(rng)
+    for i, m in enumerate(g1_meta):
+        if len(g1_arrays[f"c{i}_hard"]) >= 255:
+            streams.append(g1_arrays[f"c{i}_hard"])
+    arrays = {}
+    recs = []
+    for i, sym in enumerate(streams):
+        dec = TetraDecoder(auto_decrypt=False)
+        r = decode_record(dec, sym)
+        arrays[f"s{i}_sym"] = np.asarray(sym)
+        arrays[f"s{i}_bits"] = np.asarray(r.pop("bits"))
+        arrays[f"s{i}_mapped"] = np.asarray(r.pop("mapped"))
+        recs.append(r)
+    return arrays, recs
+
+
+def g3():
+    rng = np.random.default_rng(11)
+    p = TetraProtocolParser()
+    arrays = {}
+    # CRC KAT: "123456789" MSB-first -> 0x29B1 (CRC-16/CCITT-FALSE, protocol.py:331-347)
+    kat = np.array([(b >> (7 - k)) & 1 for b in b"123456789" for k in range(8)])
+    arrays["kat_crc"] = p._calculate_crc16(kat)
+    L = 216
+    vecs, crcs, checks = [], [], []
+    for k in range(256):
+        v = rng.integers(0, 2, L)
+        mode = k % 8
+        if mode in (1, 2, 3, 4):      # valid CRC with 0..3 flipped CRC bits
+            v[-16:] = p._calculate_crc16(v[:-16])
+            for j in rng.choice(16, mode - 1, replace=False):
+                v[L - 16 + j] ^= 1
+        elif mode == 5:               # reversed-payload CRC (protocol.py:319-325)
+            v[-16:] = p._calculate_crc16(v[:-16][::-1])
+            if k % 16 == 5:
+                v[L - 16 + int(rng.integers(0, 16))] ^= 1
+        elif mode == 6:
+            v[:] = 0 if k % 16 == 6 else 1   # all-equal rejection (protocol.py:301-304)
+        vecs.append(v)
+        crcs.append(p._calculate_crc16(v))
+        checks.append(bool(p._check_crc(v)))
+    arrays["crc_vecs"] = np.array(vecs, np.uint8)
+    arrays["crc_of_vecs"] = np.array(crcs, np.uint8)
+    arrays["check_crc"] = np.array(checks, np.bool_)
+    # 510-bit (sync burst) and short lengths
+    v510 = rng.integers(0, 2, (16, 510))
+    arrays["crc510_vecs"] = v510.astype(np.uint8)
+    arrays["check510"] = np.array([bool(p._check_crc(v)) for v in v510])
+    arrays["crc_short"] = np.array([bool(p._check_crc(np.ones(n, int))) for n in range(0, 20)])
+    # parse_burst on crafted 255-symbol vectors
+    bursts = []
+    for k in range(64):
+        s = rng.integers(0, 4, 255 + (k % 3))
+        if k % 4 == 0:   # sync-burst pattern at bits 255:277 (protocol.py:249)
+            bits = np.stack([(s >> 1) & 1, s & 1], 1).reshape(-1)
+            pat = p.SYNC_CONTINUOUS_DOWNLINK if k % 8 == 0 else p.SYNC_DISCONTINUOUS_DOWNLINK
+            bits[255:277] = pat
+            for j in rng.choice(22, int(k % 5), replace=False):
+                bits[255 + j] ^= 1
+            s = (bits[0::2] << 1) | bits[1::2]
+        if k % 4 == 1:   # valid normal-burst CRC
+            bits = np.stack([(s >> 1) & 1, s & 1], 1).reshape(-1)
+            data = np.concatenate([bits[0:108], bits[122:230]])
+            data[-16:] = p._calculate_crc16(data[:-16])
+            bits[122:230] = data[108:]
+            s = (bits[0::2] << 1) | bits[1::2]
+        bursts.append(s)
+    types, tss, datas, oks = [], [], [], []
+    for s in bursts:
+        b = p.parse_burst(np.asarray(s), slot_number=1)
+        types.append(b.burst_type.value)
+        tss.append(np.pad(np.asarray(b.training_sequence), (0, 22 - len(b.training_sequence)), constant_values=255))
+        d = np.asarray(b.data_bits)
+        datas.append(np.pad(d, (0, 510 - len(d)), constant_values=255))
+        oks.append(bool(b.crc_ok))
+    arrays["burst_syms"] = np.array([np.pad(s, (0, 2 - (len(s) - 255)), constant_values=0) for s in bursts])
+    arrays["burst_len"] = np.array([len(s) for s in bursts])
+    arrays["burst_type"] = np.array(types)
+    arrays["burst_ts"] = np.array(tss, np.uint8)
+    arrays["burst_data"] = np.array(datas, np.uint8)
+    arrays["burst_crc_ok"] = np.array(oks)
+    arrays["burst_stats"] = np.array([p.stats["total_bursts"], p.stats["crc_pass"], p.stats["crc_fail"]])
+    assert BurstType.Synchronization.value == 5
+    return arrays
+
+
+def main():
+    info = dict(numpy=np.__version__, scipy=scipy.__version__, reference=REF,
+                note="generated by tests/golden/make_golden.py from the reference itself")
+    a1, m1 = g1()
+    np.savez_compressed(os.path.join(HERE, "g1_demod.npz"), **a1)
+    a2, r2 = g2(a1, m1)
+    np.savez_compressed(os.path.join(HERE, "g2_decode.npz"), **a2)
+    a3 = g3()
+    np.savez_compressed(os.path.join(HERE, "g3_burst.npz"), **a3)
+    with open(os.path.join(HERE, "golden_meta.json"), "w") as f:
+        json.dump(dict(info=info, g1=m1, g2=r2), f, indent=0)
+    print("wrote", len(m1), "demod cases,", len(r2), "decode streams")
+
+
+if __name__ == "__main__":
+    main()
