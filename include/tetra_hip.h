@@ -1,0 +1,170 @@
+/*
+ * tetra_hip.h -- C ABI of libtetra_hip.so, the MI355X (gfx950) TETRA receive hot path.
+ *
+ * Drop-in boundary for the reference's demod + lower-MAC path (WizzardDr/TetraEar-BladeRF):
+ *   tetraear/signal/processor.py  SignalProcessor            (processor.py:18-273)
+ *   tetraear/core/decoder.py      TetraDecoder lower MAC      (decoder.py:140-295, 835-888)
+ *   tetraear/core/protocol.py     parse_burst / CRC           (protocol.py:192-347)
+ * plus the ETSI EN 300 392-2 receive chain the reference lacks (BASELINE.json north_star):
+ *   polyphase FIR channel filter/resampler, RRC matched filter, Gardner timing recovery,
+ *   differential decision with soft bits, descrambler, block deinterleaver, RCPC depuncture,
+ *   K=5 rate-1/4 Viterbi, CRC-16.
+ *
+ * Conventions
+ *   - Every entry point returns 0 on success or a negative TETRA_E* code; nothing aborts.
+ *     tetra_last_error() returns the message of the last failure on that context.
+ *   - Array arguments may be HOST or DEVICE pointers (the library asks HIP which); host arrays
+ *     are staged through context-owned device buffers.  Calls with device arguments enqueue on
+ *     the context's stream and return without waiting; calls that touch host memory return
+ *     after their results are in host memory.
+ *   - Complex arrays are interleaved (re, im).  "cf32" = complex64, "cf64" = complex128.
+ *   - One context per host thread; a context is not thread-safe.  No allocation happens on a
+ *     repeat call with sizes no larger than a previous call (workspaces are cached).
+ */
+#ifndef TETRA_HIP_H
+#define TETRA_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TETRA_ABI_VERSION 1
+
+enum {
+    TETRA_OK = 0,
+    TETRA_E_INVALID = -1,   /* bad argument */
+    TETRA_E_HIP = -2,       /* HIP runtime error */
+    TETRA_E_NODEVICE = -3,  /* no usable gfx950 device */
+    TETRA_E_NOMEM = -4
+};
+
+/* Sample formats of input arrays. */
+enum { TETRA_CF32 = 0, TETRA_CF64 = 1 };
+
+typedef struct tetra_ctx tetra_ctx;
+
+int tetra_abi_version(void);
+/* Create a context on HIP device `device`; NULL on failure (see tetra_last_error(NULL)). */
+tetra_ctx *tetra_create(int device);
+void tetra_destroy(tetra_ctx *ctx);
+const char *tetra_last_error(const tetra_ctx *ctx);
+/* The context's hipStream_t; tetra_set_stream() makes the context enqueue on a caller stream. */
+void *tetra_get_stream(tetra_ctx *ctx);
+int tetra_set_stream(tetra_ctx *ctx, void *hip_stream);
+int tetra_synchronize(tetra_ctx *ctx);
+/* Device name / arch of the context's device (e.g. "gfx950"). */
+int tetra_device_arch(tetra_ctx *ctx, char *buf, size_t n);
+
+/* =====================================================================================
+ * Compat demod -- bit-compatible with SignalProcessor (processor.py:221-273)
+ * ===================================================================================== */
+
+/* Filter design and control decisions are made by the host (the same scipy.signal design calls
+ * the reference makes: cheby1/sosfilt_zi for decimate, butter/lfilter_zi for filter_signal);
+ * the plan carries them to the device.  Field-by-field:                                     */
+typedef struct tetra_compat_plan {
+    int32_t q;            /* decimation factor (processor.py:249); <= 1: decimation stage skipped */
+    int32_t dec_f64;      /* 0: decimate in complex64 arithmetic (cf32 input), 1: complex128 */
+    int32_t filt;         /* 1: filtfilt runs (len > padlen 15); 0: filter_signal returned input */
+    int32_t ntaps;        /* butter(4) -> 5 */
+    int32_t sps;          /* int(rate/18000) (processor.py:183) */
+    int32_t phase_step;   /* max(1, sps//8) (processor.py:194) */
+    int32_t reserved[2];
+    double fs_dec;        /* sample rate after decimation: time base of frequency_shift */
+    float sos_f32[24];    /* cheby1(8, 0.05, 0.8/q) SOS [4][6] as complex64 real parts */
+    float zi_f32[8];      /* sosfilt_zi in complex64 */
+    double sos_f64[24];
+    double zi_f64[8];
+    double b[8], a[8];    /* butter(4, cutoff) */
+    double lzi[8];        /* lfilter_zi(b, a) */
+    double thr[4];        /* -5*pi/8, -3*pi/8, 3*pi/8, 5*pi/8 as Python evaluates them */
+} tetra_compat_plan;
+
+/* Fused process() over a batch of C equal-length chunks.
+ *   iq        [C][N] complex, format iq_fmt (TETRA_CF32 for SC16-derived capture data)
+ *   mix_c     [C] imaginary part of (-1j*2*pi*freq_offset) per channel (processor.py:98-99)
+ *   mix_on    [C] 1 where freq_offset != 0 (processor.py:260)
+ *   soft      [C][smax] complex128: the `.symbols` attribute (processor.py:268)
+ *   hard      [C][smax] uint8: process() return value; hard count = max(0, nsym-1)
+ *   nsym      [C] number of soft symbols per channel
+ *   soft_f32  set to 1 when `.symbols` is complex64 in the reference (no filter, no mixer)
+ * smax must be >= the symbol count the plan implies (tetra_compat_symbols()). */
+int tetra_demod_compat(tetra_ctx *ctx, const tetra_compat_plan *plan, const void *iq, int iq_fmt,
+                       size_t C, size_t N, const double *mix_c, const uint8_t *mix_on,
+                       void *soft, uint8_t *hard, int32_t *nsym, size_t smax, int32_t *soft_f32);
+/* Number of soft symbols process() yields for N input samples under `plan`. */
+int64_t tetra_compat_symbols(const tetra_compat_plan *plan, size_t N);
+
+/* Component entry points, one per SignalProcessor method (each over C rows of length N). */
+/* scipy.signal.decimate(x, q) as called at processor.py:254: out [C][ceil(N/q)] in iq_fmt. */
+int tetra_decimate(tetra_ctx *ctx, const tetra_compat_plan *plan, const void *iq, int iq_fmt,
+                   size_t C, size_t N, void *out);
+/* frequency_shift (processor.py:85-100): out [C][N] complex128. */
+int tetra_frequency_shift(tetra_ctx *ctx, const void *iq, int iq_fmt, size_t C, size_t N,
+                          const double *mix_c, double fs, void *out);
+/* filter_signal's filtfilt (processor.py:78-79): out [C][N] complex128; needs N > 3*ntaps. */
+int tetra_filtfilt(tetra_ctx *ctx, const tetra_compat_plan *plan, const void *iq, int iq_fmt,
+                   size_t C, size_t N, void *out);
+/* extract_symbols (processor.py:168-219): sym [C][smax] in iq_fmt, nsym [C], best phase [C]. */
+int tetra_extract_symbols(tetra_ctx *ctx, const void *x, int fmt, size_t C, size_t N, int sps,
+                          int phase_step, void *sym, int32_t *nsym, int32_t *best_phase, size_t smax);
+/* demodulate_dqpsk (processor.py:102-166): hard [C][S-1] for C rows of S symbols. */
+int tetra_demod_dqpsk(tetra_ctx *ctx, const void *sym, int fmt, size_t C, size_t S,
+                      const double *thr4, uint8_t *hard);
+
+/* =====================================================================================
+ * Compat lower MAC -- TetraDecoder.decode / find_sync / parse_burst (decoder.py, protocol.py)
+ * ===================================================================================== */
+
+#define TETRA_MAX_SYNC 16
+/* Per-sync record written by tetra_lmac_compat (int32 fields). */
+enum {
+    TETRA_F_POS = 0,      /* sync position (bit index of the training sequence) */
+    TETRA_F_START,        /* pos - 216 (decoder.py:865) */
+    TETRA_F_VALID,        /* 1 if the frame is sliced (start >= 0 and start//2+255 <= S) */
+    TETRA_F_NBITS,        /* len(bits[start:start+510]) (decoder_frame needs 510) */
+    TETRA_F_NUMBER,       /* start // 510 (decoder.py:881) */
+    TETRA_F_BTYPE,        /* BurstType value: 2 NormalDownlink, 5 Synchronization */
+    TETRA_F_CRC,          /* parse_burst crc_ok */
+    TETRA_F_HDR,          /* (pdu_type << 2) | encryption_mode (decoder.py:906-909) */
+    TETRA_F_FIELDS = 8
+};
+
+/* Batched decode() lower MAC for C symbol streams.
+ *   sym       [C][stride] int64 symbols (0..3, or 0..7 for the 8-PSK branch)
+ *   nsym      [C] stream lengths
+ *   k_of_max  [23] sync count threshold as a function of the stream's best correlation count,
+ *             -1 for "no sync" (the 0.90/0.85/0.80/adaptive cascade, decoder.py:845-857,
+ *             tabulated by the host)
+ *   nsync     [C]; rec [C][TETRA_MAX_SYNC][TETRA_F_FIELDS]
+ *   frame_bits[C][TETRA_MAX_SYNC][510] = bits[start:start+510]  (decode_frame 'bits')
+ *   burst_bits[C][TETRA_MAX_SYNC][510] = bits of mapped[start//2:+255] (parse_burst input)  */
+int tetra_lmac_compat(tetra_ctx *ctx, const int64_t *sym, const int32_t *nsym, size_t C, size_t stride,
+                      const int8_t *k_of_max, int32_t *nsync, int32_t *rec, uint8_t *frame_bits,
+                      uint8_t *burst_bits);
+/* symbols_to_bits (decoder.py:140-169): bits [2S] int64, mapped [S] int64. */
+int tetra_symbols_to_bits(tetra_ctx *ctx, const int64_t *sym, size_t S, int64_t *bits, int64_t *mapped);
+/* find_sync main scan (decoder.py:226-259) at integer count threshold kthr:
+ * pos [maxpos], *npos hits, *maxc = max evaluated correlation count. */
+int tetra_find_sync(tetra_ctx *ctx, const uint8_t *bits, size_t nbits, int kthr, int64_t *pos,
+                    int maxpos, int32_t *npos, int32_t *maxc);
+/* Pattern match counts (the np.sum(window == pattern) of decoder.py:239 / protocol.py:262):
+ * counts[f] = #{j < 22 : bits[f][offset+j] == pattern22[j]} over F rows of L bytes. */
+int tetra_match_count(tetra_ctx *ctx, const uint8_t *bits, size_t F, size_t L, const uint8_t *pattern22,
+                      size_t offset, int32_t *counts);
+/* parse_burst over F bursts of 255 symbols (protocol.py:192-244): btype [F], crc_ok [F],
+ * bits [F][510] burst bits (training sequence/data are slices of these). */
+int tetra_parse_bursts(tetra_ctx *ctx, const int64_t *sym, size_t F, int32_t *btype, uint8_t *crc_ok,
+                       uint8_t *bits);
+/* _calculate_crc16 over F rows of L bits (reversed != 0: payload reversed): crc [F]. */
+int tetra_crc16(tetra_ctx *ctx, const uint8_t *bits, size_t F, size_t L, int reversed, uint16_t *crc);
+/* _check_crc over F rows of L bits: ok [F]. */
+int tetra_check_crc(tetra_ctx *ctx, const uint8_t *bits, size_t F, size_t L, uint8_t *ok);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TETRA_HIP_H */

@@ -1,0 +1,70 @@
+// common.h -- shared plumbing for libtetra_hip.so (context, errors, host/device staging).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <type_traits>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/tetra_hip.h"
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+// Workspace slots owned by a context (grown on demand, never shrunk).
+enum Slot {
+    S_IN0 = 0, S_IN1, S_IN2, S_IN3, S_IN4, S_IN5,          // staged host inputs
+    S_OUT0, S_OUT1, S_OUT2, S_OUT3, S_OUT4, S_OUT5,        // staged host outputs
+    S_W0, S_W1, S_W2, S_W3, S_W4, S_W5, S_W6, S_W7,        // kernel workspaces
+    S_COUNT
+};
+
+struct tetra_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = true;
+    std::string err;
+    DevBuf slot[S_COUNT];
+    char arch[64] = {0};
+};
+
+extern thread_local std::string g_tetra_err;
+
+int tetra_fail(tetra_ctx *ctx, int code, const char *fmt, ...);
+
+#define HIP_TRY(ctx, expr)                                                                         \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return tetra_fail((ctx), TETRA_E_HIP, "%s failed: %s (%s:%d)", #expr,                   \
+                              hipGetErrorString(e_), __FILE__, __LINE__);                          \
+    } while (0)
+
+// Returns device-side workspace of >= bytes in slot s (nullptr on failure, error set).
+void *ws(tetra_ctx *ctx, int s, size_t bytes);
+bool is_device_ptr(const void *p);
+
+// Host/device argument staging.  `in` returns a device pointer holding the bytes of p;
+// `out` returns a device pointer whose contents are copied back to p by finish().
+struct Staging {
+    tetra_ctx *ctx;
+    int next_in = S_IN0, next_out = S_OUT0;
+    struct Back { void *host; const void *dev; size_t bytes; };
+    std::vector<Back> back;
+    bool host_touched = false;
+    bool failed = false;
+    explicit Staging(tetra_ctx *c) : ctx(c) {}
+    const void *in(const void *p, size_t bytes);
+    void *out(void *p, size_t bytes);
+    int finish();   // D2H copies (if any) + stream sync when host memory was involved
+};
+
+static inline unsigned grid_for(size_t threads, unsigned block) {
+    return (unsigned)((threads + block - 1) / block);
+}

@@ -1,0 +1,659 @@
+// compat_demod.hip -- SignalProcessor.process on gfx950, bit-compatible with the reference.
+//
+// Reference path (/root/reference/tetraear/signal/processor.py:221-273):
+//   scipy.signal.decimate(x, q)      cheby1(8,0.05,0.8/q) SOS, sosfiltfilt (odd pad 27)   :254
+//   frequency_shift                   x * exp(-j*2*pi*f*n/fs)                              :85-100
+//   filter_signal                     butter(4) + filtfilt (odd pad 15), complex128        :51-83
+//   extract_symbols                   best integer phase by mean |x|^2, then gather       :168-219
+//   demodulate_dqpsk                  normalise, differential phase, shifted thresholds   :102-166
+//
+// Numerics: every recursion restates the operation order of scipy's compiled loops (no FMA
+// contraction: built with -ffp-contract=off), and the vector math follows numpy's kernels on
+// x86-64 (complex multiply fma(a,c,-(b*d)) / fma(a,d,b*c); |z| = max*sqrt(fma(r,r,1)),
+// pairwise summation for np.mean).  Only sin/cos (mixer) and atan2 (decision) come from a
+// different libm, i.e. they can differ from the CPU by an ulp.
+//
+// Parallel layout: IIR recursions are sequential in time, so one lane owns one real component
+// of one channel ("lane = (channel, re|im)"); channels batch across lanes.  Per-lane streams
+// live in a "grouped" layout [C/32][time][32 channels][re,im] so the 64 lanes of a wave touch
+// 64 consecutive scalars per time step (coalesced).
+#include "common.h"
+
+namespace {
+
+// Strided view of complex rows: element (ch, n) real part at base[off(ch, n)], imag at +1.
+struct Lay {
+    size_t s_grp, s_n, s_lane;
+    __host__ __device__ size_t off(int ch, long n) const {
+        return (size_t)(ch >> 5) * s_grp + (size_t)n * s_n + (size_t)(ch & 31) * s_lane;
+    }
+};
+static Lay row_major(long len) { return Lay{(size_t)64 * len, 2, (size_t)2 * len}; }
+static Lay grouped(long len) { return Lay{(size_t)64 * len, 64, 2}; }
+static size_t grouped_elems(int C, long len) { return (size_t)((C + 31) / 32) * 64 * (size_t)len; }
+
+constexpr int NSEC = 4;   // decimate's cheby1(8) -> 4 second-order sections
+
+// ------------------------------------------------------------------ decimator (sosfiltfilt)
+template <typename T>
+__device__ __forceinline__ T sos_step(const T (&c)[NSEC * 6], T (&z)[NSEC * 2], T xc) {
+#pragma unroll
+    for (int s = 0; s < NSEC; ++s) {
+        // scipy _sosfilt: x_new = b0*x + z0; z0 = (b1*x - a1*x_new) + z1; z1 = b2*x - a2*x_new
+        T xn = c[6 * s + 0] * xc + z[2 * s];
+        z[2 * s] = (c[6 * s + 1] * xc - c[6 * s + 4] * xn) + z[2 * s + 1];
+        z[2 * s + 1] = c[6 * s + 2] * xc - c[6 * s + 5] * xn;
+        xc = xn;
+    }
+    return xc;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_sos_fwd(const T *__restrict__ x, Lay lx, int C, long N, int pad,
+                                                 const T *__restrict__ sos, const T *__restrict__ zi,
+                                                 T *__restrict__ scr, Lay ls) {
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ch = gid >> 1, comp = gid & 1;
+    if (ch >= C) return;
+    T c[NSEC * 6], z[NSEC * 2];
+#pragma unroll
+    for (int i = 0; i < NSEC * 6; ++i) c[i] = sos[i];
+    const T *xp = x + lx.off(ch, 0) + comp;
+    const size_t sx = lx.s_n;
+    const T two = 2, x0 = xp[0], xl = xp[(size_t)(N - 1) * sx];
+    // odd extension (scipy _arraytools.odd_ext): ext[j] = 2*x0 - x[pad-j] (j<pad), x[j-pad],
+    // 2*x[N-1] - x[N-2-(j-pad-N)] (j >= pad+N)
+    const T e0 = two * x0 - xp[(size_t)pad * sx];
+#pragma unroll
+    for (int i = 0; i < NSEC * 2; ++i) z[i] = zi[i] * e0;
+    T *sp = scr + ls.off(ch, 0) + comp;
+    const size_t ss = ls.s_n;
+    long j = 0;
+    for (; j < pad; ++j) sp[(size_t)j * ss] = sos_step(c, z, two * x0 - xp[(size_t)(pad - j) * sx]);
+    for (long n = 0; n < N; ++n, ++j) sp[(size_t)j * ss] = sos_step(c, z, xp[(size_t)n * sx]);
+    for (long k = 0; k < pad; ++k, ++j) sp[(size_t)j * ss] = sos_step(c, z, two * xl - xp[(size_t)(N - 2 - k) * sx]);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_sos_bwd(const T *__restrict__ scr, Lay ls, int C, long N, int pad, int q,
+                                                 const T *__restrict__ sos, const T *__restrict__ zi,
+                                                 T *__restrict__ out, Lay lo) {
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ch = gid >> 1, comp = gid & 1;
+    if (ch >= C) return;
+    T c[NSEC * 6], z[NSEC * 2];
+#pragma unroll
+    for (int i = 0; i < NSEC * 6; ++i) c[i] = sos[i];
+    const T *sp = scr + ls.off(ch, 0) + comp;
+    const size_t ss = ls.s_n;
+    const long L = N + 2 * pad;
+    const T y0 = sp[(size_t)(L - 1) * ss];
+#pragma unroll
+    for (int i = 0; i < NSEC * 2; ++i) z[i] = zi[i] * y0;
+    T *op = out + lo.off(ch, 0) + comp;
+    const size_t so = lo.s_n;
+    long j = L - 1;
+    for (; j >= pad + N; --j) sos_step(c, z, sp[(size_t)j * ss]);
+    // output y[t] for t = j - pad with t % q == 0 (decimate's y[::q])
+    long t = N - 1;
+    int cnt = (int)(t % q);
+    for (; t >= 0; --t, --j) {
+        T v = sos_step(c, z, sp[(size_t)j * ss]);
+        if (cnt == 0) {
+            op[(size_t)(t / q) * so] = v;
+            cnt = q;
+        }
+        --cnt;
+    }
+    for (; j >= 0; --j) sos_step(c, z, sp[(size_t)j * ss]);
+}
+
+// ------------------------------------------------------------------ mixer + filtfilt (lfilter)
+// Value of component `comp` of (possibly frequency-shifted) sample n, in double.
+template <typename TIn>
+__device__ __forceinline__ double mixed_val(const TIn *xp, size_t sx, long n, int comp, bool mix, double c,
+                                            double fs) {
+    const double xr = (double)xp[(size_t)n * sx], xi = (double)xp[(size_t)n * sx + 1];
+    if (!mix) return comp ? xi : xr;
+    // numpy: t = arange/fs; arg = (-1j*2*pi*f)*t has real part 0, imag c*t; exp(arg) = (cos, sin)
+    const double th = c * ((double)n / fs);
+    double s, co;
+    sincos(th, &s, &co);
+    // numpy SIMD complex multiply: re = fma(xr, sr, -(xi*si)), im = fma(xr, si, xi*sr)
+    return comp ? fma(xr, s, xi * co) : fma(xr, co, -(xi * s));
+}
+
+// Odd-extended input of filtfilt at ext index j.  The extension is computed in the precision of
+// the array filtfilt receives: complex128 when mixed, else the input type (complex64 from
+// decimate), then promoted to double (scipy lfilter runs in complex128).
+template <typename TIn>
+__device__ __forceinline__ double lf_ext(const TIn *xp, size_t sx, long M, int pad, long j, int comp, bool mix,
+                                         double c, double fs) {
+    long n;
+    int side;
+    if (j < pad) { n = pad - j; side = -1; }
+    else if (j < pad + M) { n = j - pad; side = 0; }
+    else { n = M - 2 - (j - pad - M); side = 1; }
+    if (mix) {
+        const double v = mixed_val(xp, sx, n, comp, true, c, fs);
+        if (side == 0) return v;
+        const double e = mixed_val(xp, sx, side < 0 ? 0 : M - 1, comp, true, c, fs);
+        return 2.0 * e - v;
+    }
+    const TIn v = xp[(size_t)n * sx + comp];
+    if (side == 0) return (double)v;
+    const TIn e = xp[(size_t)(side < 0 ? 0 : M - 1) * sx + comp];
+    return (double)((TIn)2 * e - v);
+}
+
+constexpr int MAXTAP = 8;
+
+template <typename TIn>
+__global__ __launch_bounds__(256) void k_lf_fwd(const TIn *__restrict__ x, Lay lx, int C, long M, int pad, int nt,
+                                                const double *__restrict__ b, const double *__restrict__ a,
+                                                const double *__restrict__ zi, const double *__restrict__ mixc,
+                                                const uint8_t *__restrict__ mixon, double fs,
+                                                double *__restrict__ scr, Lay ls) {
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ch = gid >> 1, comp = gid & 1;
+    if (ch >= C) return;
+    double bb[MAXTAP], aa[MAXTAP], z[MAXTAP];
+    for (int k = 0; k < nt; ++k) { bb[k] = b[k]; aa[k] = a[k]; }
+    const bool mix = mixon && mixon[ch];
+    const double c = mix ? mixc[ch] : 0.0;
+    const TIn *xp = x + lx.off(ch, 0);
+    const size_t sx = lx.s_n;
+    const long L = M + 2 * pad;
+    const double e0 = lf_ext(xp, sx, M, pad, 0, comp, mix, c, fs);
+    for (int k = 0; k < nt - 1; ++k) z[k] = zi[k] * e0;
+    double *sp = scr + ls.off(ch, 0) + comp;
+    const size_t ss = ls.s_n;
+    for (long j = 0; j < L; ++j) {
+        const double xn = lf_ext(xp, sx, M, pad, j, comp, mix, c, fs);
+        // scipy lfilter (DF-II-T): y = z0 + b0*x; z_k = (z_{k+1} + x*b_{k+1}) - y*a_{k+1}
+        const double yn = z[0] + bb[0] * xn;
+#pragma unroll
+        for (int k = 0; k < MAXTAP - 2; ++k)
+            if (k < nt - 2) z[k] = (z[k + 1] + xn * bb[k + 1]) - yn * aa[k + 1];
+        // last delay
+#pragma unroll
+        for (int k = 0; k < MAXTAP - 1; ++k)
+            if (k == nt - 2) z[k] = xn * bb[k + 1] - yn * aa[k + 1];
+        sp[(size_t)j * ss] = yn;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_lf_bwd(const double *__restrict__ scr, Lay ls, int C, long M, int pad, int nt,
+                                                const double *__restrict__ b, const double *__restrict__ a,
+                                                const double *__restrict__ zi, double *__restrict__ out, Lay lo) {
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ch = gid >> 1, comp = gid & 1;
+    if (ch >= C) return;
+    double bb[MAXTAP], aa[MAXTAP], z[MAXTAP];
+    for (int k = 0; k < nt; ++k) { bb[k] = b[k]; aa[k] = a[k]; }
+    const double *sp = scr + ls.off(ch, 0) + comp;
+    const size_t ss = ls.s_n;
+    const long L = M + 2 * pad;
+    const double y0 = sp[(size_t)(L - 1) * ss];
+    for (int k = 0; k < nt - 1; ++k) z[k] = zi[k] * y0;
+    double *op = out + lo.off(ch, 0) + comp;
+    const size_t so = lo.s_n;
+    for (long j = L - 1; j >= 0; --j) {
+        const double xn = sp[(size_t)j * ss];
+        const double yn = z[0] + bb[0] * xn;
+#pragma unroll
+        for (int k = 0; k < MAXTAP - 2; ++k)
+            if (k < nt - 2) z[k] = (z[k + 1] + xn * bb[k + 1]) - yn * aa[k + 1];
+#pragma unroll
+        for (int k = 0; k < MAXTAP - 1; ++k)
+            if (k == nt - 2) z[k] = xn * bb[k + 1] - yn * aa[k + 1];
+        const long t = j - pad;
+        if (t >= 0 && t < M) op[(size_t)t * so] = yn;
+    }
+}
+
+// frequency_shift alone (component API, and the unfiltered-but-shifted process() path).
+template <typename TIn>
+__global__ __launch_bounds__(256) void k_mix(const TIn *__restrict__ x, Lay lx, int C, long N,
+                                             const double *__restrict__ mixc, const uint8_t *__restrict__ mixon,
+                                             double fs, double *__restrict__ out, Lay lo) {
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int ch = (int)(gid / N);
+    const long n = gid - (long)ch * N;
+    if (ch >= C) return;
+    const bool mix = !mixon || mixon[ch];
+    const TIn *xp = x + lx.off(ch, 0);
+    double *op = out + lo.off(ch, n);
+    op[0] = mixed_val(xp, lx.s_n, n, 0, mix, mixc[ch], fs);
+    op[1] = mixed_val(xp, lx.s_n, n, 1, mix, mixc[ch], fs);
+}
+
+// ------------------------------------------------------------------ extract_symbols
+// numpy complex |z| (SIMD kernel): larger*sqrt(fma(r, r, 1)), r = smaller/larger.
+template <typename T>
+__device__ __forceinline__ T np_cabs(T xr, T xi) {
+    T re = fabs(xr), im = fabs(xi);
+    const T inf = (T)INFINITY;
+    const bool re_inf = re == inf, im_inf = im == inf;
+    im = re_inf ? inf : im;
+    re = im_inf ? inf : re;
+    const bool re_ok = !isnan(re), im_ok = !isnan(im);
+    im = re_ok ? im : (T)NAN;
+    re = im_ok ? re : (T)NAN;
+    const T larger = fmax(re, im), smaller = fmin(im, re);
+    const bool div_ok = !(larger == (T)0 || smaller == inf);
+    const T r = div_ok ? smaller / larger : (T)0;
+    return sqrt(fma(r, r, (T)1)) * larger;
+}
+
+// np.mean of v(0..n-1): numpy's pairwise summation (leaf blocks <= 128 with 8 accumulators,
+// split point n/2 rounded down to a multiple of 8), then / n.
+template <typename T, typename F>
+__device__ T pairwise_mean(F v, long n) {
+    long st_s[24], st_n[24];
+    int st_stage[24];
+    T st_left[24];
+    int sp = 0;
+    st_s[0] = 0; st_n[0] = n; st_stage[0] = 0; sp = 1;
+    T ret = 0;
+    while (sp > 0) {
+        const int top = sp - 1;
+        const long s = st_s[top], m = st_n[top];
+        if (m <= 128) {
+            if (m < 8) {
+                T r = 0;
+                for (long i = 0; i < m; ++i) r += v(s + i);
+                ret = r;
+            } else {
+                T r[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) r[k] = v(s + k);
+                long i = 8;
+                for (; i < m - (m % 8); i += 8) {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) r[k] += v(s + i + k);
+                }
+                T res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+                for (; i < m; ++i) res += v(s + i);
+                ret = res;
+            }
+            --sp;
+            continue;
+        }
+        long n2 = m / 2;
+        n2 -= n2 % 8;
+        if (st_stage[top] == 0) {
+            st_stage[top] = 1;
+            st_s[sp] = s; st_n[sp] = n2; st_stage[sp] = 0; ++sp;
+        } else if (st_stage[top] == 1) {
+            st_left[top] = ret;
+            st_stage[top] = 2;
+            st_s[sp] = s + n2; st_n[sp] = m - n2; st_stage[sp] = 0; ++sp;
+        } else {
+            ret = st_left[top] + ret;
+            --sp;
+        }
+    }
+    return ret / (T)n;
+}
+
+// 16 lanes per channel: lane k tries phase k*step (processor.py:196-210), then the group gathers
+// the chosen phase into sym[ch][0..ns).
+template <typename T>
+__global__ __launch_bounds__(256) void k_extract(const T *__restrict__ y, Lay ly, int C, long M, int sps, int step,
+                                                 T *__restrict__ sym, long smax, int32_t *__restrict__ nsym,
+                                                 int32_t *__restrict__ bestph) {
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ch = gid >> 4, k = gid & 15;
+    const int lane = threadIdx.x & 63;
+    const bool ok = ch < C;
+    const int nph = (sps + step - 1) / step;
+    const int ph = k * step;
+    const T *yp = y + ly.off(ok ? ch : 0, 0);
+    const size_t sy = ly.s_n;
+    T power = (T)-2;
+    long ns = (ok && k < nph) ? (M - ph) / sps : 0;
+    if (ns > 0) {
+        auto v = [&](long i) -> T {
+            const size_t o = (size_t)(ph + i * sps) * sy;
+            const T a = np_cabs(yp[o], yp[o + 1]);
+            return a * a;
+        };
+        power = pairwise_mean<T>(v, ns);
+    }
+    T best = (T)-1;
+    int bph = 0;
+    for (int q = 0; q < nph && q < 16; ++q) {
+        const T p = __shfl(power, (lane & ~15) + q, 64);
+        const long nq = (M - q * step) / sps;
+        if (nq > 0 && p > best) { best = p; bph = q * step; }
+    }
+    if (!ok) return;
+    const long nout = (M - bph) / sps;
+    if (k == 0) {
+        nsym[ch] = (int32_t)nout;
+        if (bestph) bestph[ch] = bph;
+    }
+    T *op = sym + (size_t)ch * smax * 2;
+    for (long i = k; i < nout; i += 16) {
+        const size_t o = (size_t)(bph + i * sps) * sy;
+        op[2 * i] = yp[o];
+        op[2 * i + 1] = yp[o + 1];
+    }
+}
+
+// ------------------------------------------------------------------ demodulate_dqpsk
+// One wave per channel.  sym rows [C][stride] complex T, S = nsym[ch] (or S_all).
+template <typename T>
+__global__ __launch_bounds__(64) void k_demod(const T *__restrict__ sym, long stride, int C, const int32_t *__restrict__ nsym,
+                                              long S_all, double t0, double t1, double t2, double t3,
+                                              uint8_t *__restrict__ hard, long hstride) {
+    const int ch = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (ch >= C) return;
+    const long S = nsym ? nsym[ch] : S_all;
+    if (S < 2) return;
+    const T *sp = sym + (size_t)ch * stride * 2;
+    T m = (T)-INFINITY;
+    bool any_nan = false;
+    for (long k = lane; k < S; k += 64) {
+        const T a = np_cabs(sp[2 * k], sp[2 * k + 1]);
+        any_nan |= isnan(a);
+        m = fmax(m, a);
+    }
+    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    any_nan = __any(any_nan);
+    const T mx = any_nan ? (T)NAN : m;   // np.max propagates NaN
+    // samples / max_power: numpy complex division (Smith) by (m + 0j): rat = 0/m, scl = 1/m,
+    // out = ((xr + xi*rat)*scl, (xi - xr*rat)*scl)
+    const bool norm = mx > (T)0;
+    const T rat = norm ? (T)0 / mx : (T)0;
+    const T scl = norm ? (T)1 / (mx + (T)0 * rat) : (T)1;
+    const T th0 = (T)t0, th1 = (T)t1, th2 = (T)t2, th3 = (T)t3;
+    uint8_t *hp = hard + (size_t)ch * hstride;
+    for (long k = 1 + lane; k < S; k += 64) {
+        T sr = sp[2 * k], si = sp[2 * k + 1], pr = sp[2 * k - 2], pi = sp[2 * k - 1];
+        if (norm) {
+            const T a = (sr + si * rat) * scl, b = (si - sr * rat) * scl;
+            const T c = (pr + pi * rat) * scl, d = (pi - pr * rat) * scl;
+            sr = a; si = b; pr = c; pi = d;
+        }
+        // numpy scalar complex multiply sample * conj(prev), no FMA
+        const T npi = -pi;
+        const T dr = sr * pr - si * npi;
+        const T di = sr * npi + si * pr;
+        const T ph = atan2(di, dr);
+        uint8_t s;
+        if (ph < th0) s = 3;
+        else if (ph < th1) s = 2;
+        else if (ph < th2) s = 0;
+        else if (ph < th3) s = 1;
+        else s = 3;
+        hp[k - 1] = s;
+    }
+}
+
+// grouped [C/32][len][32][2] -> row-major [C][len] complex
+template <typename T>
+__global__ void k_relayout(const T *__restrict__ in, Lay li, int C, long len, T *__restrict__ out, Lay lo) {
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int ch = (int)(gid / len);
+    const long n = gid - (long)ch * len;
+    if (ch >= C) return;
+    const T *ip = in + li.off(ch, n);
+    T *op = out + lo.off(ch, n);
+    op[0] = ip[0];
+    op[1] = ip[1];
+}
+
+long ceil_div(long a, long b) { return (a + b - 1) / b; }
+
+// ----------------------------------------------------------------- host-side stage drivers
+template <typename T>
+int run_decimate(tetra_ctx *ctx, const tetra_compat_plan *P, const T *x, Lay lx, int C, long N, T *out, Lay lo) {
+    const int pad = 27;   // 3 * (2*4 + 1): sosfiltfilt default padlen for 4 sections
+    const long L = N + 2 * pad;
+    T *scr = (T *)ws(ctx, S_W0, grouped_elems(C, L) * sizeof(T));
+    T *coef = (T *)ws(ctx, S_W7, 32 * sizeof(T));
+    if (!scr || !coef) return TETRA_E_NOMEM;
+    T hc[32];
+    for (int i = 0; i < 24; ++i) hc[i] = std::is_same<T, float>::value ? (T)P->sos_f32[i] : (T)P->sos_f64[i];
+    for (int i = 0; i < 8; ++i) hc[24 + i] = std::is_same<T, float>::value ? (T)P->zi_f32[i] : (T)P->zi_f64[i];
+    HIP_TRY(ctx, hipMemcpyAsync(coef, hc, sizeof hc, hipMemcpyHostToDevice, ctx->stream));
+    const unsigned blk = 64;
+    hipLaunchKernelGGL(k_sos_fwd<T>, dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, x, lx, C, N, pad,
+                       coef, coef + 24, scr, grouped(L));
+    hipLaunchKernelGGL(k_sos_bwd<T>, dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, scr, grouped(L), C,
+                       N, pad, P->q, coef, coef + 24, out, lo);
+    return TETRA_OK;
+}
+
+template <typename TIn>
+int run_filtfilt(tetra_ctx *ctx, const tetra_compat_plan *P, const TIn *x, Lay lx, int C, long M,
+                 const double *mixc, const uint8_t *mixon, double *out, Lay lo) {
+    const int nt = P->ntaps, pad = 3 * nt;
+    if (nt < 2 || nt > MAXTAP) return tetra_fail(ctx, TETRA_E_INVALID, "ntaps %d unsupported", nt);
+    const long L = M + 2 * pad;
+    double *scr = (double *)ws(ctx, S_W2, grouped_elems(C, L) * sizeof(double));
+    double *coef = (double *)ws(ctx, S_W6, 3 * MAXTAP * sizeof(double));
+    if (!scr || !coef) return TETRA_E_NOMEM;
+    double hc[3 * MAXTAP] = {0};
+    for (int k = 0; k < nt; ++k) { hc[k] = P->b[k]; hc[MAXTAP + k] = P->a[k]; }
+    for (int k = 0; k < nt - 1; ++k) hc[2 * MAXTAP + k] = P->lzi[k];
+    HIP_TRY(ctx, hipMemcpyAsync(coef, hc, sizeof hc, hipMemcpyHostToDevice, ctx->stream));
+    const unsigned blk = 64;
+    hipLaunchKernelGGL(k_lf_fwd<TIn>, dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, x, lx, C, M, pad,
+                       nt, coef, coef + MAXTAP, coef + 2 * MAXTAP, mixc, mixon, P->fs_dec, scr, grouped(L));
+    hipLaunchKernelGGL(k_lf_bwd, dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, scr, grouped(L), C, M,
+                       pad, nt, coef, coef + MAXTAP, coef + 2 * MAXTAP, out, lo);
+    return TETRA_OK;
+}
+
+template <typename T>
+void launch_extract(tetra_ctx *ctx, const T *y, Lay ly, int C, long M, int sps, int step, T *sym, long smax,
+                    int32_t *nsym, int32_t *bph) {
+    hipLaunchKernelGGL(k_extract<T>, dim3(grid_for((size_t)16 * C, 256)), dim3(256), 0, ctx->stream, y, ly, C, M, sps,
+                       step, sym, smax, nsym, bph);
+}
+
+template <typename T>
+void launch_demod(tetra_ctx *ctx, const T *sym, long stride, int C, const int32_t *nsym, long S_all,
+                  const double *thr, uint8_t *hard, long hstride) {
+    hipLaunchKernelGGL(k_demod<T>, dim3(C), dim3(64), 0, ctx->stream, sym, stride, C, nsym, S_all, thr[0], thr[1],
+                       thr[2], thr[3], hard, hstride);
+}
+
+int check_plan(tetra_ctx *ctx, const tetra_compat_plan *P) {
+    if (!P) return tetra_fail(ctx, TETRA_E_INVALID, "plan is NULL");
+    if (P->sps < 1 || P->phase_step < 1) return tetra_fail(ctx, TETRA_E_INVALID, "bad sps/phase_step");
+    return TETRA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t tetra_compat_symbols(const tetra_compat_plan *P, size_t N) {
+    if (!P || N == 0) return 0;
+    long M = P->q > 1 ? ceil_div((long)N, P->q) : (long)N;
+    return M / (P->sps < 1 ? 1 : P->sps) + 1;   // upper bound over phases
+}
+
+int tetra_decimate(tetra_ctx *ctx, const tetra_compat_plan *P, const void *iq, int fmt, size_t C, size_t N, void *out) {
+    if (!ctx) return TETRA_E_INVALID;
+    int rc = check_plan(ctx, P);
+    if (rc) return rc;
+    if (P->q < 2 || N <= 27 || C == 0) return tetra_fail(ctx, TETRA_E_INVALID, "decimate needs q>=2 and N>27");
+    const size_t es = fmt == TETRA_CF64 ? 8 : 4;
+    const long M = ceil_div((long)N, P->q);
+    Staging st(ctx);
+    const void *x = st.in(iq, C * N * 2 * es);
+    void *o = st.out(out, C * M * 2 * es);
+    if (!x || !o) return st.finish();
+    if (fmt == TETRA_CF64)
+        rc = run_decimate<double>(ctx, P, (const double *)x, row_major(N), (int)C, (long)N, (double *)o, row_major(M));
+    else
+        rc = run_decimate<float>(ctx, P, (const float *)x, row_major(N), (int)C, (long)N, (float *)o, row_major(M));
+    if (rc) return rc;
+    return st.finish();
+}
+
+int tetra_frequency_shift(tetra_ctx *ctx, const void *iq, int fmt, size_t C, size_t N, const double *mix_c, double fs,
+                          void *out) {
+    if (!ctx || C == 0) return TETRA_E_INVALID;
+    if (N == 0) return TETRA_OK;
+    const size_t es = fmt == TETRA_CF64 ? 8 : 4;
+    Staging st(ctx);
+    const void *x = st.in(iq, C * N * 2 * es);
+    const double *mc = (const double *)st.in(mix_c, C * sizeof(double));
+    void *o = st.out(out, C * N * 16);
+    if (!x || !mc || !o) return st.finish();
+    const unsigned blk = 256;
+    if (fmt == TETRA_CF64)
+        hipLaunchKernelGGL(k_mix<double>, dim3(grid_for(C * N, blk)), dim3(blk), 0, ctx->stream, (const double *)x,
+                           row_major(N), (int)C, (long)N, mc, (const uint8_t *)nullptr, fs, (double *)o, row_major(N));
+    else
+        hipLaunchKernelGGL(k_mix<float>, dim3(grid_for(C * N, blk)), dim3(blk), 0, ctx->stream, (const float *)x,
+                           row_major(N), (int)C, (long)N, mc, (const uint8_t *)nullptr, fs, (double *)o, row_major(N));
+    return st.finish();
+}
+
+int tetra_filtfilt(tetra_ctx *ctx, const tetra_compat_plan *P, const void *iq, int fmt, size_t C, size_t N, void *out) {
+    if (!ctx) return TETRA_E_INVALID;
+    if (!P || (long)N <= 3 * P->ntaps || C == 0)
+        return tetra_fail(ctx, TETRA_E_INVALID, "filtfilt needs N > padlen");
+    const size_t es = fmt == TETRA_CF64 ? 8 : 4;
+    Staging st(ctx);
+    const void *x = st.in(iq, C * N * 2 * es);
+    void *o = st.out(out, C * N * 16);
+    if (!x || !o) return st.finish();
+    int rc;
+    if (fmt == TETRA_CF64)
+        rc = run_filtfilt<double>(ctx, P, (const double *)x, row_major(N), (int)C, (long)N, nullptr, nullptr,
+                                  (double *)o, row_major(N));
+    else
+        rc = run_filtfilt<float>(ctx, P, (const float *)x, row_major(N), (int)C, (long)N, nullptr, nullptr,
+                                 (double *)o, row_major(N));
+    if (rc) return rc;
+    return st.finish();
+}
+
+int tetra_extract_symbols(tetra_ctx *ctx, const void *x, int fmt, size_t C, size_t N, int sps, int step, void *sym,
+                          int32_t *nsym, int32_t *bestph, size_t smax) {
+    if (!ctx || C == 0 || N == 0 || sps < 1 || step < 1) return tetra_fail(ctx, TETRA_E_INVALID, "bad extract args");
+    if ((sps + step - 1) / step > 16) return tetra_fail(ctx, TETRA_E_INVALID, "more than 16 phases");
+    const size_t es = fmt == TETRA_CF64 ? 8 : 4;
+    Staging st(ctx);
+    const void *xd = st.in(x, C * N * 2 * es);
+    void *sd = st.out(sym, C * smax * 2 * es);
+    int32_t *nd = (int32_t *)st.out(nsym, C * 4);
+    int32_t *bd = bestph ? (int32_t *)st.out(bestph, C * 4) : nullptr;
+    if (!xd || !sd || !nd) return st.finish();
+    if (fmt == TETRA_CF64)
+        launch_extract<double>(ctx, (const double *)xd, row_major(N), (int)C, (long)N, sps, step, (double *)sd,
+                               (long)smax, nd, bd);
+    else
+        launch_extract<float>(ctx, (const float *)xd, row_major(N), (int)C, (long)N, sps, step, (float *)sd,
+                              (long)smax, nd, bd);
+    return st.finish();
+}
+
+int tetra_demod_dqpsk(tetra_ctx *ctx, const void *sym, int fmt, size_t C, size_t S, const double *thr4, uint8_t *hard) {
+    if (!ctx || !thr4) return TETRA_E_INVALID;
+    if (S < 2 || C == 0) return TETRA_OK;
+    const size_t es = fmt == TETRA_CF64 ? 8 : 4;
+    Staging st(ctx);
+    const void *sd = st.in(sym, C * S * 2 * es);
+    uint8_t *hd = (uint8_t *)st.out(hard, C * (S - 1));
+    if (!sd || !hd) return st.finish();
+    if (fmt == TETRA_CF64)
+        launch_demod<double>(ctx, (const double *)sd, (long)S, (int)C, nullptr, (long)S, thr4, hd, (long)(S - 1));
+    else
+        launch_demod<float>(ctx, (const float *)sd, (long)S, (int)C, nullptr, (long)S, thr4, hd, (long)(S - 1));
+    return st.finish();
+}
+
+int tetra_demod_compat(tetra_ctx *ctx, const tetra_compat_plan *P, const void *iq, int fmt, size_t C, size_t N,
+                       const double *mix_c, const uint8_t *mix_on, void *soft, uint8_t *hard, int32_t *nsym,
+                       size_t smax, int32_t *soft_f32) {
+    if (!ctx) return TETRA_E_INVALID;
+    int rc = check_plan(ctx, P);
+    if (rc) return rc;
+    if (C == 0 || N == 0) return tetra_fail(ctx, TETRA_E_INVALID, "empty batch (process() handles len 0 on host)");
+    if ((P->sps + P->phase_step - 1) / P->phase_step > 16) return tetra_fail(ctx, TETRA_E_INVALID, "more than 16 phases");
+    const bool dec = P->q > 1;
+    if (dec && (int)(fmt == TETRA_CF64) != P->dec_f64) return tetra_fail(ctx, TETRA_E_INVALID, "plan/iq precision mismatch");
+    const long M = dec ? ceil_div((long)N, P->q) : (long)N;
+    if ((long)smax < M / P->sps + 1 && (long)smax < M) return tetra_fail(ctx, TETRA_E_INVALID, "smax too small");
+    const size_t es = fmt == TETRA_CF64 ? 8 : 4;
+    Staging st(ctx);
+    const void *x = st.in(iq, C * N * 2 * es);
+    const double *mc = (const double *)st.in(mix_c, C * sizeof(double));
+    const uint8_t *mo = (const uint8_t *)st.in(mix_on, C);
+    if (!x || !mc || !mo) return st.finish();
+    // mixed precision of the unfiltered path is per channel; require it uniform (host splits)
+    uint8_t any_mix = 0, all_mix = 1;
+    if (!P->filt) {
+        std::vector<uint8_t> h(C);
+        HIP_TRY(ctx, hipMemcpyAsync(h.data(), mo, C, hipMemcpyDefault, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        for (auto v : h) { any_mix |= v; all_mix &= v; }
+        if (any_mix && !all_mix) return tetra_fail(ctx, TETRA_E_INVALID, "unfiltered batch with mixed freq_offset flags");
+    }
+    const bool f32_soft = !P->filt && !any_mix && fmt == TETRA_CF32;
+    const size_t ses = f32_soft ? 4 : 8;
+    void *so = st.out(soft, C * smax * 2 * ses);
+    uint8_t *ho = (uint8_t *)st.out(hard, C * smax);
+    int32_t *no = (int32_t *)st.out(nsym, C * 4);
+    if (!so || !ho || !no) return st.finish();
+    // stage 1: decimate (processor.py:248-257)
+    const void *d = x;
+    Lay ld = row_major(N);
+    if (dec) {
+        void *db = ws(ctx, S_W1, grouped_elems((int)C, M) * es);
+        if (!db) return TETRA_E_NOMEM;
+        rc = fmt == TETRA_CF64 ? run_decimate<double>(ctx, P, (const double *)x, row_major(N), (int)C, (long)N,
+                                                      (double *)db, grouped(M))
+                               : run_decimate<float>(ctx, P, (const float *)x, row_major(N), (int)C, (long)N,
+                                                     (float *)db, grouped(M));
+        if (rc) return rc;
+        d = db;
+        ld = grouped(M);
+    }
+    // stage 2: mixer + filtfilt (processor.py:260-264)
+    const void *y = d;
+    Lay ly = ld;
+    bool y_f64 = fmt == TETRA_CF64;
+    if (P->filt || any_mix) {
+        double *fb = (double *)ws(ctx, S_W3, grouped_elems((int)C, M) * 8);
+        if (!fb) return TETRA_E_NOMEM;
+        if (P->filt) {
+            rc = fmt == TETRA_CF64 ? run_filtfilt<double>(ctx, P, (const double *)d, ld, (int)C, M, mc, mo, fb, grouped(M))
+                                   : run_filtfilt<float>(ctx, P, (const float *)d, ld, (int)C, M, mc, mo, fb, grouped(M));
+            if (rc) return rc;
+        } else if (fmt == TETRA_CF64) {
+            hipLaunchKernelGGL(k_mix<double>, dim3(grid_for(C * M, 256)), dim3(256), 0, ctx->stream, (const double *)d,
+                               ld, (int)C, M, mc, mo, P->fs_dec, fb, grouped(M));
+        } else {
+            hipLaunchKernelGGL(k_mix<float>, dim3(grid_for(C * M, 256)), dim3(256), 0, ctx->stream, (const float *)d,
+                               ld, (int)C, M, mc, mo, P->fs_dec, fb, grouped(M));
+        }
+        y = fb;
+        ly = grouped(M);
+        y_f64 = true;
+    }
+    // stage 3+4: extract_symbols + demodulate_dqpsk (processor.py:267-271)
+    if (y_f64) {
+        launch_extract<double>(ctx, (const double *)y, ly, (int)C, M, P->sps, P->phase_step, (double *)so, (long)smax, no,
+                               nullptr);
+        launch_demod<double>(ctx, (const double *)so, (long)smax, (int)C, no, 0, P->thr, ho, (long)smax);
+    } else {
+        launch_extract<float>(ctx, (const float *)y, ly, (int)C, M, P->sps, P->phase_step, (float *)so, (long)smax, no,
+                              nullptr);
+        launch_demod<float>(ctx, (const float *)so, (long)smax, (int)C, no, 0, P->thr, ho, (long)smax);
+    }
+    if (soft_f32) *soft_f32 = f32_soft ? 1 : 0;
+    return st.finish();
+}
+
+}  // extern "C"

@@ -1,0 +1,159 @@
+// ctx.hip -- context lifecycle, error reporting and host/device argument staging.
+#include "common.h"
+
+thread_local std::string g_tetra_err;
+
+int tetra_fail(tetra_ctx *ctx, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->err = buf;
+    g_tetra_err = buf;
+    return code;
+}
+
+void *ws(tetra_ctx *ctx, int s, size_t bytes) {
+    DevBuf &b = ctx->slot[s];
+    if (bytes == 0) bytes = 16;
+    if (b.bytes >= bytes) return b.p;
+    if (b.p) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipFree(b.p);
+        b.p = nullptr;
+        b.bytes = 0;
+    }
+    size_t want = bytes + (bytes >> 3);   // headroom against regrowth
+    hipError_t e = hipMalloc(&b.p, want);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        tetra_fail(ctx, TETRA_E_NOMEM, "hipMalloc(%zu) failed: %s", want, hipGetErrorString(e));
+        b.p = nullptr;
+        return nullptr;
+    }
+    b.bytes = want;
+    return b.p;
+}
+
+bool is_device_ptr(const void *p) {
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+const void *Staging::in(const void *p, size_t bytes) {
+    if (failed) return nullptr;
+    if (bytes == 0) return p ? p : ws(ctx, next_in++, 16);
+    if (is_device_ptr(p)) return p;
+    host_touched = true;
+    void *d = ws(ctx, next_in++, bytes);
+    if (!d || hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) {
+        failed = true;
+        if (d) tetra_fail(ctx, TETRA_E_HIP, "H2D staging copy failed");
+        return nullptr;
+    }
+    return d;
+}
+
+void *Staging::out(void *p, size_t bytes) {
+    if (failed) return nullptr;
+    if (bytes == 0) return p ? p : ws(ctx, next_out++, 16);
+    if (is_device_ptr(p)) return p;
+    host_touched = true;
+    void *d = ws(ctx, next_out++, bytes);
+    if (!d) {
+        failed = true;
+        return nullptr;
+    }
+    back.push_back({p, d, bytes});
+    return d;
+}
+
+int Staging::finish() {
+    if (failed) return ctx->err.empty() ? tetra_fail(ctx, TETRA_E_HIP, "staging failed") : TETRA_E_HIP;
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return tetra_fail(ctx, TETRA_E_HIP, "kernel launch failed: %s", hipGetErrorString(e));
+    for (auto &b : back)
+        HIP_TRY(ctx, hipMemcpyAsync(b.host, b.dev, b.bytes, hipMemcpyDeviceToHost, ctx->stream));
+    if (host_touched) HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return TETRA_OK;
+}
+
+extern "C" {
+
+int tetra_abi_version(void) { return TETRA_ABI_VERSION; }
+
+tetra_ctx *tetra_create(int device) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        tetra_fail(nullptr, TETRA_E_NODEVICE, "no HIP device visible (%s)", hipGetErrorString(e));
+        return nullptr;
+    }
+    if (device < 0 || device >= n) {
+        tetra_fail(nullptr, TETRA_E_INVALID, "device %d out of range (%d devices)", device, n);
+        return nullptr;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess || hipSetDevice(device) != hipSuccess) {
+        tetra_fail(nullptr, TETRA_E_HIP, "cannot open device %d", device);
+        return nullptr;
+    }
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        tetra_fail(nullptr, TETRA_E_NODEVICE, "device %d is %s; libtetra_hip is built for gfx950", device,
+                   prop.gcnArchName);
+        return nullptr;
+    }
+    tetra_ctx *ctx = new tetra_ctx();
+    ctx->device = device;
+    snprintf(ctx->arch, sizeof ctx->arch, "%s", prop.gcnArchName);
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        tetra_fail(nullptr, TETRA_E_HIP, "hipStreamCreate failed");
+        delete ctx;
+        return nullptr;
+    }
+    return ctx;
+}
+
+void tetra_destroy(tetra_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (auto &b : ctx->slot)
+        if (b.p) (void)hipFree(b.p);
+    if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char *tetra_last_error(const tetra_ctx *ctx) { return ctx ? ctx->err.c_str() : g_tetra_err.c_str(); }
+
+void *tetra_get_stream(tetra_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+int tetra_set_stream(tetra_ctx *ctx, void *s) {
+    if (!ctx) return TETRA_E_INVALID;
+    if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    ctx->stream = (hipStream_t)s;
+    ctx->own_stream = false;
+    return TETRA_OK;
+}
+
+int tetra_synchronize(tetra_ctx *ctx) {
+    if (!ctx) return TETRA_E_INVALID;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return TETRA_OK;
+}
+
+int tetra_device_arch(tetra_ctx *ctx, char *buf, size_t n) {
+    if (!ctx || !buf || !n) return TETRA_E_INVALID;
+    snprintf(buf, n, "%s", ctx->arch);
+    return TETRA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,144 @@
+"""ctypes binding of libtetra_hip.so (include/tetra_hip.h).
+
+This is the only way the Python surface reaches compute: every numeric method of
+SignalProcessor / TetraDecoder / TetraProtocolParser calls an entry point here.  There is no CPU
+fallback: if the library or a gfx950 device is missing, ``ctx()`` raises ``TetraHipError``.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("TETRA_HIP_LIB", os.path.join(os.path.dirname(_PKG), "lib", "libtetra_hip.so"))
+
+TETRA_CF32, TETRA_CF64 = 0, 1
+MAX_SYNC = 16
+F_POS, F_START, F_VALID, F_NBITS, F_NUMBER, F_BTYPE, F_CRC, F_HDR, F_FIELDS = range(9)
+
+
+class TetraHipError(RuntimeError):
+    pass
+
+
+class CompatPlan(ctypes.Structure):
+    """Mirror of struct tetra_compat_plan (include/tetra_hip.h)."""
+    _fields_ = [
+        ("q", ctypes.c_int32), ("dec_f64", ctypes.c_int32), ("filt", ctypes.c_int32),
+        ("ntaps", ctypes.c_int32), ("sps", ctypes.c_int32), ("phase_step", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 2), ("fs_dec", ctypes.c_double),
+        ("sos_f32", ctypes.c_float * 24), ("zi_f32", ctypes.c_float * 8),
+        ("sos_f64", ctypes.c_double * 24), ("zi_f64", ctypes.c_double * 8),
+        ("b", ctypes.c_double * 8), ("a", ctypes.c_double * 8), ("lzi", ctypes.c_double * 8),
+        ("thr", ctypes.c_double * 4),
+    ]
+
+
+_lib = None
+_lib_lock = threading.Lock()
+_tls = threading.local()
+
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+_i32 = ctypes.c_int
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_dp = ctypes.POINTER(ctypes.c_double)
+
+
+def _bind(L):
+    sig = {
+        "tetra_abi_version": (_i32, []),
+        "tetra_create": (_vp, [_i32]),
+        "tetra_destroy": (None, [_vp]),
+        "tetra_last_error": (ctypes.c_char_p, [_vp]),
+        "tetra_get_stream": (_vp, [_vp]),
+        "tetra_set_stream": (_i32, [_vp, _vp]),
+        "tetra_synchronize": (_i32, [_vp]),
+        "tetra_device_arch": (_i32, [_vp, ctypes.c_char_p, _sz]),
+        "tetra_compat_symbols": (ctypes.c_int64, [ctypes.POINTER(CompatPlan), _sz]),
+        "tetra_demod_compat": (_i32, [_vp, ctypes.POINTER(CompatPlan), _vp, _i32, _sz, _sz, _vp, _vp, _vp, _vp, _vp,
+                                      _sz, _i32p]),
+        "tetra_decimate": (_i32, [_vp, ctypes.POINTER(CompatPlan), _vp, _i32, _sz, _sz, _vp]),
+        "tetra_frequency_shift": (_i32, [_vp, _vp, _i32, _sz, _sz, _vp, ctypes.c_double, _vp]),
+        "tetra_filtfilt": (_i32, [_vp, ctypes.POINTER(CompatPlan), _vp, _i32, _sz, _sz, _vp]),
+        "tetra_extract_symbols": (_i32, [_vp, _vp, _i32, _sz, _sz, _i32, _i32, _vp, _vp, _vp, _sz]),
+        "tetra_demod_dqpsk": (_i32, [_vp, _vp, _i32, _sz, _sz, _vp, _vp]),
+        "tetra_lmac_compat": (_i32, [_vp, _vp, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp]),
+        "tetra_symbols_to_bits": (_i32, [_vp, _vp, _sz, _vp, _vp]),
+        "tetra_find_sync": (_i32, [_vp, _vp, _sz, _i32, _vp, _i32, _i32p, _i32p]),
+        "tetra_match_count": (_i32, [_vp, _vp, _sz, _sz, _vp, _sz, _vp]),
+        "tetra_parse_bursts": (_i32, [_vp, _vp, _sz, _vp, _vp, _vp]),
+        "tetra_crc16": (_i32, [_vp, _vp, _sz, _sz, _i32, _vp]),
+        "tetra_check_crc": (_i32, [_vp, _vp, _sz, _sz, _vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    return L
+
+
+def lib():
+    """Load libtetra_hip.so (raises TetraHipError when it is missing -- no fallback)."""
+    global _lib
+    if _lib is None:
+        with _lib_lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise TetraHipError(f"libtetra_hip.so not found at {LIB_PATH}: build it with "
+                                        f"`make -C tetraear-bladerf_amd` (no CPU fallback exists)")
+                _lib = _bind(ctypes.CDLL(LIB_PATH))
+    return _lib
+
+
+class Context:
+    """One HIP context (device + stream) per host thread, as the C ABI requires."""
+
+    def __init__(self, device=None):
+        if device is None:
+            device = int(os.environ.get("TETRA_HIP_DEVICE", "0"))
+        self.lib = lib()
+        self.handle = self.lib.tetra_create(device)
+        if not self.handle:
+            raise TetraHipError("tetra_create failed: " + (self.lib.tetra_last_error(None) or b"").decode())
+        self.device = device
+
+    def check(self, rc, what=""):
+        if rc != 0:
+            msg = (self.lib.tetra_last_error(self.handle) or b"").decode()
+            raise TetraHipError(f"{what} failed (rc={rc}): {msg}")
+
+    def arch(self):
+        buf = ctypes.create_string_buffer(64)
+        self.check(self.lib.tetra_device_arch(self.handle, buf, 64), "tetra_device_arch")
+        return buf.value.decode()
+
+    def synchronize(self):
+        self.check(self.lib.tetra_synchronize(self.handle), "tetra_synchronize")
+
+    def __del__(self):
+        try:
+            if self.handle:
+                self.lib.tetra_destroy(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+
+def ctx():
+    c = getattr(_tls, "ctx", None)
+    if c is None:
+        c = Context()
+        _tls.ctx = c
+    return c
+
+
+def ptr(a):
+    """Address of a C-contiguous numpy array (or a torch tensor's data_ptr)."""
+    if a is None:
+        return None
+    if hasattr(a, "data_ptr"):
+        return ctypes.c_void_p(a.data_ptr())
+    assert a.flags["C_CONTIGUOUS"], "arrays passed to libtetra_hip must be C-contiguous"
+    return a.ctypes.data_as(ctypes.c_void_p)

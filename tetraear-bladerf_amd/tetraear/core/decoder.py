@@ -1,0 +1,243 @@
+"""MI355X TetraDecoder -- the reference's lower-MAC surface, computed by libtetra_hip.so.
+
+Mirrors the hot-path methods of /root/reference/tetraear/core/decoder.py:
+  symbols_to_bits  :140-169     find_sync  :171-295     decode :835-888     decode_frame :890-992
+Correlation, the greedy sync scan, burst slicing, burst typing and CRC run on the GPU
+(tetra_lmac_compat / tetra_find_sync / tetra_symbols_to_bits).  The Python here keeps the
+reference's float decisions (threshold comparisons, the adaptive re-search rule) and builds the
+frame dicts.  Upper-MAC parsing, SDS and decryption (decoder.py:994-1117) are not part of this
+hot-path build: they stay the reference's Python and attach through ``upper_mac``.
+
+``mode="etsi"`` decodes ETSI channel coding (descramble, deinterleave, RCPC Viterbi, CRC-16) on
+the soft bits of the ETSI demodulator instead; see tetraear.core.etsi.
+"""
+import ctypes
+import functools
+import logging
+from typing import Optional
+
+import numpy as np
+
+from tetraear import _hip
+from tetraear.core.protocol import TetraProtocolParser, burst_from_bits
+
+logger = logging.getLogger(__name__)
+
+TS1 = np.array([1, 1, 0, 1, 0, 0, 0, 0, 1, 1, 1, 0, 1, 0, 0, 1, 1, 1, 0, 1, 0, 0])
+TS2 = np.array([0, 1, 1, 1, 1, 0, 1, 0, 0, 1, 0, 0, 0, 0, 1, 1, 0, 1, 1, 1, 0, 0])
+FRAME_TYPE_NAMES = {0: "MAC-RESOURCE", 1: "MAC-FRAG", 2: "MAC-BROADCAST", 3: "MAC-END/RES"}
+FRAME_TYPE_DESC = {0: "Resource allocation", 1: "Fragment", 2: "Broadcast info", 3: "End/Reserved"}
+ENC_MODES = {1: ("TEA1", "Class 2 (SCK)"), 2: ("TEA2", "Class 3 (DCK)"), 3: ("TEA3", "Reserved")}
+
+
+def count_threshold(thr):
+    """Least match count c with c/22 >= thr -- the float test of decoder.py:240-245."""
+    for c in range(23):
+        if c / 22 >= thr:
+            return c
+    return 23
+
+
+def _find_sync_outcome(thr, best):
+    """(count threshold used, max_corr) of find_sync(thr) when the stream's best count is `best`.
+
+    With no hit every position is visited, so max_corr is best/22 and the adaptive re-search
+    (decoder.py:263-281) is a greedy scan at the adaptive threshold."""
+    k = count_threshold(thr)
+    if best >= k:
+        return k, None
+    mc = best / 22
+    if mc > 0.75 and mc >= (thr - 0.15):
+        ad = max(0.75, mc - 0.02)
+        if ad < thr:
+            ka = count_threshold(ad)
+            if best >= ka:
+                return ka, mc
+    return None, mc
+
+
+@functools.lru_cache(maxsize=1)
+def cascade_table():
+    """decode()'s 0.90 -> 0.85 -> 0.80 -> adaptive cascade (decoder.py:845-857) as a function of
+    the stream's best correlation count: the count threshold its sync positions use, or -1."""
+    tab = np.full(23, -1, np.int8)
+    for best in range(23):
+        k, mc = _find_sync_outcome(0.90, best)
+        if k is None:
+            k, mc = _find_sync_outcome(0.85, best)
+        if k is None:
+            k, mc = _find_sync_outcome(0.80, best)
+            if k is None and mc >= 0.75:
+                k, _ = _find_sync_outcome(max(0.75, mc - 0.02), best)
+        tab[best] = -1 if k is None else k
+    return tab
+
+
+def _bits_u8(bits):
+    b = np.asarray(bits)
+    return np.ascontiguousarray(np.where((b == 0) | (b == 1), b, 2), dtype=np.uint8)
+
+
+class TetraDecoder:
+    """Decodes TETRA frames from demodulated symbols (decoder.py:16)."""
+
+    def __init__(self, key_manager=None, auto_decrypt: bool = True, mode: str = "compat"):
+        self.SYNC_PATTERN = [0, 1, 0, 1, 1, 0, 0, 1, 1, 1, 0, 0, 0, 1, 0, 0,
+                             1, 0, 1, 1, 0, 0, 1, 1, 1, 0, 0, 0, 1, 0, 0]
+        self.FRAME_LENGTH = 510
+        self.key_manager = key_manager
+        self.auto_decrypt = auto_decrypt
+        self.protocol_parser = TetraProtocolParser()
+        self.sync_patterns = {'TS1': TS1.copy(), 'TS2': TS2.copy()}
+        self.user_keys = []
+        if mode not in ("compat", "etsi"):
+            raise ValueError("mode must be 'compat' or 'etsi'")
+        self.mode = mode
+        self._etsi = None
+
+    # ------------------------------------------------------------------ bits
+    def symbols_to_bits(self, symbols):
+        """Dibits MSB-first; 8-PSK neighbour map when max(symbols) > 3 (decoder.py:140-169)."""
+        s = np.asarray(symbols)
+        if len(s) == 0:
+            return np.array([]), np.array([])
+        s = np.ascontiguousarray(s, dtype=np.int64)
+        bits = np.empty(2 * len(s), np.int64)
+        mapped = np.empty(len(s), np.int64)
+        c = _hip.ctx()
+        c.check(c.lib.tetra_symbols_to_bits(c.handle, _hip.ptr(s), len(s), _hip.ptr(bits), _hip.ptr(mapped)),
+                "tetra_symbols_to_bits")
+        return bits, mapped
+
+    # ------------------------------------------------------------------ sync
+    def _greedy(self, b, k, maxpos):
+        pos = np.zeros(max(1, maxpos), np.int64)
+        n, mc = ctypes.c_int32(0), ctypes.c_int32(0)
+        c = _hip.ctx()
+        c.check(c.lib.tetra_find_sync(c.handle, _hip.ptr(b), len(b), k, _hip.ptr(pos), len(pos), n, mc),
+                "tetra_find_sync")
+        return [int(p) for p in pos[:min(n.value, len(pos))]], mc.value
+
+    def find_sync(self, bits, threshold=0.85, return_max_corr=False):
+        """22-bit TS1/TS2 correlation with greedy +250 skip and adaptive re-search (decoder.py:171-295)."""
+        self.sync_patterns = {'TS1': TS1.copy(), 'TS2': TS2.copy()}
+        if len(bits) < 22:
+            return ([], 0.0) if return_max_corr else []
+        b = _bits_u8(bits)
+        maxpos = (len(b) - 21) // 250 + 2
+        sync, maxc = self._greedy(b, count_threshold(threshold), maxpos)
+        max_corr = maxc / 22
+        if not sync and max_corr > 0.75 and max_corr >= (threshold - 0.15):
+            adaptive = max(0.75, max_corr - 0.02)
+            if adaptive < threshold:
+                sync, _ = self._greedy(b, count_threshold(adaptive), maxpos)
+                logger.debug(f"Found {len(sync)} syncs at adaptive threshold {adaptive:.4f} "
+                             f"(max: {max_corr:.4f}, original: {threshold:.4f})")
+        return (sync, max_corr) if return_max_corr else sync
+
+    # ------------------------------------------------------------------ frames
+    def decode(self, symbols):
+        """Sync cascade, slot slicing and burst parsing of one symbol stream (decoder.py:835-888)."""
+        if self.mode == "etsi":
+            return self._etsi_rx().decode(symbols)
+        return self.decode_batch([symbols])[0]
+
+    def decode_batch(self, streams):
+        """decode() over many independent symbol streams with one device pass."""
+        streams = [np.asarray(s) for s in streams]
+        C = len(streams)
+        stride = max([len(s) for s in streams] + [1])
+        sym = np.zeros((C, stride), np.int64)
+        ns = np.zeros(C, np.int32)
+        for i, s in enumerate(streams):
+            sym[i, :len(s)] = s
+            ns[i] = len(s)
+        nsync = np.zeros(C, np.int32)
+        rec = np.zeros((C, _hip.MAX_SYNC, _hip.F_FIELDS), np.int32)
+        fbits = np.zeros((C, _hip.MAX_SYNC, 510), np.uint8)
+        bbits = np.zeros((C, _hip.MAX_SYNC, 510), np.uint8)
+        c = _hip.ctx()
+        c.check(c.lib.tetra_lmac_compat(c.handle, _hip.ptr(sym), _hip.ptr(ns), C, stride, _hip.ptr(cascade_table()),
+                                        _hip.ptr(nsync), _hip.ptr(rec), _hip.ptr(fbits), _hip.ptr(bbits)),
+                "tetra_lmac_compat")
+        out = []
+        for i in range(C):
+            frames = []
+            for f in range(int(nsync[i])):
+                r = rec[i, f]
+                if not r[_hip.F_VALID]:
+                    continue
+                nb = int(r[_hip.F_NBITS])
+                number = int(r[_hip.F_NUMBER])
+                frame = self._frame_from_device(fbits[i, f, :nb].astype(np.int64), number, r, bbits[i, f])
+                if frame:
+                    frames.append(frame)
+                    logger.info(f"Decoded frame {frame['number']} (type: {frame['type']})")
+            out.append(frames)
+        return out
+
+    def _frame_dict(self, frame_bits, start_pos, frame_number):
+        """The lower-MAC frame dict of decode_frame (decoder.py:898-972)."""
+        pdu = int(frame_bits[0]) * 2 + int(frame_bits[1])
+        enc = int(frame_bits[2]) * 2 + int(frame_bits[3])
+        info = {'description': FRAME_TYPE_DESC.get(pdu, f'Raw type {pdu}')}
+        alg = None
+        if enc in ENC_MODES:
+            alg, info['encryption_mode'] = ENC_MODES[enc]
+        return {
+            'type': pdu,
+            'type_name': FRAME_TYPE_NAMES.get(pdu, f"Type {pdu}"),
+            'number': frame_number,
+            'timeslot': frame_number % 4,
+            'bits': frame_bits,
+            'header': "".join("1" if v else "0" for v in frame_bits[:32]),
+            'position': start_pos,
+            'encrypted': enc > 0,
+            'encryption_algorithm': alg,
+            'key_id': '0',
+            'additional_info': info,
+        }
+
+    def _frame_from_device(self, frame_bits, number, rec, burst_bits):
+        if len(frame_bits) < self.FRAME_LENGTH:
+            return None
+        frame = self._frame_dict(frame_bits, 0, number)
+        crc_ok = bool(rec[_hip.F_CRC])
+        self.protocol_parser.count_burst(crc_ok)
+        burst = burst_from_bits(burst_bits, int(rec[_hip.F_BTYPE]), crc_ok, number % 4,
+                                self.protocol_parser.current_frame_number, self.protocol_parser.colour_code or 0)
+        frame['burst_crc'] = crc_ok
+        return self.upper_mac(frame, burst)
+
+    def decode_frame(self, bits, start_pos, symbols=None, frame_number=0):
+        """Frame header + burst parse of one 510-bit slot (decoder.py:890-992)."""
+        if len(bits) < self.FRAME_LENGTH:
+            return None
+        fb = np.asarray(bits)
+        frame = self._frame_dict(fb, start_pos, frame_number)
+        try:
+            if symbols is None:   # rebuild 0-3 symbols from bit pairs (decoder.py:977-983)
+                b = fb.astype(np.int64)
+                if len(b) % 2:
+                    raise IndexError("index out of range")
+                symbols = (b[0::2] << 1) | b[1::2]
+            burst = self.protocol_parser.parse_burst(np.asarray(symbols), slot_number=frame_number % 4)
+            if burst:
+                frame['burst_crc'] = burst.crc_ok
+                return self.upper_mac(frame, burst)
+        except Exception as e:   # the reference logs and keeps the frame (decoder.py:1102-1103)
+            logger.debug(f"Protocol parsing error: {e}")
+        return frame
+
+    def upper_mac(self, frame, burst):
+        """Hook for the reference's upper MAC / SDS / decryption (decoder.py:994-1117).
+
+        This build stops at the lower MAC and returns the frame unchanged; INTEGRATION.md shows how
+        the reference's own Python parsers attach here."""
+        return frame
+
+    def _etsi_rx(self):
+        if self._etsi is None:
+            from tetraear.core.etsi import EtsiLowerMac
+            self._etsi = EtsiLowerMac()
+        return self._etsi

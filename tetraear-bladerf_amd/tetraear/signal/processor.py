@@ -1,0 +1,279 @@
+"""MI355X SignalProcessor -- the reference's demod surface, computed by libtetra_hip.so.
+
+Surface mirrors /root/reference/tetraear/signal/processor.py:18-273 (same class, attributes,
+method names, argument meaning, return dtypes and swallow-and-continue error behaviour).
+This module only PLANS: it makes the reference's control decisions (decimate or not, filter or
+not, samples per symbol, phase step) and its scipy filter designs, then hands every sample
+computation to the HIP library.  There is no CPU fallback: without the library or a gfx950
+device, the first numeric call raises ``TetraHipError``.
+
+``mode="etsi"`` selects the ETSI EN 300 392-2 receiver (polyphase RRC channel filter, Gardner
+timing recovery, correct pi/4-DQPSK decision with soft bits) instead of the reference-compatible
+("compat") chain; see tetraear.signal.etsi.
+"""
+import functools
+import logging
+import math
+
+import numpy as np
+from scipy import signal as _design   # filter DESIGN only (coefficients), as the reference does
+
+from tetraear import _hip
+
+logger = logging.getLogger(__name__)
+
+SYMBOL_RATE = 18000
+TARGET_RATE = 240000
+# decision thresholds evaluated exactly as processor.py:152-158 writes them
+THRESHOLDS = (-5 * np.pi / 8, -3 * np.pi / 8, 3 * np.pi / 8, 5 * np.pi / 8)
+
+
+def _fmt_of(x):
+    """(library sample format, reference dtype class) for an input array."""
+    if x.dtype in (np.complex64, np.float32):
+        return _hip.TETRA_CF32
+    return _hip.TETRA_CF64
+
+
+def _as_complex(x, fmt):
+    t = np.complex64 if fmt == _hip.TETRA_CF32 else np.complex128
+    return np.ascontiguousarray(x, dtype=t)
+
+
+@functools.lru_cache(maxsize=64)
+def _decimator_design(q):
+    """scipy.signal.decimate's filter (ftype='iir', n=8) in both working precisions."""
+    sos = _design.cheby1(8, 0.05, 0.8 / q, output="sos")
+    out = {}
+    for name, t in (("f32", np.complex64), ("f64", np.complex128)):
+        s = np.asarray(sos, dtype=t)
+        out[name] = (s.real.copy(), _design.sosfilt_zi(s).real.copy())
+    return out
+
+
+@functools.lru_cache(maxsize=64)
+def _lowpass_design(bandwidth, fs):
+    """filter_signal's butter(4) design (processor.py:69-78)."""
+    nyquist = fs / 2
+    cutoff = min(0.99, max(0.01, (bandwidth / 2) / nyquist))
+    b, a = _design.butter(4, cutoff, btype="low")
+    return b, a, _design.lfilter_zi(b, a)
+
+
+def _fill(arr, vals):
+    for i, v in enumerate(np.asarray(vals).ravel()):
+        arr[i] = v
+
+
+def compat_plan(sample_rate, n, fmt, bandwidth=25000):
+    """Build the device plan for process() on n samples (processor.py:239-273 decisions)."""
+    p = _hip.CompatPlan()
+    rate = sample_rate
+    p.q = 0
+    if rate > TARGET_RATE * 2:
+        q = int(rate / TARGET_RATE)
+        if q > 1:
+            if n > 27:   # sosfiltfilt padlen = 3*(2*4+1); decimate raises for len <= 27
+                p.q = q
+                rate = rate / q
+            else:
+                logger.warning("Decimation failed: The length of the input vector x must be greater "
+                               "than padlen, which is 27.")
+    m = -(-n // p.q) if p.q > 1 else n
+    p.dec_f64 = int(fmt == _hip.TETRA_CF64)
+    if p.q > 1:
+        d = _decimator_design(p.q)
+        _fill(p.sos_f32, d["f32"][0])
+        _fill(p.zi_f32, d["f32"][1])
+        _fill(p.sos_f64, d["f64"][0])
+        _fill(p.zi_f64, d["f64"][1])
+    b, a, zi = _lowpass_design(bandwidth, rate)
+    p.ntaps = len(b)
+    p.filt = int(m > 3 * max(len(a), len(b)))
+    if not p.filt:
+        logger.warning("Filter design failed, using unfiltered samples: The length of the input vector x "
+                       "must be greater than padlen, which is %d.", 3 * max(len(a), len(b)))
+    _fill(p.b, b)
+    _fill(p.a, a)
+    _fill(p.lzi, zi)
+    sps = int(rate / SYMBOL_RATE)
+    p.sps = sps if sps > 1 else 1
+    p.phase_step = max(1, sps // 8) if sps > 1 else 1
+    p.fs_dec = rate
+    _fill(p.thr, THRESHOLDS)
+    return p, m, rate
+
+
+def mixer_coefficient(freq_offset):
+    """Imaginary part of -1j*2*np.pi*freq_offset, evaluated as processor.py:99 evaluates it."""
+    c = -1j * 2 * np.pi * freq_offset
+    return float(np.imag(c))
+
+
+class SignalProcessor:
+    """Processes raw IQ samples for TETRA demodulation (processor.py:18)."""
+
+    def __init__(self, sample_rate=2.4e6, mode="compat"):
+        self.sample_rate = sample_rate
+        self.symbol_rate = SYMBOL_RATE
+        self.samples_per_symbol = int(sample_rate / self.symbol_rate)
+        self.symbols = None
+        if mode not in ("compat", "etsi"):
+            raise ValueError("mode must be 'compat' or 'etsi'")
+        self.mode = mode
+        self._etsi = None
+
+    # --------------------------------------------------------------- component methods
+    def resample(self, samples, target_rate):
+        """FFT resampling (processor.py:35-49) -- outside the hot path; delegates to scipy as the
+        reference does."""
+        new_n = int(len(samples) * target_rate / self.sample_rate)
+        return _design.resample(samples, new_n)
+
+    def filter_signal(self, samples, bandwidth=25000, sample_rate=None):
+        """Butterworth-4 filtfilt low-pass (processor.py:51-83), on the GPU."""
+        if len(samples) == 0:
+            return samples
+        fs = sample_rate if sample_rate is not None else self.sample_rate
+        x = np.asarray(samples)
+        try:
+            b, a, zi = _lowpass_design(bandwidth, fs)
+            if len(x) <= 3 * max(len(a), len(b)):
+                raise ValueError("The length of the input vector x must be greater than padlen, "
+                                 f"which is {3 * max(len(a), len(b))}.")
+        except Exception as e:
+            logger.warning(f"Filter design failed, using unfiltered samples: {e}")
+            return samples
+        p, _, _ = compat_plan(fs, len(x), _fmt_of(x), bandwidth)
+        _fill(p.b, b)
+        _fill(p.a, a)
+        _fill(p.lzi, zi)
+        p.ntaps = len(b)
+        fmt = _fmt_of(x)
+        xc = _as_complex(x, fmt)
+        out = np.empty(len(x), np.complex128)
+        c = _hip.ctx()
+        c.check(c.lib.tetra_filtfilt(c.handle, p, _hip.ptr(xc), fmt, 1, len(x), _hip.ptr(out)), "tetra_filtfilt")
+        return out if np.iscomplexobj(x) else out.real.copy()
+
+    def frequency_shift(self, samples, freq_offset, sample_rate=None):
+        """Complex mixer x*exp(-j*2*pi*f*n/fs) (processor.py:85-100), on the GPU."""
+        fs = sample_rate if sample_rate is not None else self.sample_rate
+        x = np.asarray(samples)
+        if len(x) == 0:
+            return np.zeros(0, np.complex128)
+        fmt = _fmt_of(x)
+        xc = _as_complex(x, fmt)
+        out = np.empty(len(x), np.complex128)
+        cf = np.array([mixer_coefficient(freq_offset)], np.float64)
+        c = _hip.ctx()
+        c.check(c.lib.tetra_frequency_shift(c.handle, _hip.ptr(xc), fmt, 1, len(x), _hip.ptr(cf), float(fs),
+                                            _hip.ptr(out)), "tetra_frequency_shift")
+        return out
+
+    def demodulate_dqpsk(self, samples):
+        """Differential decision with the reference's thresholds (processor.py:102-166)."""
+        if self.mode == "etsi":
+            return self._etsi_rx().decide(samples)
+        if len(samples) < 2:
+            return np.array([], dtype=np.uint8)
+        x = np.asarray(samples)
+        fmt = _fmt_of(x)
+        xc = _as_complex(x, fmt)
+        out = np.empty(len(x) - 1, np.uint8)
+        thr = np.array(THRESHOLDS, np.float64)
+        c = _hip.ctx()
+        c.check(c.lib.tetra_demod_dqpsk(c.handle, _hip.ptr(xc), fmt, 1, len(x), _hip.ptr(thr), _hip.ptr(out)),
+                "tetra_demod_dqpsk")
+        return out
+
+    def extract_symbols(self, samples, sample_rate=None):
+        """Best integer sampling phase by mean power, then decimate (processor.py:168-219)."""
+        if len(samples) == 0:
+            return np.array([], dtype=complex)
+        fs = sample_rate if sample_rate is not None else self.sample_rate
+        sps = int(fs / self.symbol_rate)
+        if sps <= 1:
+            return samples
+        x = np.asarray(samples)
+        fmt = _fmt_of(x)
+        xc = _as_complex(x, fmt)
+        smax = len(x) // sps + 1
+        sym = np.empty(smax, xc.dtype)
+        ns = np.zeros(1, np.int32)
+        c = _hip.ctx()
+        c.check(c.lib.tetra_extract_symbols(c.handle, _hip.ptr(xc), fmt, 1, len(x), sps, max(1, sps // 8),
+                                            _hip.ptr(sym), _hip.ptr(ns), None, smax), "tetra_extract_symbols")
+        out = sym[:int(ns[0])]
+        return out if np.iscomplexobj(x) else out.real.astype(x.dtype)
+
+    # --------------------------------------------------------------- pipeline
+    def process(self, samples, freq_offset=0):
+        """Complete demodulation of one chunk (processor.py:221-273); sets ``self.symbols``."""
+        if self.mode == "etsi":
+            hard, self.symbols = self._etsi_rx().process(np.asarray(samples), freq_offset)
+            return hard
+        if len(samples) == 0:
+            self.symbols = np.array([], dtype=complex)
+            return np.array([], dtype=np.uint8)
+        x = np.asarray(samples)
+        real_in = not np.iscomplexobj(x)
+        fmt = _fmt_of(x)
+        xc = _as_complex(x, fmt)
+        plan, m, _ = compat_plan(self.sample_rate, len(x), fmt)
+        smax = m // plan.sps + 1
+        soft = np.empty(smax, np.complex128)
+        hard = np.empty(smax, np.uint8)
+        ns = np.zeros(1, np.int32)
+        f32 = ctypes_int()
+        mc = np.array([mixer_coefficient(freq_offset) if freq_offset != 0 else 0.0], np.float64)
+        mo = np.array([1 if freq_offset != 0 else 0], np.uint8)
+        c = _hip.ctx()
+        c.check(c.lib.tetra_demod_compat(c.handle, plan, _hip.ptr(xc), fmt, 1, len(x), _hip.ptr(mc), _hip.ptr(mo),
+                                         _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(ns), smax, f32),
+                "tetra_demod_compat")
+        n = int(ns[0])
+        if f32.value:
+            sym = soft.view(np.complex64)[:n].copy()
+        else:
+            sym = soft[:n].copy()
+        if real_in and freq_offset == 0:
+            sym = sym.real.copy() if plan.filt else sym.real.astype(np.float32 if fmt == _hip.TETRA_CF32 else np.float64)
+        self.symbols = sym
+        return hard[:max(0, n - 1)].copy()
+
+    def process_batch(self, samples, freq_offsets=None):
+        """process() over a [C, N] batch of independent chunks in one launch sequence.
+
+        Returns (hard [C, S-1] uint8, symbols [C, S] complex128, nsym [C]); row c holds what
+        process(samples[c], freq_offsets[c]) returns / stores in .symbols, in its first
+        nsym[c]-1 / nsym[c] entries."""
+        x = np.asarray(samples)
+        C, N = x.shape
+        fmt = _fmt_of(x)
+        xc = _as_complex(x, fmt)
+        fo = np.zeros(C) if freq_offsets is None else np.asarray(freq_offsets, np.float64)
+        plan, m, _ = compat_plan(self.sample_rate, N, fmt)
+        smax = m // plan.sps + 1
+        soft = np.empty((C, smax), np.complex128)
+        hard = np.empty((C, smax), np.uint8)
+        ns = np.zeros(C, np.int32)
+        f32 = ctypes_int()
+        mc = np.array([mixer_coefficient(f) if f != 0 else 0.0 for f in fo], np.float64)
+        mo = (fo != 0).astype(np.uint8)
+        c = _hip.ctx()
+        c.check(c.lib.tetra_demod_compat(c.handle, plan, _hip.ptr(xc), fmt, C, N, _hip.ptr(mc), _hip.ptr(mo),
+                                         _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(ns), smax, f32),
+                "tetra_demod_compat")
+        return hard, soft, ns
+
+    def _etsi_rx(self):
+        if self._etsi is None:
+            from tetraear.signal.etsi import EtsiReceiver
+            self._etsi = EtsiReceiver(self.sample_rate)
+        return self._etsi
+
+
+def ctypes_int():
+    import ctypes
+    return ctypes.c_int32(0)
