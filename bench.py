@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""Benchmark: sustained IQ Msamples/s through the TETRA receive hot path on 1..N MI355X.
+
+Workload (BASELINE.json configs[4], per rank): C channels x N samples of 2.4 MSps complex64 IQ
+(the reference's drop-in unit: one GUI chunk, /root/reference/tetraear/ui/modern.py:1919), resident
+in HBM before the timed region.  Channels are independent shards: rank r owns its own C channels
+(weak scaling, no data-path collective; 65536 channels at 8 GPUs with the default C=8192).
+
+A step = one pass of the hot path over the rank's batch:
+  --chain etsi   (default) channel filter + pi/4-DQPSK demod with Gardner timing + sync/slicing +
+                 descramble + deinterleave + RCPC Viterbi + CRC  (the north-star chain)
+  --chain compat reference-compatible process() + decode() lower MAC
+
+Launch: python bench.py --gpus 1 --steps 5 --warmup 2
+        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "tetraear-bladerf_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from tetraear import _hip  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+FS = 2.4e6
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--chain", choices=("etsi", "compat"), default=os.environ.get("TETRA_BENCH_CHAIN", "etsi"))
+    ap.add_argument("--channels", type=int, default=8192, help="channels per rank")
+    ap.add_argument("--samples", type=int, default=131072, help="samples per channel chunk")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (rank 0)")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def read_profile(c):
+    names = ctypes.create_string_buffer(4096)
+    ms = (ctypes.c_double * 64)()
+    cnt = (ctypes.c_int64 * 64)()
+    n = ctypes.c_int(0)
+    c.check(c.lib.tetra_profile_read(c.handle, names, 4096, ms, cnt, 64, ctypes.byref(n)), "tetra_profile_read")
+    raw = names.raw.split(b"\0")
+    return {raw[i].decode(): (ms[i], cnt[i]) for i in range(n.value)}
+
+
+class CompatStep:
+    """process() + decode() lower MAC over the batch (tetra_demod_compat + tetra_lmac_compat)."""
+
+    def __init__(self, c, iq, C, N):
+        from tetraear.signal.processor import compat_plan
+        from tetraear.core.decoder import cascade_table
+        self.c, self.C, self.N = c, C, N
+        self.plan, m, _ = compat_plan(FS, N, _hip.TETRA_CF32)
+        self.smax = m // self.plan.sps + 1
+        dev = iq.device
+        self.iq = iq
+        self.mc = torch.zeros(C, dtype=torch.float64, device=dev)
+        self.mo = torch.zeros(C, dtype=torch.uint8, device=dev)
+        self.soft = torch.empty((C, self.smax, 2), dtype=torch.float64, device=dev)
+        self.hard = torch.empty((C, self.smax), dtype=torch.uint8, device=dev)
+        self.hard64 = torch.empty((C, self.smax), dtype=torch.int64, device=dev)
+        self.nsym = torch.empty(C, dtype=torch.int32, device=dev)
+        self.nhard = torch.empty(C, dtype=torch.int32, device=dev)
+        self.kmax = torch.from_numpy(cascade_table().copy()).to(dev)
+        self.nsync = torch.empty(C, dtype=torch.int32, device=dev)
+        self.rec = torch.empty((C, _hip.MAX_SYNC, _hip.F_FIELDS), dtype=torch.int32, device=dev)
+        self.fb = torch.empty((C, _hip.MAX_SYNC, 510), dtype=torch.uint8, device=dev)
+        self.bb = torch.empty((C, _hip.MAX_SYNC, 510), dtype=torch.uint8, device=dev)
+        self.f32 = ctypes.c_int32(0)
+
+    def __call__(self):
+        c = self.c
+        c.check(c.lib.tetra_demod_compat(c.handle, self.plan, _hip.ptr(self.iq), _hip.TETRA_CF32, self.C, self.N,
+                                         _hip.ptr(self.mc), _hip.ptr(self.mo), _hip.ptr(self.soft),
+                                         _hip.ptr(self.hard), _hip.ptr(self.nsym), self.smax, self.f32), "demod")
+        # hard symbols -> int64 stream rows for the lower MAC (torch ops on the same stream)
+        self.hard64.copy_(self.hard)
+        torch.sub(self.nsym, 1, out=self.nhard)
+        self.nhard.clamp_(min=0)
+        c.check(c.lib.tetra_lmac_compat(c.handle, _hip.ptr(self.hard64), _hip.ptr(self.nhard), self.C, self.smax,
+                                        _hip.ptr(self.kmax), _hip.ptr(self.nsync), _hip.ptr(self.rec),
+                                        _hip.ptr(self.fb), _hip.ptr(self.bb)), "lmac")
+
+    def algorithmic_bytes_per_sample(self):
+        # 8 B cf32 in + per symbol (16 B complex128 soft + 1 B hard) + decoded bits (negligible)
+        return 8.0 + 17.0 * 18000.0 / FS
+
+    def dominant(self):
+        return ("compat_sos_fwd", 8.0)   # reads each input sample once (8 B)
+
+    def cpu_baseline(self, budget_s):
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+        import compat as oracle   # the CPU restatement (cpu_baseline leg only)
+        import _signals
+        rng = np.random.default_rng(0)
+        chunks = [_signals.family("tetra", rng, self.N, FS)[0] for _ in range(4)]
+        t0 = time.perf_counter()
+        n = 0
+        while time.perf_counter() - t0 < budget_s:
+            p = oracle.SignalProcessor(FS)
+            h = p.process(chunks[n % 4], 0)
+            oracle.decode_frames(h)
+            n += 1
+        dt = time.perf_counter() - t0
+        return dict(value=n * self.N / dt / 1e6, unit="Msamples/s", cores=1, kind="port",
+                    sample=f"{n} chunks x {self.N} cf32 @2.4 MSps, oracle process()+decode lower MAC, 1 thread")
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    os.environ["TETRA_HIP_DEVICE"] = str(local)
+    c = _hip.ctx()
+    stream = torch.cuda.current_stream(dev)
+    c.check(c.lib.tetra_set_stream(c.handle, ctypes.c_void_p(stream.cuda_stream)), "set_stream")
+
+    C, N = a.channels, a.samples
+    if a.chain == "etsi":
+        from tetraear.signal.etsi import BenchStep as EtsiStep
+        step = EtsiStep(c, C, N, FS, seed=1000 + rank, device=dev)
+    else:
+        g = torch.Generator(device=dev)
+        g.manual_seed(1000 + rank)
+        iq = (0.25 * torch.randn((C, N, 2), generator=g, device=dev, dtype=torch.float32))
+        iq = torch.round(iq * 32768) / 32768   # SC16 grid, like capture.py:259-269
+        step = CompatStep(c, iq, C, N)
+    torch.cuda.synchronize(dev)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    c.check(c.lib.tetra_profile(c.handle, 1), "profile")
+    read_profile(c)   # drop warm-up records
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = read_profile(c)
+    c.check(c.lib.tetra_profile(c.handle, 0), "profile")
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_step = elapsed / a.steps * 1e3
+    total_samples = C * N * world * a.steps
+    value = total_samples / elapsed / 1e6
+
+    if rank == 0:
+        name, per_sample = step.dominant()
+        kms, kcnt = prof.get(name, (0.0, 0))
+        launch_ms = kms / max(1, kcnt)
+        units_per_launch = C * N
+        achieved = per_sample * units_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
+        cpu = None if a.no_cpu else step.cpu_baseline(a.cpu_seconds)
+        out = {
+            "metric": "IQ Msamples/s demod+Viterbi; real-time 25 kHz TETRA channels @1/2/4/8 GPU",
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": step.dtype if hasattr(step, "dtype") else "f32/f64",
+            "data": "synthetic (device-generated, seeded per rank)",
+            "config": {
+                "workload": f"C5 shard: {C} channels x {N} cf32 samples @2.4 MSps per GPU, chain={a.chain}",
+                "channels_per_gpu": C, "samples_per_channel": N, "sample_rate": FS,
+                "parallelism": f"channel-sharded x{world}",
+            },
+            "realtime_channels": int(value * 1e6 / FS),
+            "roofline": {
+                "bound": "hbm", "kernel": name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "launch_ms": round(launch_ms, 4), "algorithmic_bytes_per_launch": per_sample * units_per_launch,
+            },
+            "stages_ms_per_step": {k: round(v[0] / a.steps, 4) for k, v in prof.items()},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -58,6 +58,13 @@ int tetra_synchronize(tetra_ctx *ctx);
 /* Device name / arch of the context's device (e.g. "gfx950"). */
 int tetra_device_arch(tetra_ctx *ctx, char *buf, size_t n);
 
+/* Per-stage device timing: when enabled, every kernel stage is bracketed by HIP events on the
+ * context stream.  tetra_profile_read() synchronizes, then returns the accumulated milliseconds
+ * and launch counts per stage since the previous read (names NUL-separated, in first-seen order). */
+int tetra_profile(tetra_ctx *ctx, int enable);
+int tetra_profile_read(tetra_ctx *ctx, char *names, size_t names_len, double *ms, int64_t *count,
+                       int max_stages, int *n_stages);
+
 /* =====================================================================================
  * Compat demod -- bit-compatible with SignalProcessor (processor.py:221-273)
  * ===================================================================================== */

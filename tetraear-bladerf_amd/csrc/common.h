@@ -25,7 +25,15 @@ enum Slot {
     S_COUNT
 };
 
+struct ProfRec {
+    const char *name;
+    hipEvent_t a, b;
+};
+
 struct tetra_ctx {
+    bool prof = false;                 // per-stage HIP-event timing (tetra_profile)
+    std::vector<ProfRec> recs;
+    std::vector<hipEvent_t> ev_pool;
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = true;
@@ -64,6 +72,19 @@ struct Staging {
     void *out(void *p, size_t bytes);
     int finish();   // D2H copies (if any) + stream sync when host memory was involved
 };
+
+// Brackets the kernels launched in its scope with HIP events on the context stream when
+// profiling is on: the device time of each named stage, measured on the stream it runs on.
+struct ProfScope {
+    tetra_ctx *c;
+    const char *name;
+    hipEvent_t a = nullptr;
+    ProfScope(tetra_ctx *ctx, const char *n);
+    ~ProfScope();
+};
+#define PROF_CAT2(a, b) a##b
+#define PROF_CAT(a, b) PROF_CAT2(a, b)
+#define PROF(ctx, name) ProfScope PROF_CAT(prof_scope_, __LINE__)((ctx), (name))
 
 static inline unsigned grid_for(size_t threads, unsigned block) {
     return (unsigned)((threads + block - 1) / block);

@@ -421,10 +421,16 @@ int run_decimate(tetra_ctx *ctx, const tetra_compat_plan *P, const T *x, Lay lx,
     for (int i = 0; i < 8; ++i) hc[24 + i] = std::is_same<T, float>::value ? (T)P->zi_f32[i] : (T)P->zi_f64[i];
     HIP_TRY(ctx, hipMemcpyAsync(coef, hc, sizeof hc, hipMemcpyHostToDevice, ctx->stream));
     const unsigned blk = 64;
-    hipLaunchKernelGGL(k_sos_fwd<T>, dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, x, lx, C, N, pad,
+    {
+        PROF(ctx, "compat_sos_fwd");
+        hipLaunchKernelGGL(k_sos_fwd<T>, dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, x, lx, C, N, pad,
                        coef, coef + 24, scr, grouped(L));
-    hipLaunchKernelGGL(k_sos_bwd<T>, dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, scr, grouped(L), C,
+    }
+    {
+        PROF(ctx, "compat_sos_bwd");
+        hipLaunchKernelGGL(k_sos_bwd<T>, dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, scr, grouped(L), C,
                        N, pad, P->q, coef, coef + 24, out, lo);
+    }
     return TETRA_OK;
 }
 
@@ -442,16 +448,23 @@ int run_filtfilt(tetra_ctx *ctx, const tetra_compat_plan *P, const TIn *x, Lay l
     for (int k = 0; k < nt - 1; ++k) hc[2 * MAXTAP + k] = P->lzi[k];
     HIP_TRY(ctx, hipMemcpyAsync(coef, hc, sizeof hc, hipMemcpyHostToDevice, ctx->stream));
     const unsigned blk = 64;
-    hipLaunchKernelGGL(k_lf_fwd<TIn>, dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, x, lx, C, M, pad,
+    {
+        PROF(ctx, "compat_filtfilt_fwd");
+        hipLaunchKernelGGL(k_lf_fwd<TIn>, dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, x, lx, C, M, pad,
                        nt, coef, coef + MAXTAP, coef + 2 * MAXTAP, mixc, mixon, P->fs_dec, scr, grouped(L));
-    hipLaunchKernelGGL(k_lf_bwd, dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, scr, grouped(L), C, M,
+    }
+    {
+        PROF(ctx, "compat_filtfilt_bwd");
+        hipLaunchKernelGGL(k_lf_bwd, dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, scr, grouped(L), C, M,
                        pad, nt, coef, coef + MAXTAP, coef + 2 * MAXTAP, out, lo);
+    }
     return TETRA_OK;
 }
 
 template <typename T>
 void launch_extract(tetra_ctx *ctx, const T *y, Lay ly, int C, long M, int sps, int step, T *sym, long smax,
                     int32_t *nsym, int32_t *bph) {
+    PROF(ctx, "compat_extract");
     hipLaunchKernelGGL(k_extract<T>, dim3(grid_for((size_t)16 * C, 256)), dim3(256), 0, ctx->stream, y, ly, C, M, sps,
                        step, sym, smax, nsym, bph);
 }
@@ -459,6 +472,7 @@ void launch_extract(tetra_ctx *ctx, const T *y, Lay ly, int C, long M, int sps, 
 template <typename T>
 void launch_demod(tetra_ctx *ctx, const T *sym, long stride, int C, const int32_t *nsym, long S_all,
                   const double *thr, uint8_t *hard, long hstride) {
+    PROF(ctx, "compat_demod");
     hipLaunchKernelGGL(k_demod<T>, dim3(C), dim3(64), 0, ctx->stream, sym, stride, C, nsym, S_all, thr[0], thr[1],
                        thr[2], thr[3], hard, hstride);
 }

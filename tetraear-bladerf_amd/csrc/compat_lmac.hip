@@ -346,6 +346,7 @@ int tetra_lmac_compat(tetra_ctx *ctx, const int64_t *sym, const int32_t *nsym, s
     uint8_t *fb = (uint8_t *)st.out(frame_bits, C * TETRA_MAX_SYNC * 510);
     uint8_t *bb = (uint8_t *)st.out(burst_bits, C * TETRA_MAX_SYNC * 510);
     if (!s || !n || !k || !ns || !r || !fb || !bb) return st.finish();
+    PROF(ctx, "compat_lmac");
     hipLaunchKernelGGL(k_lmac, dim3((unsigned)C), dim3(64), 0, ctx->stream, s, n, (int)C, (long)stride, k, ns, r, fb, bb);
     return st.finish();
 }

@@ -85,7 +85,73 @@ int Staging::finish() {
     return TETRA_OK;
 }
 
+static hipEvent_t take_event(tetra_ctx *c) {
+    if (!c->ev_pool.empty()) {
+        hipEvent_t e = c->ev_pool.back();
+        c->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+ProfScope::ProfScope(tetra_ctx *ctx, const char *n) : c(ctx), name(n) {
+    if (c && c->prof) {
+        a = take_event(c);
+        if (a) (void)hipEventRecord(a, c->stream);
+    }
+}
+
+ProfScope::~ProfScope() {
+    if (!a) return;
+    hipEvent_t b = take_event(c);
+    if (!b) return;
+    (void)hipEventRecord(b, c->stream);
+    c->recs.push_back({name, a, b});
+}
+
 extern "C" {
+
+int tetra_profile(tetra_ctx *ctx, int enable) {
+    if (!ctx) return TETRA_E_INVALID;
+    ctx->prof = enable != 0;
+    return TETRA_OK;
+}
+
+int tetra_profile_read(tetra_ctx *ctx, char *names, size_t names_len, double *ms, int64_t *count, int max_stages,
+                       int *n_stages) {
+    if (!ctx || !n_stages) return TETRA_E_INVALID;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    std::vector<std::string> nm;
+    std::vector<double> acc;
+    std::vector<int64_t> cnt;
+    for (auto &r : ctx->recs) {
+        float t = 0.f;
+        (void)hipEventElapsedTime(&t, r.a, r.b);
+        size_t i = 0;
+        while (i < nm.size() && nm[i] != r.name) ++i;
+        if (i == nm.size()) { nm.push_back(r.name); acc.push_back(0); cnt.push_back(0); }
+        acc[i] += t;
+        cnt[i] += 1;
+        ctx->ev_pool.push_back(r.a);
+        ctx->ev_pool.push_back(r.b);
+    }
+    ctx->recs.clear();
+    size_t off = 0;
+    int n = 0;
+    for (size_t i = 0; i < nm.size() && n < max_stages; ++i, ++n) {
+        if (ms) ms[n] = acc[i];
+        if (count) count[n] = cnt[i];
+        if (names && off + nm[i].size() + 1 < names_len) {
+            memcpy(names + off, nm[i].c_str(), nm[i].size() + 1);
+            off += nm[i].size() + 1;
+        }
+    }
+    if (names && off < names_len) names[off] = 0;
+    *n_stages = n;
+    return TETRA_OK;
+}
 
 int tetra_abi_version(void) { return TETRA_ABI_VERSION; }
 
@@ -126,6 +192,8 @@ void tetra_destroy(tetra_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (auto &r : ctx->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+    for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
     for (auto &b : ctx->slot)
         if (b.p) (void)hipFree(b.p);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);

@@ -56,6 +56,8 @@ def _bind(L):
         "tetra_set_stream": (_i32, [_vp, _vp]),
         "tetra_synchronize": (_i32, [_vp]),
         "tetra_device_arch": (_i32, [_vp, ctypes.c_char_p, _sz]),
+        "tetra_profile": (_i32, [_vp, _i32]),
+        "tetra_profile_read": (_i32, [_vp, ctypes.c_char_p, _sz, _vp, _vp, _i32, _i32p]),
         "tetra_compat_symbols": (ctypes.c_int64, [ctypes.POINTER(CompatPlan), _sz]),
         "tetra_demod_compat": (_i32, [_vp, ctypes.POINTER(CompatPlan), _vp, _i32, _sz, _sz, _vp, _vp, _vp, _vp, _vp,
                                       _sz, _i32p]),
