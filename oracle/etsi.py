@@ -1,0 +1,254 @@
+"""CPU oracle for the ETSI receive chain + a transmitter for round-trip tests (TEST INFRASTRUCTURE).
+
+PARITY UNPINNED against the reference: /root/reference has no descrambler, deinterleaver, Viterbi,
+Gardner or polyphase channel filter.  This oracle is pinned instead by
+  * known answers: CRC-16 check value 0xD64E for "123456789", residue 0x1D0F;
+  * transmitter -> receiver round trips (tests/test_etsi_oracle.py);
+and the HIP kernels are checked against it (bit-exact coding, soft symbols within 1e-5).
+Restated spec: EN 300 392-2 §5.3, §8.2.3-§8.2.5, §9.4.4 (see etsi_oracle.c header).
+"""
+import ctypes
+import os
+
+import numpy as np
+from scipy import signal as _design
+
+from compat import lib as _lib_loader  # same liboracle.so
+
+FS_NOMINAL = 2.4e6
+SYMBOL_RATE = 18000.0
+KIND = {"SCH/F": 0, "SCH/HD": 1, "BSCH": 2}
+KIND_PARAMS = {0: (432, 103, 288, 268), 1: (216, 101, 144, 124), 2: (120, 11, 80, 60)}  # K, a, n2, n1
+BURST_NDB_N, BURST_NDB_P, BURST_SB = 0, 1, 2
+
+Q_BITS = np.array([1, 0, 1, 1, 0, 1, 1, 1, 0, 0, 0, 0, 0, 1, 1, 0, 1, 0, 1, 1, 0, 1], np.uint8)
+N_BITS = np.array([1, 1, 0, 1, 0, 0, 0, 0, 1, 1, 1, 0, 1, 0, 0, 1, 1, 1, 0, 1, 0, 0], np.uint8)
+P_BITS = np.array([0, 1, 1, 1, 1, 0, 1, 0, 0, 1, 0, 0, 0, 0, 1, 1, 0, 1, 1, 1, 0, 0], np.uint8)
+Y_BITS = np.array([1, 1, 0, 0, 0, 0, 0, 1, 1, 0, 0, 1, 1, 1, 0, 0, 1, 1, 1, 0, 1, 0, 0, 1, 1, 1, 0, 0, 0, 0,
+                   0, 1, 1, 0, 0, 1, 1, 1], np.uint8)
+F_BITS = np.array([1] * 8 + [0] * 64 + [1] * 8, np.uint8)
+
+_bound = False
+
+
+def lib():
+    global _bound
+    L = _lib_loader()
+    if not _bound:
+        f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+        u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+        i8p = np.ctypeslib.ndpointer(np.int8, flags="C_CONTIGUOUS")
+        i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+        L.eo_scramble_seq.argtypes = [ctypes.c_uint32, ctypes.c_int, u8p]
+        L.eo_scramble_init.argtypes = [ctypes.c_uint32] * 3
+        L.eo_scramble_init.restype = ctypes.c_uint32
+        L.eo_crc16_reg.argtypes = [u8p, ctypes.c_int]
+        L.eo_crc16_reg.restype = ctypes.c_uint32
+        L.eo_encode_block.argtypes = [u8p, ctypes.c_int, u8p, u8p]
+        L.eo_decode_block.argtypes = [i8p, ctypes.c_int, u8p, u8p]
+        L.eo_decode_block.restype = ctypes.c_int
+        L.eo_viterbi.argtypes = [i8p, ctypes.c_int, u8p]
+        L.eo_chanfilt.argtypes = [f32p, ctypes.c_int, f32p, ctypes.c_int, ctypes.c_int, f32p, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_int, f32p, f32p]
+        L.eo_chanfilt.restype = ctypes.c_int
+        L.eo_timing.argtypes = [f32p, ctypes.c_int, ctypes.c_float, ctypes.c_float, f32p, f32p, i8p, u8p,
+                                ctypes.c_int, f32p]
+        L.eo_timing.restype = ctypes.c_int
+        L.eo_sync.argtypes = [u8p, ctypes.c_int, i32p, i32p, ctypes.c_int]
+        L.eo_sync.restype = ctypes.c_int
+        _bound = True
+    return L
+
+
+# ------------------------------------------------------------------------------ design
+
+def rrc(t, alpha=0.35):
+    t = np.asarray(t, np.float64)
+    out = np.empty_like(t)
+    z = np.abs(t) < 1e-9
+    out[z] = 1.0 - alpha + 4 * alpha / np.pi
+    s = np.abs(np.abs(4 * alpha * t) - 1.0) < 1e-9
+    out[s] = (alpha / np.sqrt(2)) * ((1 + 2 / np.pi) * np.sin(np.pi / (4 * alpha))
+                                     + (1 - 2 / np.pi) * np.cos(np.pi / (4 * alpha)))
+    o = ~(z | s)
+    tt = t[o]
+    out[o] = (np.sin(np.pi * tt * (1 - alpha)) + 4 * alpha * tt * np.cos(np.pi * tt * (1 + alpha))) / \
+        (np.pi * tt * (1 - (4 * alpha * tt) ** 2))
+    return out
+
+
+def design(fs=FS_NOMINAL):
+    """Receiver constants: stage-1 decimator taps, RRC polyphase prototype, loop constants."""
+    q1 = int(round(fs / 240000.0))
+    if abs(q1 * 240000.0 - fs) > 1e-6 or q1 < 1:
+        raise ValueError("ETSI receiver needs fs = q * 240 kHz")
+    L1 = 48 if q1 > 1 else 1
+    h1 = (_design.firwin(L1, 60e3, fs=fs, window=("kaiser", 6.0)) if q1 > 1 else np.ones(1)).astype(np.float32)
+    Lp = 321
+    hp = rrc((np.arange(Lp) - (Lp - 1) / 2) / 40.0, 0.35).astype(np.float32)
+    return dict(q1=q1, L1=L1, h1=h1, Lp=Lp, hp=hp, up=3, down=10, gain=np.float32(1.5), soft_scale=np.float32(64.0))
+
+
+def scramble_seq(init, n=432):
+    out = np.empty(n, np.uint8)
+    lib().eo_scramble_seq(init, n, out)
+    return out
+
+
+def scramble_init(mcc, mnc, cc):
+    return int(lib().eo_scramble_init(mcc, mnc, cc))
+
+
+def crc16_reg(bits):
+    b = np.ascontiguousarray(np.asarray(bits) & 1, np.uint8)
+    return int(lib().eo_crc16_reg(b, len(b)))
+
+
+# ------------------------------------------------------------------------------ transmitter
+
+def encode_block(type1, kind, scr):
+    K = KIND_PARAMS[kind][0]
+    out = np.empty(K, np.uint8)
+    lib().eo_encode_block(np.ascontiguousarray(type1, np.uint8), kind, np.ascontiguousarray(scr[:K], np.uint8), out)
+    return out
+
+
+def make_burst(btype, rng, cell_scr, payloads=None):
+    """One 510-bit continuous-downlink burst; returns (bits, [(kind, type1), ...])."""
+    bb = rng.integers(0, 2, 30).astype(np.uint8)
+    head, tail, h2 = Q_BITS[10:22], Q_BITS[0:10], np.zeros(2, np.uint8)
+    jobs = []
+
+    def payload(kind):
+        n1 = KIND_PARAMS[kind][3]
+        return rng.integers(0, 2, n1).astype(np.uint8) if payloads is None else payloads.pop(0)
+
+    if btype == BURST_SB:
+        t_b = payload(2)
+        t_h = payload(1)
+        sb1 = encode_block(t_b, 2, scramble_seq(3, 120))
+        bk2 = encode_block(t_h, 1, cell_scr)
+        bits = np.concatenate([head, h2, F_BITS, sb1, Y_BITS, bb, bk2, h2, tail])
+        jobs = [(2, t_b), (1, t_h)]
+    elif btype == BURST_NDB_N:
+        t_f = payload(0)
+        blk = encode_block(t_f, 0, cell_scr)
+        bits = np.concatenate([head, h2, blk[:216], bb[:14], N_BITS, bb[14:], blk[216:], h2, tail])
+        jobs = [(0, t_f)]
+    else:
+        t1, t2 = payload(1), payload(1)
+        b1 = encode_block(t1, 1, cell_scr)
+        b2 = encode_block(t2, 1, cell_scr)
+        bits = np.concatenate([head, h2, b1, bb[:14], P_BITS, bb[14:], b2, h2, tail])
+        jobs = [(1, t1), (1, t2)]
+    assert len(bits) == 510
+    return bits, jobs
+
+
+def burst_stream(rng, nbursts, cell_scr, kinds=None):
+    bits, jobs = [], []
+    for i in range(nbursts):
+        bt = kinds[i % len(kinds)] if kinds is not None else int(rng.choice([0, 0, 1, 2]))
+        b, j = make_burst(bt, rng, cell_scr)
+        bits.append(b)
+        jobs.append((bt, j))
+    return np.concatenate(bits), jobs
+
+
+def modulate(bits, n, fs=FS_NOMINAL, t0=0.0, phase0=0.0, cfo=0.0, snr_db=None, rng=None, amp=0.5, span=6):
+    """pi/4-DQPSK (Table 5.1) with RRC(0.35) pulses sampled at fs; sample n is at symbol time
+    t0 + n*18000/fs (symbols counted from the first dibit)."""
+    d = np.asarray(bits, np.int64).reshape(-1, 2)
+    step = np.where(d[:, 0] == 0, np.where(d[:, 1] == 0, 1, 3), np.where(d[:, 1] == 0, -1, -3))  # x pi/4
+    ph = phase0 + np.pi / 4 * np.cumsum(step)
+    sym = np.exp(1j * ph)
+    t = t0 + np.arange(n) * (SYMBOL_RATE / fs)
+    k0 = np.floor(t).astype(np.int64)
+    x = np.zeros(n, np.complex128)
+    for dd in range(-span, span + 1):
+        k = k0 + dd
+        ok = (k >= 0) & (k < len(sym))
+        x[ok] += sym[k[ok]] * rrc(t[ok] - k[ok])
+    x *= amp
+    if cfo:
+        x *= np.exp(2j * np.pi * cfo * np.arange(n) / fs)
+    if snr_db is not None:   # Es/N0: N0 = (P * Ts) / 10^(snr/10), per-sample variance N0 * fs
+        p = np.mean(np.abs(x) ** 2)
+        sigma = np.sqrt(p * (fs / SYMBOL_RATE) / 10 ** (snr_db / 10) / 2)
+        x += sigma * (rng.standard_normal(n) + 1j * rng.standard_normal(n))
+    return x.astype(np.complex64)
+
+
+# ------------------------------------------------------------------------------ receiver
+
+class Receiver:
+    def __init__(self, fs=FS_NOMINAL):
+        self.fs = fs
+        self.d = design(fs)
+
+    def chanfilt(self, x):
+        d = self.d
+        x = np.ascontiguousarray(np.asarray(x, np.complex64)).view(np.float32)
+        N = len(x) // 2
+        M1 = max(0, (N - d["L1"]) // d["q1"] + 1)
+        x240 = np.zeros(2 * max(M1, 1), np.float32)
+        y = np.zeros(2 * max(M1 * 3 // 10 + 2, 1), np.float32)
+        M2 = lib().eo_chanfilt(x, N, d["h1"], d["L1"], d["q1"], d["hp"], d["Lp"], d["up"], d["down"], x240, y)
+        return y[:2 * M2].view(np.complex64).copy()
+
+    def timing(self, y):
+        d = self.d
+        yv = np.ascontiguousarray(np.asarray(y, np.complex64)).view(np.float32)
+        M2 = len(yv) // 2
+        smax = M2 // 4 + 2
+        sym = np.zeros(2 * smax, np.float32)
+        dscr = np.zeros(2 * smax, np.float32)
+        soft = np.zeros(2 * smax, np.int8)
+        hard = np.zeros(smax, np.uint8)
+        diag = np.zeros(4, np.float32)
+        S = lib().eo_timing(yv, M2, d["gain"], d["soft_scale"], sym, dscr, soft, hard, smax, diag)
+        return (sym[:2 * S].view(np.complex64).copy(), soft[:2 * max(S - 1, 0)].copy(),
+                hard[:max(S - 1, 0)].copy(), diag)
+
+    def demod(self, x):
+        return self.timing(self.chanfilt(x))
+
+    @staticmethod
+    def hard_bits(hard):
+        h = np.asarray(hard, np.uint8)
+        return np.stack([(h >> 1) & 1, h & 1], axis=1).reshape(-1).astype(np.uint8)
+
+    def sync(self, hard, maxb=8):
+        bits = np.ascontiguousarray(self.hard_bits(hard))
+        starts = np.zeros(maxb, np.int32)
+        kinds = np.zeros(maxb, np.int32)
+        n = lib().eo_sync(bits, len(bits), starts, kinds, maxb)
+        return list(zip(starts[:n].tolist(), kinds[:n].tolist()))
+
+    @staticmethod
+    def decode_block(soft5, kind, scr):
+        n1 = KIND_PARAMS[kind][3]
+        out = np.zeros(288, np.uint8)
+        ok = lib().eo_decode_block(np.ascontiguousarray(soft5, np.int8), kind,
+                                   np.ascontiguousarray(scr[:KIND_PARAMS[kind][0]], np.uint8), out)
+        return out[:n1].copy(), bool(ok)
+
+    def lower_mac(self, softbits, hard, cell_init):
+        """Bursts -> decoded blocks: [(start, burst_kind, [(kind, type1, crc_ok), ...])]."""
+        cell = scramble_seq(cell_init, 432)
+        bsch = scramble_seq(3, 120)
+        out = []
+        for s, bk in self.sync(hard):
+            sb = np.asarray(softbits, np.int8)
+            blocks = []
+            if bk == BURST_NDB_N:
+                blocks.append((0, np.concatenate([sb[s + 14:s + 230], sb[s + 282:s + 498]]), cell))
+            elif bk == BURST_NDB_P:
+                blocks.append((1, sb[s + 14:s + 230], cell))
+                blocks.append((1, sb[s + 282:s + 498], cell))
+            else:
+                blocks.append((2, sb[s + 94:s + 214], bsch))
+                blocks.append((1, sb[s + 282:s + 498], cell))
+            dec = [(k,) + self.decode_block(v, k, scr) for k, v, scr in blocks]
+            out.append((s, bk, dec))
+        return out

@@ -1,0 +1,62 @@
+"""CPU: pin the ETSI oracle (no reference counterpart exists -- parity unpinned vs reference).
+
+Known answers + encoder->decoder round trips + full IQ round trips through the oracle receiver."""
+import numpy as np
+import pytest
+
+import etsi as E
+
+
+def test_crc16_known_answers():
+    kat = np.array([(x >> (7 - k)) & 1 for x in b"123456789" for k in range(8)], np.uint8)
+    assert E.crc16_reg(kat) == 0x29B1                 # CCITT-FALSE register
+    assert E.crc16_reg(kat) ^ 0xFFFF == 0xD64E        # ones' complement (CRC-16/GENIBUS check value)
+    c = E.crc16_reg(kat) ^ 0xFFFF
+    full = np.concatenate([kat, [(c >> (15 - k)) & 1 for k in range(16)]]).astype(np.uint8)
+    assert E.crc16_reg(full) == 0x1D0F                # residue of a valid codeword
+
+
+def test_scrambler_properties():
+    assert E.scramble_init(0, 0, 0) == 3               # BSCH: colour code 0 with the two leading 1s
+    s = E.scramble_seq(E.scramble_init(262, 1, 5), 4096)
+    assert 0.45 < s.mean() < 0.55
+    assert not np.array_equal(s[:432], E.scramble_seq(E.scramble_init(262, 1, 6), 432))
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_block_round_trip_with_errors(kind):
+    rng = np.random.default_rng(kind)
+    K, a, n2, n1 = E.KIND_PARAMS[kind]
+    scr = E.scramble_seq(E.scramble_init(901, 77, 12) if kind != 2 else 3, K)
+    for trial in range(30):
+        t1 = rng.integers(0, 2, n1).astype(np.uint8)
+        t5 = E.encode_block(t1, kind, scr)
+        soft = np.where(t5 == 0, 40, -40).astype(np.int8)
+        flip = rng.choice(K, int(0.01 * K), replace=False)
+        soft[flip] = -soft[flip]
+        dec, ok = E.Receiver.decode_block(soft, kind, scr)
+        assert ok and np.array_equal(dec, t1)
+    fails = 0
+    for trial in range(30):   # noise must (almost always) fail the CRC
+        garbage = rng.integers(-60, 61, K).astype(np.int8)
+        fails += not E.Receiver.decode_block(garbage, kind, scr)[1]
+    assert fails >= 29
+
+
+@pytest.mark.parametrize("snr", [None, 15.0])
+def test_iq_round_trip(snr):
+    rng = np.random.default_rng(11)
+    cell = E.scramble_init(262, 1, 5)
+    bits, jobs = E.burst_stream(rng, 6, E.scramble_seq(cell))
+    rx = E.Receiver()
+    for t0 in (3.0, 3.41, 5.9):
+        x = E.modulate(bits, 131072, t0=t0, phase0=rng.uniform(0, 6.28), cfo=rng.uniform(-600, 600),
+                       snr_db=snr, rng=rng)
+        sym, soft, hard, diag = rx.demod(x)
+        assert 960 < len(sym) < 990
+        res = rx.lower_mac(soft, hard, cell)
+        assert len(res) >= 2
+        sent = [tuple(t) for _, jj in jobs for _, t in jj]
+        for _, _, dec in res:
+            for kind, t1, ok in dec:
+                assert ok and tuple(t1) in sent
