@@ -171,6 +171,68 @@ int tetra_crc16(tetra_ctx *ctx, const uint8_t *bits, size_t F, size_t L, int rev
 /* _check_crc over F rows of L bits: ok [F]. */
 int tetra_check_crc(tetra_ctx *ctx, const uint8_t *bits, size_t F, size_t L, uint8_t *ok);
 
+/* =====================================================================================
+ * ETSI EN 300 392-2 receive chain (north star; no reference counterpart)
+ * ===================================================================================== */
+
+/* Receiver design (filled by the host: tetraear.signal.etsi.etsi_plan).  Supported: input at
+ * q1 * 240 kHz with q1 = 10 (2.4 MSps), stage-1 48-tap decimator, stage-2 RRC (0.35) prototype at
+ * 720 kHz resampled x3/10 to 72 kHz (4 samples/symbol). */
+typedef struct tetra_etsi_plan {
+    int32_t q1, L1, Lp, up, down;
+    float gain;           /* block-Gardner loop gain */
+    float soft_scale;     /* int8 soft-bit scale: soft = rint(x * soft_scale / mean|d|) */
+    int32_t reserved;
+    float h1[64];
+    float hp[384];
+} tetra_etsi_plan;
+
+#define TETRA_ETSI_MAXB 8    /* bursts per channel chunk */
+#define TETRA_ETSI_MAXJ 16   /* coded blocks per channel chunk */
+/* block kinds */
+enum { TETRA_SCH_F = 0, TETRA_SCH_HD = 1, TETRA_BSCH = 2 };
+/* burst kinds */
+enum { TETRA_NDB_N = 0, TETRA_NDB_P = 1, TETRA_SB = 2 };
+
+/* M1 (240 kHz samples), M2 (72 kHz samples) and the symbol capacity smax for N input samples. */
+int tetra_etsi_lengths(const tetra_etsi_plan *plan, size_t N, int64_t *M1, int64_t *M2, int64_t *smax);
+/* Channel filter + RRC resampler: iq [C][N] cf32 -> y [C][M2] cf32. */
+int tetra_etsi_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *plan, const void *iq, size_t C, size_t N, void *y);
+/* Timing recovery + differential decision: y [C][M2] ->
+ *   soft [C][smax] cf32 symbol-spaced samples (the ETSI `.symbols`), softbits [C][2*smax] int8
+ *   (>0: bit 0), hard [C][smax] dibit symbols 0..3 (count nsym-1), nsym [C],
+ *   diag [C][4] (timing phase, final Gardner correction, CFO rotation re/im) or NULL. */
+int tetra_etsi_timing(tetra_ctx *ctx, const tetra_etsi_plan *plan, const void *y, size_t C, size_t M2,
+                      void *soft, int8_t *softbits, uint8_t *hard, int32_t *nsym, size_t smax, float *diag);
+/* Fused demod (chanfilt + timing) over a batch. */
+int tetra_demod_etsi(tetra_ctx *ctx, const tetra_etsi_plan *plan, const void *iq, size_t C, size_t N,
+                     void *soft, int8_t *softbits, uint8_t *hard, int32_t *nsym, size_t smax, float *diag);
+/* Cell configuration: scrambling code init per channel ((MCC<<20|MNC<<6|CC)<<2|3). */
+int tetra_etsi_set_cells(tetra_ctx *ctx, const uint32_t *scramb_init, size_t C);
+/* Lower MAC: burst sync + descramble + deinterleave + depuncture + Viterbi + CRC per channel.
+ *   nburst [C], bursts [C][TETRA_ETSI_MAXB][2] (start bit, burst kind),
+ *   nblock [C], blocks [C][TETRA_ETSI_MAXJ][4] (block kind, crc_ok, burst index, block index),
+ *   type1 [C][TETRA_ETSI_MAXJ][268] decoded type-1 bits. */
+int tetra_lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard, const int32_t *nsym,
+                    size_t C, size_t smax, int32_t *nburst, int32_t *bursts, int32_t *nblock,
+                    int32_t *blocks, uint8_t *type1);
+/* Component: decode F type-5 soft blocks of one kind (K = 432/216/120): type1 [F][n1], crc_ok [F]. */
+int tetra_etsi_decode_blocks(tetra_ctx *ctx, const int8_t *soft5, size_t F, int kind,
+                             const uint32_t *scramb_init, uint8_t *type1, uint8_t *crc_ok);
+/* Component: encode F type-1 blocks (CRC, tail, RCPC 2/3, interleave, scramble): type5 [F][K]. */
+int tetra_etsi_encode_blocks(tetra_ctx *ctx, const uint8_t *type1, size_t F, int kind,
+                             const uint32_t *scramb_init, uint8_t *type5);
+
+/* Synthetic capture generator (device side; bench.py and tests).  Per channel: a continuous
+ * downlink of coded bursts (1/2 normal-n, 1/4 normal-p, 1/4 sync), pi/4-DQPSK + RRC(0.35) at fs,
+ * random carrier phase, CFO uniform in [-cfo_max, cfo_max] Hz, AWGN at Es/N0 = snr_db (no noise if
+ * snr_db >= 200), SC16 quantisation.  Outputs: iq [C][N] cf32, cell_init [C] scrambling inits,
+ * and optionally kinds [C][NB] burst kinds, payload [C][NB][2][268] type-1 bits (zero-padded),
+ * t0 [C] symbol time of sample 0; NB = tetra_synth_bursts_per_channel(N, fs). */
+int tetra_synth_bursts_per_channel(size_t N, double fs);
+int tetra_synth_etsi(tetra_ctx *ctx, size_t C, size_t N, double fs, uint64_t seed, float snr_db, float cfo_max,
+                     void *iq, uint32_t *cell_init, int32_t *kinds, uint8_t *payload, double *t0);
+
 #ifdef __cplusplus
 }
 #endif

@@ -212,6 +212,22 @@ static float wave_sum(float *v)
 
 static const float K6 = 1.0f / 6.0f;
 
+/* atan2 from IEEE basic operations only (max error ~1e-5 rad), so the timing phase is computed
+ * bit-identically by this oracle and by the HIP kernel (libm atan2 implementations differ). */
+static float pat2(float y, float x)
+{
+    float ax = fabsf(x), ay = fabsf(y);
+    float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    float a = mx == 0.0f ? 0.0f : mn / mx;
+    float s = a * a;
+    float r = fmaf(fmaf(fmaf(fmaf(fmaf(-0.0117212f, s, 0.05265332f), s, -0.11643287f), s, 0.19354346f), s,
+                        -0.33262347f), s, 0.99997726f) * a;
+    if (ay > ax) r = 1.57079637f - r;
+    if (x < 0.0f) r = 3.14159274f - r;
+    if (y < 0.0f) r = -r;
+    return r;
+}
+
 static void interp(const float *y, float t, float *o)
 {
     float fi = floorf(t);
@@ -272,7 +288,7 @@ int eo_timing(const float *y, int M2, float gain, float soft_scale, float *soft_
         }
     }
     float Xr = acc[0] - acc[2], Xi = acc[3] - acc[1];
-    float p = -0.63661977236758134f * atan2f(Xi, Xr);   /* -(2/pi) arg X */
+    float p = -0.63661977236758134f * pat2(Xi, Xr);   /* -(2/pi) arg X */
     float base = p < 0.0f ? p + 4.0f : p;
     if (base >= 4.0f) base -= 4.0f;
     int kstart = base >= 3.0f ? 0 : 1;

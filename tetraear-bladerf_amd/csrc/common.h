@@ -34,6 +34,7 @@ struct tetra_ctx {
     bool prof = false;                 // per-stage HIP-event timing (tetra_profile)
     std::vector<ProfRec> recs;
     std::vector<hipEvent_t> ev_pool;
+    size_t cells = 0;                  // channels configured by tetra_etsi_set_cells
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = true;

@@ -1,0 +1,738 @@
+// etsi_rx.hip -- ETSI EN 300 392-2 receive chain on gfx950 (the north-star path).
+//
+// The reference has no such chain; this is the receiver BASELINE.json's
+// north_star asks for, restating oracle/etsi_oracle.c operation for operation (explicit fmaf,
+// emulated 64-lane reductions, a libm-free atan2), so GPU and oracle results are bit-identical.
+//
+//   k_chanfilt   stage 1: 48-tap decimate-by-q1 FIR (2.4 MSps -> 240 kHz), stage 2: polyphase RRC
+//                (alpha 0.35) resampler x3/10 -> 72 kHz = 4 samples/symbol.  One workgroup streams
+//                one channel: 2560-sample input tiles (float4 loads, register prefetch one tile
+//                ahead), stage-1 outputs in an LDS ring, stage-2 outputs stored coalesced.
+//                HBM-bound: ~8 B read per input sample, 0.24 B written.
+//   k_timing     one wave per channel: Oerder-Meyr timing phase (wave reduction), block Gardner
+//                tracking (64 symbols per block = one per lane; error summed by xor-butterfly),
+//                cubic interpolation, differential decision, 4th-power CFO estimate, int8 soft bits.
+//   k_lmac_etsi  one wave per channel: burst sync on packed hard bits (head/training/tail
+//                correlation by XOR+popcount, ballot greedy scan), then per block: descramble,
+//                deinterleave, depuncture (rate 2/3), 16-state Viterbi (one lane per state, 4 blocks
+//                per wave, survivors as 64-bit ballots in LDS), traceback, CRC-16.
+#include "common.h"
+
+namespace {
+
+constexpr int ETSI_MAXB = 8;    // bursts per channel chunk
+constexpr int ETSI_MAXJ = 16;   // coded blocks per channel chunk (2 per burst)
+constexpr int TILE_K = 256;     // stage-1 outputs per tile (one per thread)
+constexpr int TILE_IN = TILE_K * 10;   // new input samples per tile (q1 = 10)
+constexpr int HALO = 48;
+constexpr int RING = 1024;      // stage-1 ring (power of two)
+
+struct KindP { int K, a, n2, n1; };
+__host__ __device__ inline KindP kind_params(int kind) {
+    return kind == 0 ? KindP{432, 103, 288, 268} : kind == 1 ? KindP{216, 101, 144, 124} : KindP{120, 11, 80, 60};
+}
+
+// --------------------------------------------------------------------------- E1 channel filter
+// plan arrays in constant-ish global memory (read through the scalar cache)
+__global__ __launch_bounds__(256) void k_chanfilt(const float4 *__restrict__ iq, long N, int M1, int M2,
+                                                  const float *__restrict__ h1, const float *__restrict__ hp,
+                                                  int Lp, float2 *__restrict__ y) {
+    __shared__ float2 xin[TILE_IN + HALO];
+    __shared__ float2 ring[RING];
+    const int ch = blockIdx.x;
+    const int tid = threadIdx.x;
+    const float4 *xp = iq + (size_t)ch * (N / 2);   // N even: 2 complex samples per float4
+    float2 *yp = y + (size_t)ch * M2;
+    float hr[48];
+#pragma unroll
+    for (int j = 0; j < 48; ++j) hr[j] = h1[j];
+    // register prefetch of tile 0: samples [0, 2560) land at xin[48 + i]
+    float4 pf[5];
+    auto load_tile = [&](int t) {
+#pragma unroll
+        for (int r = 0; r < 5; ++r) {
+            const long q = (long)t * (TILE_IN / 2) + r * 256 + tid;   // float4 index
+            pf[r] = (2 * q + 1 < N) ? xp[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    load_tile(0);
+    int m_done = 0;
+    for (int t = 0;; ++t) {
+        const int kfirst = TILE_K * t - 4;   // stage-1 output of thread 0 in this tile
+        if (kfirst >= M1) break;
+#pragma unroll
+        for (int r = 0; r < 5; ++r) {
+            const int i = 2 * (r * 256 + tid);
+            xin[HALO + i] = make_float2(pf[r].x, pf[r].y);
+            xin[HALO + i + 1] = make_float2(pf[r].z, pf[r].w);
+        }
+        load_tile(t + 1);   // next tile in flight during compute
+        __syncthreads();
+        // stage 1: x240[k] = sum_j h1[j] * x[10k + j], k = kfirst + tid
+        const int k = kfirst + tid;
+        if (k >= 0 && k < M1) {
+            const float2 *w = xin + 10 * tid + 8;
+            float ar = 0.f, ai = 0.f;
+#pragma unroll
+            for (int j = 0; j < 48; ++j) {
+                const float2 v = w[j];
+                ar = fmaf(hr[j], v.x, ar);
+                ai = fmaf(hr[j], v.y, ai);
+            }
+            ring[k & (RING - 1)] = make_float2(ar, ai);
+        }
+        __syncthreads();
+        // halo for the next tile: its xin[0..48) = this tile's xin[2560..2608)
+        if (tid < HALO) xin[tid] = xin[TILE_IN + tid];
+        // stage 2: outputs m whose taps end at or before the last stage-1 output available
+        const int kav = min(kfirst + TILE_K - 1, M1 - 1);
+        const int num = 3 * kav + 2 - (Lp - 1);   // largest m with floor((Lp-1+10m)/3) <= kav
+        int m_hi = num >= 0 ? num / 10 : -1;
+        if (m_hi > M2 - 1) m_hi = M2 - 1;
+        for (int m0 = m_done; m0 <= m_hi; m0 += 256) {
+            const int m = m0 + tid;
+            if (m <= m_hi) {
+                const int n = (Lp - 1) + 10 * m;
+                const int kmin = (10 * m + 2) / 3, kmax = n / 3;
+                float ar = 0.f, ai = 0.f;
+                for (int kk = kmin; kk <= kmax; ++kk) {
+                    const float h = hp[n - 3 * kk];
+                    const float2 v = ring[kk & (RING - 1)];
+                    ar = fmaf(h, v.x, ar);
+                    ai = fmaf(h, v.y, ai);
+                }
+                yp[m] = make_float2(ar, ai);
+            }
+        }
+        if (m_hi + 1 > m_done) m_done = m_hi + 1;
+        __syncthreads();
+    }
+}
+
+// --------------------------------------------------------------------------- E2 timing
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
+    return v;
+}
+
+__device__ __forceinline__ float pat2(float y, float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    const float a = mx == 0.0f ? 0.0f : mn / mx;
+    const float s = a * a;
+    float r = fmaf(fmaf(fmaf(fmaf(fmaf(-0.0117212f, s, 0.05265332f), s, -0.11643287f), s, 0.19354346f), s,
+                        -0.33262347f), s, 0.99997726f) * a;
+    if (ay > ax) r = 1.57079637f - r;
+    if (x < 0.0f) r = 3.14159274f - r;
+    if (y < 0.0f) r = -r;
+    return r;
+}
+
+__device__ __forceinline__ float2 interp(const float2 *y, float t) {
+    const float K6 = 1.0f / 6.0f;
+    const float fi = floorf(t);
+    const int i = (int)fi;
+    const float f = t - fi;
+    const float fm1 = f - 1.0f, fm2 = f - 2.0f, fp1 = f + 1.0f;
+    const float cm = -(f * fm1 * fm2) * K6;
+    const float c0 = (fp1 * fm1 * fm2) * 0.5f;
+    const float c1 = -(fp1 * f * fm2) * 0.5f;
+    const float c2 = (fp1 * f * fm1) * K6;
+    const float2 a = y[i - 1], b = y[i], c = y[i + 1], d = y[i + 2];
+    float r = cm * a.x, q = cm * a.y;
+    r = fmaf(c0, b.x, r); q = fmaf(c0, b.y, q);
+    r = fmaf(c1, c.x, r); q = fmaf(c1, c.y, q);
+    r = fmaf(c2, d.x, r); q = fmaf(c2, d.y, q);
+    return make_float2(r, q);
+}
+
+__device__ __forceinline__ float2 csqrt_p(float x, float y) {
+    const float r = sqrtf(fmaf(x, x, y * y));
+    if (r == 0.0f) return make_float2(0.f, 0.f);
+    if (x >= 0.0f) {
+        const float s = sqrtf((r + x) * 0.5f);
+        return make_float2(s, y / (2.0f * s));
+    }
+    float s = sqrtf((r - x) * 0.5f);
+    if (y < 0.0f) s = -s;
+    return make_float2(y / (2.0f * s), s);
+}
+
+__global__ __launch_bounds__(64) void k_timing(const float2 *__restrict__ yall, int M2, float gain, float soft_scale,
+                                               float2 *__restrict__ sym, float2 *__restrict__ dscr,
+                                               int8_t *__restrict__ softbits, uint8_t *__restrict__ hard,
+                                               int32_t *__restrict__ nsym, int smax, float4 *__restrict__ diag) {
+    const int ch = blockIdx.x, lane = threadIdx.x;
+    const float2 *y = yall + (size_t)ch * M2;
+    float2 *sp = sym + (size_t)ch * smax;
+    float2 *dp = dscr + (size_t)ch * smax;
+    int8_t *sb = softbits + (size_t)ch * 2 * smax;
+    uint8_t *hp = hard + (size_t)ch * smax;
+    if (M2 < 16) {
+        if (lane == 0) nsym[ch] = 0;
+        return;
+    }
+    // Oerder-Meyr: class sums of |y|^2 over n mod 4
+    float s = 0.f;
+    for (int n = lane; n < M2; n += 64) {
+        const float2 v = y[n];
+        s += fmaf(v.x, v.x, v.y * v.y);
+    }
+#pragma unroll
+    for (int off = 32; off >= 4; off >>= 1) s = s + __shfl_xor(s, off, 64);
+    const float A0 = __shfl(s, 0, 64), A1 = __shfl(s, 1, 64), A2 = __shfl(s, 2, 64), A3 = __shfl(s, 3, 64);
+    const float Xr = A0 - A2, Xi = A3 - A1;
+    const float p = -0.63661977236758134f * pat2(Xi, Xr);
+    float base = p < 0.0f ? p + 4.0f : p;
+    if (base >= 4.0f) base -= 4.0f;
+    const int kstart = base >= 3.0f ? 0 : 1;
+    float delta = 0.0f;
+    int S = 0;
+    float2 prev = make_float2(0.f, 0.f);
+    bool have_prev = false;
+    for (int kb = kstart;; kb += 64) {
+        const float off = base + delta;
+        const float t = (float)(4 * (kb + lane)) + off;
+        const bool valid = (t - 3.0f >= 0.0f) && (t + 2.0f <= (float)(M2 - 1)) && (S + lane < smax);
+        const unsigned long long bal = __ballot(!valid);
+        const int nv = bal ? (__ffsll((long long)bal) - 1) : 64;
+        float2 on = make_float2(0.f, 0.f), mid = make_float2(0.f, 0.f);
+        if (lane < nv) {
+            on = interp(y, t);
+            mid = interp(y, t - 2.0f);
+        }
+        float2 pv = make_float2(__shfl_up(on.x, 1, 64), __shfl_up(on.y, 1, 64));
+        bool hp_ = true;
+        if (lane == 0) { pv = prev; hp_ = have_prev; }
+        float ev = 0.f, pw = 0.f;
+        if (lane < nv) {
+            pw = fmaf(on.x, on.x, on.y * on.y);
+            if (hp_) {
+                const float dr = on.x - pv.x, di = on.y - pv.y;
+                ev = fmaf(dr, mid.x, di * mid.y);
+                const int j = S + lane;
+                dp[j - 1] = make_float2(fmaf(on.x, pv.x, on.y * pv.y), fmaf(on.y, pv.x, -(on.x * pv.y)));
+            }
+            sp[S + lane] = on;
+        }
+        if (nv > 0) {
+            const float E = wave_sum(ev), W = wave_sum(pw);
+            if (W > 0.0f) delta = delta - gain * (E / W);
+            if (delta > 1.5f) delta = 1.5f;
+            if (delta < -1.5f) delta = -1.5f;
+            prev = make_float2(__shfl(on.x, nv - 1, 64), __shfl(on.y, nv - 1, 64));
+            have_prev = true;
+        }
+        S += nv;
+        if (nv < 64) break;
+    }
+    // CFO (4th power) and soft scale; lane l owns d_j with j & 63 == l, ascending j
+    float zr = 0.f, zi = 0.f, am = 0.f;
+    for (int j = (lane == 0 ? 64 : lane); j < S; j += 64) {
+        const float2 d = dp[j - 1];
+        const float sr = fmaf(d.x, d.x, -(d.y * d.y)), si = (d.x * d.y) * 2.0f;
+        const float qr = fmaf(sr, sr, -(si * si)), qi = (sr * si) * 2.0f;
+        zr += qr;
+        zi += qi;
+        am += sqrtf(fmaf(d.x, d.x, d.y * d.y));
+    }
+    const float Zr = wave_sum(zr), Zi = wave_sum(zi), A = wave_sum(am);
+    float rr = 1.0f, ri = 0.0f;
+    const float zm = sqrtf(fmaf(Zr, Zr, Zi * Zi));
+    if (zm > 0.0f) {
+        const float2 v = csqrt_p(-Zr / zm, -Zi / zm);
+        const float2 w = csqrt_p(v.x, v.y);
+        rr = w.x;
+        ri = -w.y;
+    }
+    const float sc = (S > 1 && A > 0.0f) ? soft_scale / (A / (float)(S - 1)) : 0.0f;
+    for (int j = 1 + lane; j < S; j += 64) {
+        const float2 d = dp[j - 1];
+        const float xr = fmaf(d.x, rr, -(d.y * ri)), xi = fmaf(d.x, ri, d.y * rr);
+        float q1 = rintf(xi * sc), q2 = rintf(xr * sc);
+        q1 = q1 > 127.f ? 127.f : (q1 < -127.f ? -127.f : q1);
+        q2 = q2 > 127.f ? 127.f : (q2 < -127.f ? -127.f : q2);
+        sb[2 * (j - 1)] = (int8_t)q1;
+        sb[2 * (j - 1) + 1] = (int8_t)q2;
+        hp[j - 1] = (uint8_t)(((xi < 0.0f) << 1) | (xr < 0.0f));
+    }
+    if (lane == 0) {
+        nsym[ch] = S;
+        if (diag) diag[ch] = make_float4(base, delta, rr, ri);
+    }
+}
+
+// --------------------------------------------------------------------------- E3/E4 lower MAC
+// training/tail patterns (EN 300 392-2 §9.4.4.3), LSB-first words
+__host__ __device__ constexpr uint64_t packb(const int *p, int n) {
+    uint64_t w = 0;
+    for (int j = 0; j < n; ++j) w |= (uint64_t)p[j] << j;
+    return w;
+}
+constexpr int QB[22] = {1, 0, 1, 1, 0, 1, 1, 1, 0, 0, 0, 0, 0, 1, 1, 0, 1, 0, 1, 1, 0, 1};
+constexpr int NB[22] = {1, 1, 0, 1, 0, 0, 0, 0, 1, 1, 1, 0, 1, 0, 0, 1, 1, 1, 0, 1, 0, 0};
+constexpr int PB[22] = {0, 1, 1, 1, 1, 0, 1, 0, 0, 1, 0, 0, 0, 0, 1, 1, 0, 1, 1, 1, 0, 0};
+constexpr int YB[38] = {1, 1, 0, 0, 0, 0, 0, 1, 1, 0, 0, 1, 1, 1, 0, 0, 1, 1, 1,
+                        0, 1, 0, 0, 1, 1, 1, 0, 0, 0, 0, 0, 1, 1, 0, 0, 1, 1, 1};
+constexpr uint64_t W_HEAD = packb(QB + 10, 12), W_TAIL = packb(QB, 10), W_N = packb(NB, 22), W_P = packb(PB, 22),
+                   W_Y = packb(YB, 38);
+
+__device__ __forceinline__ uint64_t bits_at(const uint64_t *w, int pos, int len) {
+    const int q = pos >> 6, r = pos & 63;
+    uint64_t v = w[q] >> r;
+    if (r) v |= w[q + 1] << (64 - r);
+    return len == 64 ? v : (v & ((1ull << len) - 1));
+}
+__device__ __forceinline__ int matches(uint64_t v, uint64_t pat, int len) {
+    return len - __popcll((v ^ pat) & ((1ull << len) - 1));
+}
+
+__device__ __forceinline__ int punct_index(int j1) {   // rate 2/3, t=3, P=(1,2,5); 1-based
+    const int g = (j1 - 1) / 3;
+    const int r = j1 - 3 * g;
+    return 8 * g + (r == 1 ? 1 : r == 2 ? 2 : 5);
+}
+
+constexpr int LMAC_MAXBITS = 2 * 2048;
+
+// One wave per channel.  bursts [C][8][2] (start, kind); blocks [C][16][4] (kind, crc_ok, burst, block);
+// type1 [C][16][268].
+__global__ __launch_bounds__(64) void k_lmac_etsi(const int8_t *__restrict__ softbits, const uint8_t *__restrict__ hard,
+                                                  const int32_t *__restrict__ nsym, int smax,
+                                                  const uint8_t *__restrict__ cell_scr, const uint8_t *__restrict__ bsch_scr,
+                                                  int32_t *__restrict__ nburst, int32_t *__restrict__ bursts,
+                                                  int32_t *__restrict__ nblock, int32_t *__restrict__ blocks,
+                                                  uint8_t *__restrict__ type1) {
+    const int ch = blockIdx.x, lane = threadIdx.x;
+    __shared__ uint64_t words[LMAC_MAXBITS / 64 + 2];
+    __shared__ int8_t ms[4][4 * 288];
+    __shared__ uint64_t surv[288];
+    __shared__ uint8_t t2[4][288];
+    __shared__ int bstart[ETSI_MAXB], bkind[ETSI_MAXB];
+    const int S = nsym[ch];
+    int nbits = 2 * (S > 1 ? S - 1 : 0);
+    if (nbits > LMAC_MAXBITS) nbits = LMAC_MAXBITS;
+    const uint8_t *hp = hard + (size_t)ch * smax;
+    const int8_t *sb = softbits + (size_t)ch * 2 * smax;
+    // pack hard bits: bit 2i = b1 of dibit i, 2i+1 = b2
+    const int nw = (nbits + 63) / 64;
+    for (int w = lane; w < nw + 2; w += 64) {
+        uint64_t v = 0;
+        if (w < nw) {
+            for (int b = 0; b < 64; ++b) {
+                const int i = 64 * w + b;
+                if (i < nbits) {
+                    const uint32_t h = hp[i >> 1];
+                    v |= (uint64_t)((i & 1) ? (h & 1u) : (h >> 1)) << b;
+                }
+            }
+        }
+        words[w] = v;
+    }
+    __syncthreads();
+    // greedy burst scan
+    int nb = 0;
+    for (int cur = 0; cur + 510 <= nbits && nb < ETSI_MAXB;) {
+        const int s = cur + lane;
+        int kind = -1;
+        if (s + 510 <= nbits) {
+            const int ht = matches(bits_at(words, s, 12), W_HEAD, 12) + matches(bits_at(words, s + 500, 10), W_TAIL, 10);
+            const uint64_t t22 = bits_at(words, s + 244, 22);
+            const int mn = ht + matches(t22, W_N, 22), mp = ht + matches(t22, W_P, 22);
+            const int my = ht + matches(bits_at(words, s + 214, 38), W_Y, 38);
+            if (my >= 54) kind = 2;
+            else if (mn >= 40 && mn >= mp) kind = 0;
+            else if (mp >= 40) kind = 1;
+        }
+        const unsigned long long bal = __ballot(kind >= 0);
+        if (bal) {
+            const int first = __ffsll((long long)bal) - 1;
+            const int k = __shfl(kind, first, 64);
+            if (lane == 0) { bstart[nb] = cur + first; bkind[nb] = k; }
+            ++nb;
+            cur = cur + first + 500;
+        } else {
+            cur += 64;
+        }
+    }
+    __syncthreads();
+    // block jobs
+    int njob = 0;
+    int jb[ETSI_MAXJ], jk[ETSI_MAXJ], joff[ETSI_MAXJ], jblk[ETSI_MAXJ];
+    for (int b = 0; b < nb; ++b) {
+        const int s = bstart[b], k = bkind[b];
+        if (k == 0) { jb[njob] = b; jk[njob] = 0; joff[njob] = s + 14; jblk[njob] = 0; ++njob; }
+        else if (k == 1) {
+            jb[njob] = b; jk[njob] = 1; joff[njob] = s + 14; jblk[njob] = 0; ++njob;
+            jb[njob] = b; jk[njob] = 1; joff[njob] = s + 282; jblk[njob] = 1; ++njob;
+        } else {
+            jb[njob] = b; jk[njob] = 2; joff[njob] = s + 94; jblk[njob] = 0; ++njob;
+            jb[njob] = b; jk[njob] = 1; joff[njob] = s + 282; jblk[njob] = 1; ++njob;
+        }
+    }
+    if (lane == 0) {
+        nburst[ch] = nb;
+        nblock[ch] = njob;
+    }
+    for (int b = lane; b < nb; b += 64) {
+        bursts[((size_t)ch * ETSI_MAXB + b) * 2] = bstart[b];
+        bursts[((size_t)ch * ETSI_MAXB + b) * 2 + 1] = bkind[b];
+    }
+    const uint8_t *cscr = cell_scr + (size_t)ch * 432;
+    const int g = lane >> 4, st = lane & 15;
+    for (int j0 = 0; j0 < njob; j0 += 4) {
+        // --- descramble + deinterleave + depuncture into ms[g] (4 jobs, 16 lanes each)
+        const int j = j0 + g;
+        const bool act = j < njob;
+        const KindP P = kind_params(act ? jk[j] : 1);
+        const uint8_t *scr = (act && jk[j] == 2) ? bsch_scr : cscr;
+        if (act) {
+            for (int i = st; i < 4 * P.n2; i += 16) ms[g][i] = 0;
+        }
+        __syncthreads();
+        if (act) {
+            const int o = joff[j];
+            const bool two = jk[j] == 0;   // SCH/F: BKN1 (14..229) ++ BKN2 (282..497)
+            for (int i = 1 + st; i <= P.K; i += 16) {
+                const int k = 1 + (int)(((long)P.a * i) % P.K);
+                const int pos = two ? (k - 1 < 216 ? o + (k - 1) : o + 268 + (k - 1 - 216)) + 0 : o + (k - 1);
+                const int8_t v = sb[pos];
+                const int8_t d = scr[k - 1] ? (int8_t)(-v) : v;
+                ms[g][punct_index(i) - 1] = d;
+            }
+        }
+        __syncthreads();
+        // --- ACS: lane (g, st) holds the metric of state st
+        int32_t pm = st == 0 ? 0 : -(1 << 28);
+        const int n2max = 288;
+        const int b = st & 1, d0 = (st >> 1) & 1, d1 = (st >> 2) & 1, d2 = (st >> 3) & 1;
+        for (int t = 0; t < n2max; ++t) {
+            const bool live = act && t < P.n2;
+            int32_t v0 = 0, v1 = 0;
+            if (live) {
+                const int8_t *m = ms[g] + 4 * t;
+                const int32_t m0 = m[0], m1 = m[1], m2 = m[2], m3 = m[3];
+                // d3 = 0
+                v0 = ((b ^ d0) ? -m0 : m0) + ((b ^ d1 ^ d2) ? -m1 : m1) + ((b ^ d0 ^ d1) ? -m2 : m2) +
+                     ((b ^ d0 ^ d2) ? -m3 : m3);
+                // d3 = 1 flips every generator output
+                v1 = -v0;
+            }
+            const int p0 = (st >> 1), p1 = (st >> 1) | 8;
+            const int32_t a0 = __shfl(pm, (lane & ~15) + p0, 64) + v0;
+            const int32_t a1 = __shfl(pm, (lane & ~15) + p1, 64) + v1;
+            const bool take1 = a1 > a0;
+            const unsigned long long sv = __ballot(take1);
+            if (live) pm = take1 ? a1 : a0;
+            if (lane == 0) surv[t] = sv;
+            if (__all(!live)) break;
+        }
+        __syncthreads();
+        // --- traceback (lane 0 of each group) and CRC
+        if (act && st == 0) {
+            int s2 = 0;
+            for (int t = P.n2 - 1; t >= 0; --t) {
+                t2[g][t] = (uint8_t)(s2 & 1);
+                const int d3 = (int)((surv[t] >> (16 * g + s2)) & 1ull);
+                s2 = (s2 >> 1) | (d3 << 3);
+            }
+            uint32_t c = 0xFFFF;
+            for (int i = 0; i < P.n1 + 16; ++i) {
+                c ^= (uint32_t)t2[g][i] << 15;
+                c = (c & 0x8000u) ? ((c << 1) ^ 0x1021u) : (c << 1);
+                c &= 0xFFFFu;
+            }
+            int32_t *bm = blocks + ((size_t)ch * ETSI_MAXJ + j) * 4;
+            bm[0] = jk[j];
+            bm[1] = c == 0x1D0Fu;
+            bm[2] = jb[j];
+            bm[3] = jblk[j];
+        }
+        __syncthreads();
+        if (act) {
+            uint8_t *op = type1 + ((size_t)ch * ETSI_MAXJ + j) * 268;
+            for (int i = st; i < P.n1; i += 16) op[i] = t2[g][i];
+        }
+        __syncthreads();
+    }
+}
+
+// --------------------------------------------------------------------------- component kernels
+// Block decode of F independent blocks of one kind (16 lanes per block, 4 per wave).
+__global__ __launch_bounds__(64) void k_decode_blocks(const int8_t *__restrict__ soft5, int F, int kind,
+                                                      const uint8_t *__restrict__ scr /*[F][K]*/,
+                                                      uint8_t *__restrict__ type1, uint8_t *__restrict__ crc_ok) {
+    __shared__ int8_t ms[4][4 * 288];
+    __shared__ uint64_t surv[288];
+    __shared__ uint8_t t2[4][288];
+    const int lane = threadIdx.x, g = lane >> 4, st = lane & 15;
+    const int j = blockIdx.x * 4 + g;
+    const bool act = j < F;
+    const KindP P = kind_params(kind);
+    for (int i = st; i < 4 * P.n2; i += 16) ms[g][i] = 0;
+    __syncthreads();
+    if (act) {
+        for (int i = 1 + st; i <= P.K; i += 16) {
+            const int k = 1 + (int)(((long)P.a * i) % P.K);
+            const int8_t v = soft5[(size_t)j * P.K + k - 1];
+            ms[g][punct_index(i) - 1] = scr[(size_t)j * P.K + k - 1] ? (int8_t)(-v) : v;
+        }
+    }
+    __syncthreads();
+    int32_t pm = st == 0 ? 0 : -(1 << 28);
+    const int b = st & 1, d0 = (st >> 1) & 1, d1 = (st >> 2) & 1, d2 = (st >> 3) & 1;
+    for (int t = 0; t < P.n2; ++t) {
+        const int8_t *m = ms[g] + 4 * t;
+        const int32_t m0 = m[0], m1 = m[1], m2 = m[2], m3 = m[3];
+        const int32_t v0 = ((b ^ d0) ? -m0 : m0) + ((b ^ d1 ^ d2) ? -m1 : m1) + ((b ^ d0 ^ d1) ? -m2 : m2) +
+                           ((b ^ d0 ^ d2) ? -m3 : m3);
+        const int32_t a0 = __shfl(pm, (lane & ~15) + (st >> 1), 64) + v0;
+        const int32_t a1 = __shfl(pm, (lane & ~15) + ((st >> 1) | 8), 64) - v0;
+        const bool take1 = a1 > a0;
+        const unsigned long long sv = __ballot(take1);
+        pm = take1 ? a1 : a0;
+        if (lane == 0) surv[t] = sv;
+    }
+    __syncthreads();
+    if (act && st == 0) {
+        int s2 = 0;
+        for (int t = P.n2 - 1; t >= 0; --t) {
+            t2[g][t] = (uint8_t)(s2 & 1);
+            s2 = (s2 >> 1) | ((int)((surv[t] >> (16 * g + s2)) & 1ull) << 3);
+        }
+        uint32_t c = 0xFFFF;
+        for (int i = 0; i < P.n1 + 16; ++i) {
+            c ^= (uint32_t)t2[g][i] << 15;
+            c = (c & 0x8000u) ? ((c << 1) ^ 0x1021u) : (c << 1);
+            c &= 0xFFFFu;
+        }
+        crc_ok[j] = c == 0x1D0Fu;
+    }
+    __syncthreads();
+    if (act)
+        for (int i = st; i < P.n1; i += 16) type1[(size_t)j * P.n1 + i] = t2[g][i];
+}
+
+// Encoder type-1 -> type-5 (one block per thread; CRC, tail, mother code, puncture, interleave, scramble)
+__global__ void k_encode_blocks(const uint8_t *__restrict__ type1, int F, int kind, const uint8_t *__restrict__ scr,
+                                uint8_t *__restrict__ type5) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= F) return;
+    const KindP P = kind_params(kind);
+    const uint8_t *in = type1 + (size_t)j * P.n1;
+    uint8_t t2[288];
+    uint32_t c = 0xFFFF;
+    for (int i = 0; i < P.n1; ++i) {
+        t2[i] = in[i] & 1;
+        c ^= (uint32_t)t2[i] << 15;
+        c = (c & 0x8000u) ? ((c << 1) ^ 0x1021u) : (c << 1);
+        c &= 0xFFFFu;
+    }
+    c ^= 0xFFFFu;
+    for (int k = 0; k < 16; ++k) t2[P.n1 + k] = (c >> (15 - k)) & 1u;
+    for (int k = 0; k < 4; ++k) t2[P.n1 + 16 + k] = 0;
+    for (int i = 1; i <= P.K; ++i) {
+        const int mi = punct_index(i) - 1;   // mother index: step mi/4, generator mi%4
+        const int step = mi >> 2, gen = mi & 3;
+        const uint32_t bb = t2[step];
+        const uint32_t e0 = step >= 1 ? t2[step - 1] : 0, e1 = step >= 2 ? t2[step - 2] : 0,
+                       e2 = step >= 3 ? t2[step - 3] : 0, e3 = step >= 4 ? t2[step - 4] : 0;
+        uint32_t v = gen == 0 ? (bb ^ e0 ^ e3) : gen == 1 ? (bb ^ e1 ^ e2 ^ e3) : gen == 2 ? (bb ^ e0 ^ e1 ^ e3)
+                                                                                          : (bb ^ e0 ^ e2 ^ e3);
+        const int k = 1 + (int)(((long)P.a * i) % P.K);
+        type5[(size_t)j * P.K + k - 1] = (uint8_t)(v ^ scr[(size_t)j * P.K + k - 1]);
+    }
+}
+
+}  // namespace
+
+// --------------------------------------------------------------------------- host side
+static void scramble_seq(uint32_t r, int n, uint8_t *out) {
+    for (int i = 0; i < n; ++i) {
+        const uint32_t b = ((r >> 0) ^ (r >> 6) ^ (r >> 9) ^ (r >> 10) ^ (r >> 16) ^ (r >> 20) ^ (r >> 21) ^ (r >> 22) ^
+                            (r >> 24) ^ (r >> 25) ^ (r >> 27) ^ (r >> 28) ^ (r >> 30) ^ (r >> 31)) & 1u;
+        r = (r >> 1) | (b << 31);
+        out[i] = (uint8_t)b;
+    }
+}
+
+static int etsi_check(tetra_ctx *ctx, const tetra_etsi_plan *P) {
+    if (!P) return tetra_fail(ctx, TETRA_E_INVALID, "plan is NULL");
+    if (P->q1 != 10 || P->L1 != 48 || P->up != 3 || P->down != 10 || P->Lp < 16 || P->Lp > 384)
+        return tetra_fail(ctx, TETRA_E_INVALID, "unsupported ETSI plan (q1=10, L1=48, 3/10, Lp<=384 required)");
+    return TETRA_OK;
+}
+
+extern "C" {
+
+int tetra_etsi_lengths(const tetra_etsi_plan *P, size_t N, int64_t *M1, int64_t *M2, int64_t *smax) {
+    if (!P || !M1 || !M2 || !smax) return TETRA_E_INVALID;
+    long m1 = N >= (size_t)P->L1 ? ((long)N - P->L1) / P->q1 + 1 : 0;
+    long m2 = (P->up * m1 - 1 - (P->Lp - 1)) >= 0 ? (P->up * m1 - 1 - (P->Lp - 1)) / P->down + 1 : 0;
+    *M1 = m1;
+    *M2 = m2;
+    *smax = m2 / 4 + 2;
+    return TETRA_OK;
+}
+
+int tetra_etsi_set_cells(tetra_ctx *ctx, const uint32_t *scramb_init, size_t C) {
+    if (!ctx || !scramb_init || C == 0) return TETRA_E_INVALID;
+    std::vector<uint32_t> init(C);
+    HIP_TRY(ctx, hipMemcpy(init.data(), scramb_init, C * 4, hipMemcpyDefault));
+    std::vector<uint8_t> tab(C * 432 + 432);
+    for (size_t c = 0; c < C; ++c) scramble_seq(init[c], 432, tab.data() + c * 432);
+    scramble_seq(3u, 432, tab.data() + C * 432);   // BSCH: colour code 0
+    uint8_t *d = (uint8_t *)ws(ctx, S_W5, tab.size());
+    if (!d) return TETRA_E_NOMEM;
+    HIP_TRY(ctx, hipMemcpyAsync(d, tab.data(), tab.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->cells = C;
+    return TETRA_OK;
+}
+
+int tetra_etsi_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *iq, size_t C, size_t N, void *y) {
+    if (!ctx) return TETRA_E_INVALID;
+    int rc = etsi_check(ctx, P);
+    if (rc) return rc;
+    if (N % 2 || C == 0) return tetra_fail(ctx, TETRA_E_INVALID, "N must be even");
+    int64_t M1, M2, smax;
+    tetra_etsi_lengths(P, N, &M1, &M2, &smax);
+    if (M2 <= 0) return tetra_fail(ctx, TETRA_E_INVALID, "chunk too short for the channel filter");
+    Staging st(ctx);
+    const void *x = st.in(iq, C * N * 8);
+    void *yo = st.out(y, C * (size_t)M2 * 8);
+    float *coef = (float *)ws(ctx, S_W6, (64 + 384) * 4);
+    if (!x || !yo || !coef) return st.finish();
+    HIP_TRY(ctx, hipMemcpyAsync(coef, P->h1, 64 * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(coef + 64, P->hp, 384 * 4, hipMemcpyHostToDevice, ctx->stream));
+    {
+        PROF(ctx, "etsi_chanfilt");
+        hipLaunchKernelGGL(k_chanfilt, dim3((unsigned)C), dim3(256), 0, ctx->stream, (const float4 *)x, (long)N,
+                           (int)M1, (int)M2, coef, coef + 64, P->Lp, (float2 *)yo);
+    }
+    return st.finish();
+}
+
+int tetra_etsi_timing(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *y, size_t C, size_t M2, void *soft,
+                      int8_t *softbits, uint8_t *hard, int32_t *nsym, size_t smax, float *diag) {
+    if (!ctx || !P || C == 0) return TETRA_E_INVALID;
+    Staging st(ctx);
+    const void *yd = st.in(y, C * M2 * 8);
+    void *so = st.out(soft, C * smax * 8);
+    int8_t *sbo = (int8_t *)st.out(softbits, C * smax * 2);
+    uint8_t *ho = (uint8_t *)st.out(hard, C * smax);
+    int32_t *no = (int32_t *)st.out(nsym, C * 4);
+    float *dg = diag ? (float *)st.out(diag, C * 16) : nullptr;
+    float2 *dscr = (float2 *)ws(ctx, S_W4, C * smax * 8);
+    if (!yd || !so || !sbo || !ho || !no || !dscr) return st.finish();
+    {
+        PROF(ctx, "etsi_timing");
+        hipLaunchKernelGGL(k_timing, dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yd, (int)M2, P->gain,
+                           P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg);
+    }
+    return st.finish();
+}
+
+int tetra_demod_etsi(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *iq, size_t C, size_t N, void *soft,
+                     int8_t *softbits, uint8_t *hard, int32_t *nsym, size_t smax, float *diag) {
+    if (!ctx) return TETRA_E_INVALID;
+    int rc = etsi_check(ctx, P);
+    if (rc) return rc;
+    int64_t M1, M2, sm;
+    tetra_etsi_lengths(P, N, &M1, &M2, &sm);
+    if (M2 <= 0 || N % 2 || C == 0) return tetra_fail(ctx, TETRA_E_INVALID, "bad chunk for the ETSI demod");
+    if ((int64_t)smax < sm) return tetra_fail(ctx, TETRA_E_INVALID, "smax < %ld", (long)sm);
+    Staging st(ctx);
+    const void *x = st.in(iq, C * N * 8);
+    void *so = st.out(soft, C * smax * 8);
+    int8_t *sbo = (int8_t *)st.out(softbits, C * smax * 2);
+    uint8_t *ho = (uint8_t *)st.out(hard, C * smax);
+    int32_t *no = (int32_t *)st.out(nsym, C * 4);
+    float *dg = diag ? (float *)st.out(diag, C * 16) : nullptr;
+    float *coef = (float *)ws(ctx, S_W6, (64 + 384) * 4);
+    float2 *yb = (float2 *)ws(ctx, S_W3, C * (size_t)M2 * 8);
+    float2 *dscr = (float2 *)ws(ctx, S_W4, C * smax * 8);
+    if (!x || !so || !sbo || !ho || !no || !coef || !yb || !dscr) return st.finish();
+    HIP_TRY(ctx, hipMemcpyAsync(coef, P->h1, 64 * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(coef + 64, P->hp, 384 * 4, hipMemcpyHostToDevice, ctx->stream));
+    {
+        PROF(ctx, "etsi_chanfilt");
+        hipLaunchKernelGGL(k_chanfilt, dim3((unsigned)C), dim3(256), 0, ctx->stream, (const float4 *)x, (long)N,
+                           (int)M1, (int)M2, coef, coef + 64, P->Lp, yb);
+    }
+    {
+        PROF(ctx, "etsi_timing");
+        hipLaunchKernelGGL(k_timing, dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yb, (int)M2, P->gain,
+                           P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg);
+    }
+    return st.finish();
+}
+
+int tetra_lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard, const int32_t *nsym, size_t C,
+                    size_t smax, int32_t *nburst, int32_t *bursts, int32_t *nblock, int32_t *blocks, uint8_t *type1) {
+    if (!ctx || C == 0) return TETRA_E_INVALID;
+    if (ctx->cells < C) return tetra_fail(ctx, TETRA_E_INVALID, "tetra_etsi_set_cells() for %zu channels first", C);
+    if (2 * smax > LMAC_MAXBITS + 4) return tetra_fail(ctx, TETRA_E_INVALID, "chunk too long for tetra_lmac_etsi");
+    Staging st(ctx);
+    const int8_t *sb = (const int8_t *)st.in(softbits, C * smax * 2);
+    const uint8_t *hd = (const uint8_t *)st.in(hard, C * smax);
+    const int32_t *ns = (const int32_t *)st.in(nsym, C * 4);
+    int32_t *nbo = (int32_t *)st.out(nburst, C * 4);
+    int32_t *bo = (int32_t *)st.out(bursts, C * ETSI_MAXB * 2 * 4);
+    int32_t *nko = (int32_t *)st.out(nblock, C * 4);
+    int32_t *ko = (int32_t *)st.out(blocks, C * ETSI_MAXJ * 4 * 4);
+    uint8_t *to = (uint8_t *)st.out(type1, C * ETSI_MAXJ * 268);
+    if (!sb || !hd || !ns || !nbo || !bo || !nko || !ko || !to) return st.finish();
+    const uint8_t *cells = (const uint8_t *)ctx->slot[S_W5].p;
+    {
+        PROF(ctx, "etsi_lmac");
+        hipLaunchKernelGGL(k_lmac_etsi, dim3((unsigned)C), dim3(64), 0, ctx->stream, sb, hd, ns, (int)smax, cells,
+                           cells + ctx->cells * 432, nbo, bo, nko, ko, to);
+    }
+    return st.finish();
+}
+
+int tetra_etsi_decode_blocks(tetra_ctx *ctx, const int8_t *soft5, size_t F, int kind, const uint32_t *scramb_init,
+                             uint8_t *type1, uint8_t *crc_ok) {
+    if (!ctx || kind < 0 || kind > 2) return TETRA_E_INVALID;
+    if (F == 0) return TETRA_OK;
+    const KindP P = kind_params(kind);
+    std::vector<uint32_t> init(F);
+    HIP_TRY(ctx, hipMemcpy(init.data(), scramb_init, F * 4, hipMemcpyDefault));
+    std::vector<uint8_t> tab(F * P.K);
+    for (size_t f = 0; f < F; ++f) scramble_seq(init[f], P.K, tab.data() + f * P.K);
+    Staging st(ctx);
+    const int8_t *s = (const int8_t *)st.in(soft5, F * P.K);
+    const uint8_t *scr = (const uint8_t *)st.in(tab.data(), tab.size());
+    uint8_t *t = (uint8_t *)st.out(type1, F * P.n1);
+    uint8_t *o = (uint8_t *)st.out(crc_ok, F);
+    if (!s || !scr || !t || !o) return st.finish();
+    {
+        PROF(ctx, "etsi_decode_blocks");
+        hipLaunchKernelGGL(k_decode_blocks, dim3((unsigned)((F + 3) / 4)), dim3(64), 0, ctx->stream, s, (int)F, kind,
+                           scr, t, o);
+    }
+    return st.finish();
+}
+
+int tetra_etsi_encode_blocks(tetra_ctx *ctx, const uint8_t *type1, size_t F, int kind, const uint32_t *scramb_init,
+                             uint8_t *type5) {
+    if (!ctx || kind < 0 || kind > 2) return TETRA_E_INVALID;
+    if (F == 0) return TETRA_OK;
+    const KindP P = kind_params(kind);
+    std::vector<uint32_t> init(F);
+    HIP_TRY(ctx, hipMemcpy(init.data(), scramb_init, F * 4, hipMemcpyDefault));
+    std::vector<uint8_t> tab(F * P.K);
+    for (size_t f = 0; f < F; ++f) scramble_seq(init[f], P.K, tab.data() + f * P.K);
+    Staging st(ctx);
+    const uint8_t *t = (const uint8_t *)st.in(type1, F * P.n1);
+    const uint8_t *scr = (const uint8_t *)st.in(tab.data(), tab.size());
+    uint8_t *o = (uint8_t *)st.out(type5, F * P.K);
+    if (!t || !scr || !o) return st.finish();
+    hipLaunchKernelGGL(k_encode_blocks, dim3((unsigned)((F + 63) / 64)), dim3(64), 0, ctx->stream, t, (int)F, kind, scr,
+                       o);
+    return st.finish();
+}
+
+}  // extern "C"

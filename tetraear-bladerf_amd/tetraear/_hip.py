@@ -35,6 +35,17 @@ class CompatPlan(ctypes.Structure):
     ]
 
 
+class EtsiPlan(ctypes.Structure):
+    """Mirror of struct tetra_etsi_plan (include/tetra_hip.h)."""
+    _fields_ = [
+        ("q1", ctypes.c_int32), ("L1", ctypes.c_int32), ("Lp", ctypes.c_int32), ("up", ctypes.c_int32),
+        ("down", ctypes.c_int32), ("gain", ctypes.c_float), ("soft_scale", ctypes.c_float),
+        ("reserved", ctypes.c_int32), ("h1", ctypes.c_float * 64), ("hp", ctypes.c_float * 384),
+    ]
+
+
+ETSI_MAXB, ETSI_MAXJ = 8, 16
+
 _lib = None
 _lib_lock = threading.Lock()
 _tls = threading.local()
@@ -73,6 +84,17 @@ def _bind(L):
         "tetra_parse_bursts": (_i32, [_vp, _vp, _sz, _vp, _vp, _vp]),
         "tetra_crc16": (_i32, [_vp, _vp, _sz, _sz, _i32, _vp]),
         "tetra_check_crc": (_i32, [_vp, _vp, _sz, _sz, _vp]),
+        "tetra_etsi_lengths": (_i32, [ctypes.POINTER(EtsiPlan), _sz, _vp, _vp, _vp]),
+        "tetra_etsi_chanfilt": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _sz, _sz, _vp]),
+        "tetra_etsi_timing": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _sz, _sz, _vp, _vp, _vp, _vp, _sz, _vp]),
+        "tetra_demod_etsi": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _sz, _sz, _vp, _vp, _vp, _vp, _sz, _vp]),
+        "tetra_etsi_set_cells": (_i32, [_vp, _vp, _sz]),
+        "tetra_lmac_etsi": (_i32, [_vp, _vp, _vp, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp]),
+        "tetra_etsi_decode_blocks": (_i32, [_vp, _vp, _sz, _i32, _vp, _vp, _vp]),
+        "tetra_etsi_encode_blocks": (_i32, [_vp, _vp, _sz, _i32, _vp, _vp]),
+        "tetra_synth_bursts_per_channel": (_i32, [_sz, ctypes.c_double]),
+        "tetra_synth_etsi": (_i32, [_vp, _sz, _sz, ctypes.c_double, ctypes.c_uint64, ctypes.c_float, ctypes.c_float,
+                                    _vp, _vp, _vp, _vp, _vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -1,0 +1,226 @@
+"""ETSI EN 300 392-2 demodulator (north-star chain) on the GPU.
+
+The reference demodulates with integer samples/symbol and shifted decision regions
+(/root/reference/tetraear/signal/processor.py:152-183).  This receiver is the
+standard one BASELINE.json's north_star names: polyphase channel filter + RRC(0.35) matched
+filter resampled to 4 samples/symbol, Oerder-Meyr timing acquisition with block-Gardner
+tracking, pi/4-DQPSK differential decision per Table 5.1 with a 4th-power CFO correction, and
+int8 soft bits for the channel decoder.  All sample work runs in libtetra_hip.so
+(k_chanfilt, k_timing); this module designs the filters and moves arrays.
+"""
+import ctypes
+import functools
+
+import numpy as np
+from scipy import signal as _design
+
+from tetraear import _hip
+
+SYMBOL_RATE = 18000.0
+
+
+def rrc(t, alpha=0.35):
+    """Root-raised-cosine impulse response at t symbol periods (unit-energy pulse)."""
+    t = np.asarray(t, np.float64)
+    out = np.empty_like(t)
+    z = np.abs(t) < 1e-9
+    out[z] = 1.0 - alpha + 4 * alpha / np.pi
+    s = np.abs(np.abs(4 * alpha * t) - 1.0) < 1e-9
+    out[s] = (alpha / np.sqrt(2)) * ((1 + 2 / np.pi) * np.sin(np.pi / (4 * alpha))
+                                     + (1 - 2 / np.pi) * np.cos(np.pi / (4 * alpha)))
+    o = ~(z | s)
+    tt = t[o]
+    out[o] = (np.sin(np.pi * tt * (1 - alpha)) + 4 * alpha * tt * np.cos(np.pi * tt * (1 + alpha))) / \
+        (np.pi * tt * (1 - (4 * alpha * tt) ** 2))
+    return out
+
+
+@functools.lru_cache(maxsize=8)
+def etsi_plan(fs=2.4e6):
+    """Receiver design for input rate fs (= 10 x 240 kHz)."""
+    q1 = int(round(fs / 240000.0))
+    if q1 != 10 or abs(q1 * 240000.0 - fs) > 1e-6:
+        raise ValueError("the ETSI receiver is built for 2.4 MSps channel captures (10 x 240 kHz)")
+    p = _hip.EtsiPlan()
+    p.q1, p.L1, p.Lp, p.up, p.down = q1, 48, 321, 3, 10
+    p.gain, p.soft_scale = 1.5, 64.0
+    h1 = _design.firwin(48, 60e3, fs=fs, window=("kaiser", 6.0)).astype(np.float32)
+    hp = rrc((np.arange(321) - 160) / 40.0).astype(np.float32)
+    for i, v in enumerate(h1):
+        p.h1[i] = v
+    for i, v in enumerate(hp):
+        p.hp[i] = v
+    return p
+
+
+def lengths(plan, n):
+    m1, m2, sm = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    _hip.lib().tetra_etsi_lengths(plan, n, ctypes.byref(m1), ctypes.byref(m2), ctypes.byref(sm))
+    return m1.value, m2.value, sm.value
+
+
+class SoftSymbols(np.ndarray):
+    """uint8 hard dibit symbols (what process() returns) that also carry ``soft_bits`` (int8, >0 = 0)
+    so TetraDecoder(mode='etsi').decode() can run the soft-decision Viterbi on them."""
+
+    def __new__(cls, hard, soft_bits):
+        obj = np.asarray(hard, np.uint8).view(cls)
+        obj.soft_bits = soft_bits
+        return obj
+
+    def __array_finalize__(self, obj):
+        self.soft_bits = getattr(obj, "soft_bits", None)
+
+
+class EtsiReceiver:
+    def __init__(self, sample_rate=2.4e6):
+        self.sample_rate = sample_rate
+        self.plan = etsi_plan(sample_rate)
+        self.diag = None
+
+    def demod_batch(self, iq):
+        """[C, N] complex -> (hard [C, smax] u8, soft_bits [C, 2*smax] i8, symbols [C, smax] c64, nsym [C])."""
+        x = np.ascontiguousarray(iq, dtype=np.complex64)
+        C, N = x.shape
+        if N % 2:
+            x = np.ascontiguousarray(x[:, :N - 1])
+            N -= 1
+        _, _, smax = lengths(self.plan, N)
+        sym = np.zeros((C, smax), np.complex64)
+        soft = np.zeros((C, 2 * smax), np.int8)
+        hard = np.zeros((C, smax), np.uint8)
+        ns = np.zeros(C, np.int32)
+        diag = np.zeros((C, 4), np.float32)
+        c = _hip.ctx()
+        c.check(c.lib.tetra_demod_etsi(c.handle, self.plan, _hip.ptr(x), C, N, _hip.ptr(sym), _hip.ptr(soft),
+                                       _hip.ptr(hard), _hip.ptr(ns), smax, _hip.ptr(diag)), "tetra_demod_etsi")
+        self.diag = diag
+        return hard, soft, sym, ns
+
+    def process(self, samples, freq_offset=0):
+        """One chunk -> (SoftSymbols hard dibits, complex64 symbol-rate samples)."""
+        x = np.ascontiguousarray(samples, np.complex64)
+        if freq_offset and len(x):   # AFC mixer on the GPU (same kernel as frequency_shift)
+            from tetraear.signal.processor import mixer_coefficient
+            out = np.empty(len(x), np.complex128)
+            cf = np.array([mixer_coefficient(freq_offset)], np.float64)
+            c = _hip.ctx()
+            c.check(c.lib.tetra_frequency_shift(c.handle, _hip.ptr(x), _hip.TETRA_CF32, 1, len(x), _hip.ptr(cf),
+                                                float(self.sample_rate), _hip.ptr(out)), "tetra_frequency_shift")
+            x = out.astype(np.complex64)
+        _, _, smax = lengths(self.plan, len(x) - len(x) % 2)
+        if len(x) < 2 or smax <= 2 or lengths(self.plan, len(x) - len(x) % 2)[1] < 16:
+            return SoftSymbols(np.zeros(0, np.uint8), np.zeros(0, np.int8)), np.zeros(0, np.complex64)
+        hard, soft, sym, ns = self.demod_batch(x[None, :])
+        n = int(ns[0])
+        nd = max(0, n - 1)
+        return SoftSymbols(hard[0, :nd].copy(), soft[0, :2 * nd].copy()), sym[0, :n].copy()
+
+    def decide(self, symbols):
+        raise NotImplementedError("the ETSI decision runs inside the fused demod (use process())")
+
+
+def synth(C, N, fs=2.4e6, seed=1, snr_db=None, cfo_max=600.0, device_arrays=None):
+    """Device-generated synthetic capture (host copies returned).  See tetra_synth_etsi."""
+    nb = _hip.lib().tetra_synth_bursts_per_channel(N, fs)
+    iq = np.zeros((C, N), np.complex64)
+    cells = np.zeros(C, np.uint32)
+    kinds = np.zeros((C, nb), np.int32)
+    payload = np.zeros((C, nb, 2, 268), np.uint8)
+    t0 = np.zeros(C, np.float64)
+    c = _hip.ctx()
+    c.check(c.lib.tetra_synth_etsi(c.handle, C, N, fs, seed, 1000.0 if snr_db is None else float(snr_db),
+                                   float(cfo_max), _hip.ptr(iq), _hip.ptr(cells), _hip.ptr(kinds),
+                                   _hip.ptr(payload), _hip.ptr(t0)), "tetra_synth_etsi")
+    return iq, cells, kinds, payload, t0
+
+
+class BenchStep:
+    """bench.py workload: device-resident synthetic capture -> demod -> lower MAC, all on one stream."""
+
+    dtype = "f32 (DSP), int8/int32 (Viterbi)"
+
+    def __init__(self, c, C, N, fs, seed, device, snr_db=18.0):
+        import torch
+        self.c, self.C, self.N, self.fs = c, C, N, fs
+        self.plan = etsi_plan(fs)
+        _, self.M2, self.smax = lengths(self.plan, N)
+        nb = c.lib.tetra_synth_bursts_per_channel(N, fs)
+        self.iq = torch.empty((C, N, 2), dtype=torch.float32, device=device)
+        self.cells = torch.empty(C, dtype=torch.int32, device=device)
+        self.kinds = torch.empty((C, nb), dtype=torch.int32, device=device)
+        self.payload = torch.empty((C, nb, 2, 268), dtype=torch.uint8, device=device)
+        c.check(c.lib.tetra_synth_etsi(c.handle, C, N, fs, seed, snr_db, 600.0, _hip.ptr(self.iq), _hip.ptr(self.cells),
+                                       _hip.ptr(self.kinds), _hip.ptr(self.payload), None), "synth")
+        c.check(c.lib.tetra_etsi_set_cells(c.handle, _hip.ptr(self.cells), C), "set_cells")
+        sm = self.smax
+        self.sym = torch.empty((C, sm, 2), dtype=torch.float32, device=device)
+        self.soft = torch.empty((C, 2 * sm), dtype=torch.int8, device=device)
+        self.hard = torch.empty((C, sm), dtype=torch.uint8, device=device)
+        self.nsym = torch.empty(C, dtype=torch.int32, device=device)
+        self.nburst = torch.empty(C, dtype=torch.int32, device=device)
+        self.bursts = torch.empty((C, _hip.ETSI_MAXB, 2), dtype=torch.int32, device=device)
+        self.nblock = torch.empty(C, dtype=torch.int32, device=device)
+        self.blocks = torch.empty((C, _hip.ETSI_MAXJ, 4), dtype=torch.int32, device=device)
+        self.type1 = torch.empty((C, _hip.ETSI_MAXJ, 268), dtype=torch.uint8, device=device)
+
+    def __call__(self):
+        c = self.c
+        c.check(c.lib.tetra_demod_etsi(c.handle, self.plan, _hip.ptr(self.iq), self.C, self.N, _hip.ptr(self.sym),
+                                       _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.smax, None),
+                "demod_etsi")
+        c.check(c.lib.tetra_lmac_etsi(c.handle, _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.C,
+                                      self.smax, _hip.ptr(self.nburst), _hip.ptr(self.bursts), _hip.ptr(self.nblock),
+                                      _hip.ptr(self.blocks), _hip.ptr(self.type1)), "lmac_etsi")
+
+    def dominant(self):
+        # k_chanfilt: reads 8 B per input sample, writes 8 B per 72 kHz output (3/100 per input)
+        return ("etsi_chanfilt", 8.0 + 8.0 * 0.03)
+
+    def quality(self):
+        """Decoded-block statistics of the last step (device results, checked on the host)."""
+        nb = self.nblock.cpu().numpy()
+        blocks = self.blocks.cpu().numpy()
+        ok = sum(int(blocks[i, :nb[i], 1].sum()) for i in range(self.C))
+        return dict(blocks=int(nb.sum()), crc_ok=ok, bursts=int(self.nburst.sum().item()))
+
+    def cpu_baseline(self, budget_s):
+        import os
+        import sys
+        import time
+        repo = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+        sys.path.insert(0, os.path.join(repo, "oracle"))
+        import etsi as oracle   # the CPU restatement (cpu_baseline leg only)
+        x = self.iq[:4].cpu().numpy().view(np.complex64)[..., 0]
+        cells = self.cells[:4].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+        rx = oracle.Receiver(self.fs)
+        t0 = time.perf_counter()
+        n = 0
+        while time.perf_counter() - t0 < budget_s:
+            sym, soft, hard, _ = rx.demod(x[n % 4])
+            rx.lower_mac(soft, hard, int(cells[n % 4]))
+            n += 1
+        dt = time.perf_counter() - t0
+        return dict(value=n * self.N / dt / 1e6, unit="Msamples/s", cores=1, kind="port",
+                    sample=f"{n} channel chunks x {self.N} cf32 @2.4 MSps through the C oracle "
+                           f"(chanfilt+timing+sync+Viterbi), 1 thread")
+
+
+def smoke_check():
+    """Tiny ETSI round trip on the GPU (used by __graft_entry__.smoke)."""
+    from tetraear.core.etsi import EtsiLowerMac
+    iq, cells, kinds, payload, t0 = synth(2, 131072, seed=7, snr_db=20.0)
+    rx = EtsiReceiver()
+    lm = EtsiLowerMac()
+    hard, soft, sym, ns = rx.demod_batch(iq)
+    res = lm.decode_batch(soft, hard, ns, cells)
+    nok = 0
+    for ch, frames in enumerate(res):
+        sent = {tuple(p) for bb in payload[ch] for p in bb}
+        for f in frames:
+            for b in f["blocks"]:
+                if b["crc_ok"]:
+                    nok += 1
+                    padded = tuple(np.pad(b["bits"], (0, 268 - len(b["bits"]))))
+                    assert padded in sent, "decoded payload is not a transmitted block"
+    assert nok >= 4, f"ETSI smoke: only {nok} blocks passed CRC"
