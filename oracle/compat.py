@@ -30,9 +30,12 @@ def lib():
     global _LIB
     if _LIB is None:
         path = os.path.join(_HERE, "liboracle.so")
-        if not os.path.exists(path):
-            import subprocess
-            subprocess.check_call(["make", "-s", "-C", _HERE])
+        import subprocess
+        try:   # keep the checker in step with its sources (no-op when up to date)
+            subprocess.check_call(["make", "-s", "-C", _HERE], stdout=subprocess.DEVNULL)
+        except (OSError, subprocess.CalledProcessError):
+            if not os.path.exists(path):
+                raise
         L = ctypes.CDLL(path)
         f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
         f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")

@@ -93,7 +93,7 @@ def test_block_codec_vs_oracle(kind):
     c.check(c.lib.tetra_etsi_encode_blocks(c.handle, _hip.ptr(t1), F, kind, _hip.ptr(inits), _hip.ptr(t5)))
     for f in range(F):
         assert np.array_equal(t5[f], E.encode_block(t1[f], kind, E.scramble_seq(int(inits[f]), K)))
-    soft = (np.where(t5 == 0, 40, -40) + rng.normal(0, 30, t5.shape)).clip(-127, 127).astype(np.int8)
+    soft = (np.where(t5 == 0, 40, -40) + rng.normal(0, 16, t5.shape)).clip(-127, 127).astype(np.int8)
     soft[F // 2:] = rng.integers(-127, 128, (F - F // 2, K)).astype(np.int8)   # pure noise: ties, CRC fails
     dec = np.zeros((F, n1), np.uint8)
     ok = np.zeros(F, np.uint8)
