@@ -39,8 +39,10 @@ __global__ __launch_bounds__(256) void k_chanfilt(const float4 *__restrict__ iq,
                                                   int Lp, float2 *__restrict__ y) {
     __shared__ float2 xin[TILE_IN + HALO];
     __shared__ float2 ring[RING];
+    __shared__ float hps[384];
     const int ch = blockIdx.x;
     const int tid = threadIdx.x;
+    for (int i = tid; i < Lp; i += 256) hps[i] = hp[i];
     const float4 *xp = iq + (size_t)ch * (N / 2);   // N even: 2 complex samples per float4
     float2 *yp = y + (size_t)ch * M2;
     float hr[48];
@@ -84,27 +86,32 @@ __global__ __launch_bounds__(256) void k_chanfilt(const float4 *__restrict__ iq,
         __syncthreads();
         // halo for the next tile: its xin[0..48) = this tile's xin[2560..2608)
         if (tid < HALO) xin[tid] = xin[TILE_IN + tid];
-        // stage 2: outputs m whose taps end at or before the last stage-1 output available
+        // stage 2 (every third tile, so ~230 of 256 threads have an output): outputs m whose
+        // taps end at or before the last stage-1 output available
         const int kav = min(kfirst + TILE_K - 1, M1 - 1);
-        const int num = 3 * kav + 2 - (Lp - 1);   // largest m with floor((Lp-1+10m)/3) <= kav
-        int m_hi = num >= 0 ? num / 10 : -1;
-        if (m_hi > M2 - 1) m_hi = M2 - 1;
-        for (int m0 = m_done; m0 <= m_hi; m0 += 256) {
-            const int m = m0 + tid;
-            if (m <= m_hi) {
-                const int n = (Lp - 1) + 10 * m;
-                const int kmin = (10 * m + 2) / 3, kmax = n / 3;
-                float ar = 0.f, ai = 0.f;
-                for (int kk = kmin; kk <= kmax; ++kk) {
-                    const float h = hp[n - 3 * kk];
-                    const float2 v = ring[kk & (RING - 1)];
-                    ar = fmaf(h, v.x, ar);
-                    ai = fmaf(h, v.y, ai);
+        if (t % 3 == 2 || kav == M1 - 1) {
+            const int num = 3 * kav + 2 - (Lp - 1);   // largest m with floor((Lp-1+10m)/3) <= kav
+            int m_hi = num >= 0 ? num / 10 : -1;
+            if (m_hi > M2 - 1) m_hi = M2 - 1;
+            for (int m0 = m_done; m0 <= m_hi; m0 += 256) {
+                const int m = m0 + tid;
+                if (m <= m_hi) {
+                    const int n = (Lp - 1) + 10 * m;
+                    const int kmin = (10 * m + 2) / 3, kmax = n / 3;
+                    float ar = 0.f, ai = 0.f;
+                    int i = n - 3 * kmin;   // tap index, decreasing by 3 as k ascends
+#pragma unroll 8
+                    for (int kk = kmin; kk <= kmax; ++kk, i -= 3) {
+                        const float h = hps[i];
+                        const float2 v = ring[kk & (RING - 1)];
+                        ar = fmaf(h, v.x, ar);
+                        ai = fmaf(h, v.y, ai);
+                    }
+                    yp[m] = make_float2(ar, ai);
                 }
-                yp[m] = make_float2(ar, ai);
             }
+            if (m_hi + 1 > m_done) m_done = m_hi + 1;
         }
-        if (m_hi + 1 > m_done) m_done = m_hi + 1;
         __syncthreads();
     }
 }
