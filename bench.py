@@ -47,6 +47,23 @@ def parse():
     return ap.parse_args()
 
 
+def traffic_from_profiles(kernel, workload_key):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of this
+    workload (profiles/*_summary.json, written by tools/pmc_summary.py from separate FETCH_SIZE /
+    WRITE_SIZE passes with the gfx950 x2 FETCH correction), or None."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_summary.json"))):
+        try:
+            d = json.load(open(f))
+        except ValueError:
+            continue
+        k = d.get("kernels", {}).get(kernel, {})
+        if workload_key in d.get("workload", "") and "hbm_bytes_per_launch" in k:
+            best = (k["hbm_bytes_per_launch"], os.path.basename(f))
+    return None if best is None else {"bytes": best[0], "source": best[1]}
+
+
 def read_profile(c):
     names = ctypes.create_string_buffer(4096)
     ms = (ctypes.c_double * 64)()
@@ -100,7 +117,7 @@ class CompatStep:
         return 8.0 + 17.0 * 18000.0 / FS
 
     def dominant(self):
-        return ("compat_sos_fwd", 8.0)   # reads each input sample once (8 B)
+        return ("compat_sos_fwd", 8.0, "k_sos_fwd")   # reads each input sample once (8 B)
 
     def cpu_baseline(self, budget_s):
         sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -173,7 +190,7 @@ def main():
     value = total_samples / elapsed / 1e6
 
     if rank == 0:
-        name, per_sample = step.dominant()
+        name, per_sample, ksym = step.dominant()
         kms, kcnt = prof.get(name, (0.0, 0))
         launch_ms = kms / max(1, kcnt)
         units_per_launch = C * N
@@ -200,8 +217,10 @@ def main():
             "realtime_channels": int(value * 1e6 / FS),
             "roofline": {
                 "bound": "hbm", "kernel": name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic_from_profiles(ksym, f"{C} channels x {N}"),
                 "launch_ms": round(launch_ms, 4), "algorithmic_bytes_per_launch": per_sample * units_per_launch,
+                "kernel_symbol": ksym,
             },
             "stages_ms_per_step": {k: round(v[0] / a.steps, 4) for k, v in prof.items()},
             "cpu_baseline": cpu,

@@ -175,7 +175,7 @@ class BenchStep:
 
     def dominant(self):
         # k_chanfilt: reads 8 B per input sample, writes 8 B per 72 kHz output (3/100 per input)
-        return ("etsi_chanfilt", 8.0 + 8.0 * 0.03)
+        return ("etsi_chanfilt", 8.0 + 8.0 * 0.03, "k_chanfilt")
 
     def quality(self):
         """Decoded-block statistics of the last step (device results, checked on the host)."""
