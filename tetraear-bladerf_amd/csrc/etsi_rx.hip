@@ -303,42 +303,64 @@ __device__ __forceinline__ int punct_index(int j1) {   // rate 2/3, t=3, P=(1,2,
 
 constexpr int LMAC_MAXBITS = 2 * 2048;
 
-// One wave per channel.  bursts [C][8][2] (start, kind); blocks [C][16][4] (kind, crc_ok, burst, block);
-// type1 [C][16][268].
-__global__ __launch_bounds__(64) void k_lmac_etsi(const int8_t *__restrict__ softbits, const uint8_t *__restrict__ hard,
-                                                  const int32_t *__restrict__ nsym, int smax,
-                                                  const uint8_t *__restrict__ cell_scr, const uint8_t *__restrict__ bsch_scr,
-                                                  int32_t *__restrict__ nburst, int32_t *__restrict__ bursts,
-                                                  int32_t *__restrict__ nblock, int32_t *__restrict__ blocks,
-                                                  uint8_t *__restrict__ type1) {
+// CRC-16 register as a linear function of the bits (GF(2)): reg(L bits) = INIT[L] ^ XOR over
+// 1-bits at distance d from the end of T[d].  Lets the serial traceback, which emits bits last
+// to first, check the CRC on the fly instead of a second serial pass.
+struct CrcTab {
+    uint16_t t[288];
+    uint16_t init[289];
+};
+constexpr uint32_t crc_step(uint32_t r) { return ((r & 0x8000u) ? ((r << 1) ^ 0x1021u) : (r << 1)) & 0xFFFFu; }
+constexpr CrcTab make_crc_tab() {
+    CrcTab c{};
+    uint32_t r = crc_step(0x8000u);
+    for (int d = 0; d < 288; ++d) { c.t[d] = (uint16_t)r; r = crc_step(r); }
+    uint32_t s = 0xFFFFu;
+    for (int L = 0; L <= 288; ++L) { c.init[L] = (uint16_t)s; s = crc_step(s); }
+    return c;
+}
+__constant__ CrcTab CRC_TAB = make_crc_tab();
+
+// --------------------------------------------------------------------------- E3 burst sync
+struct Job {
+    int ch, slot, burst, blk, kind, off;
+};
+
+// One wave per channel: pack hard bits, greedy burst scan, then allocate this channel's coded
+// blocks a dense range of job indices (one atomic per channel; outputs are indexed by
+// (channel, slot), so results do not depend on the allocation order).
+__global__ __launch_bounds__(64) void k_etsi_sync(const uint8_t *__restrict__ hard, const int32_t *__restrict__ nsym,
+                                                  int smax, int32_t *__restrict__ nburst, int32_t *__restrict__ bursts,
+                                                  int32_t *__restrict__ nblock, int32_t *__restrict__ jcount,
+                                                  Job *__restrict__ jobs) {
     const int ch = blockIdx.x, lane = threadIdx.x;
     __shared__ uint64_t words[LMAC_MAXBITS / 64 + 2];
-    __shared__ int8_t ms[4][4 * 288];
-    __shared__ uint64_t surv[288];
-    __shared__ uint8_t t2[4][288];
     __shared__ int bstart[ETSI_MAXB], bkind[ETSI_MAXB];
     const int S = nsym[ch];
     int nbits = 2 * (S > 1 ? S - 1 : 0);
     if (nbits > LMAC_MAXBITS) nbits = LMAC_MAXBITS;
     const uint8_t *hp = hard + (size_t)ch * smax;
-    const int8_t *sb = softbits + (size_t)ch * 2 * smax;
-    // pack hard bits: bit 2i = b1 of dibit i, 2i+1 = b2
-    const int nw = (nbits + 63) / 64;
-    for (int w = lane; w < nw + 2; w += 64) {
-        uint64_t v = 0;
-        if (w < nw) {
-            for (int b = 0; b < 64; ++b) {
-                const int i = 64 * w + b;
-                if (i < nbits) {
-                    const uint32_t h = hp[i >> 1];
-                    v |= (uint64_t)((i & 1) ? (h & 1u) : (h >> 1)) << b;
-                }
-            }
+    // pack hard bits with ballots: 64 dibit symbols per step -> 2 words (bit 2i = b1, 2i+1 = b2)
+    const int nsy = nbits / 2;
+    for (int s0 = 0; s0 < nsy + 64; s0 += 64) {
+        const int s = s0 + lane;
+        const uint32_t h = s < nsy ? hp[s] : 0u;
+        const uint64_t m1 = __ballot((h >> 1) & 1u), m2 = __ballot(h & 1u);
+        auto spread = [](uint64_t x) {   // bit i -> bit 2i (32 -> 64)
+            x &= 0xFFFFFFFFull;
+            x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+            x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+            x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+            x = (x | (x << 2)) & 0x3333333333333333ull;
+            x = (x | (x << 1)) & 0x5555555555555555ull;
+            return x;
+        };
+        if (lane == 0 && s0 / 32 + 1 < LMAC_MAXBITS / 64 + 2) {
+            words[s0 / 32] = spread(m1) | (spread(m2) << 1);
+            words[s0 / 32 + 1] = spread(m1 >> 32) | (spread(m2 >> 32) << 1);
         }
-        words[w] = v;
     }
     __syncthreads();
-    // greedy burst scan
     int nb = 0;
     for (int cur = 0; cur + 510 <= nbits && nb < ETSI_MAXB;) {
         const int s = cur + lane;
@@ -364,104 +386,136 @@ __global__ __launch_bounds__(64) void k_lmac_etsi(const int8_t *__restrict__ sof
         }
     }
     __syncthreads();
-    // block jobs
-    int njob = 0;
-    int jb[ETSI_MAXJ], jk[ETSI_MAXJ], joff[ETSI_MAXJ], jblk[ETSI_MAXJ];
-    for (int b = 0; b < nb; ++b) {
-        const int s = bstart[b], k = bkind[b];
-        if (k == 0) { jb[njob] = b; jk[njob] = 0; joff[njob] = s + 14; jblk[njob] = 0; ++njob; }
-        else if (k == 1) {
-            jb[njob] = b; jk[njob] = 1; joff[njob] = s + 14; jblk[njob] = 0; ++njob;
-            jb[njob] = b; jk[njob] = 1; joff[njob] = s + 282; jblk[njob] = 1; ++njob;
-        } else {
-            jb[njob] = b; jk[njob] = 2; joff[njob] = s + 94; jblk[njob] = 0; ++njob;
-            jb[njob] = b; jk[njob] = 1; joff[njob] = s + 282; jblk[njob] = 1; ++njob;
-        }
-    }
     if (lane == 0) {
+        int njob = 0;
+        for (int b = 0; b < nb; ++b) njob += bkind[b] == 0 ? 1 : 2;
         nburst[ch] = nb;
         nblock[ch] = njob;
+        const int base = njob ? atomicAdd(jcount, njob) : 0;
+        int q = 0;
+        for (int b = 0; b < nb; ++b) {
+            const int s = bstart[b], k = bkind[b];
+            bursts[((size_t)ch * ETSI_MAXB + b) * 2] = s;
+            bursts[((size_t)ch * ETSI_MAXB + b) * 2 + 1] = k;
+            if (k == 0) {
+                jobs[base + q] = Job{ch, q, b, 0, 0, s + 14}; ++q;
+            } else if (k == 1) {
+                jobs[base + q] = Job{ch, q, b, 0, 1, s + 14}; ++q;
+                jobs[base + q] = Job{ch, q, b, 1, 1, s + 282}; ++q;
+            } else {
+                jobs[base + q] = Job{ch, q, b, 0, 2, s + 94}; ++q;
+                jobs[base + q] = Job{ch, q, b, 1, 1, s + 282}; ++q;
+            }
+        }
     }
-    for (int b = lane; b < nb; b += 64) {
-        bursts[((size_t)ch * ETSI_MAXB + b) * 2] = bstart[b];
-        bursts[((size_t)ch * ETSI_MAXB + b) * 2 + 1] = bkind[b];
+}
+
+// --------------------------------------------------------------------------- E4 Viterbi
+// One LANE per coded block: descramble + deinterleave into an LDS row, then the 16-state trellis
+// with all path metrics in registers (no cross-lane traffic), survivors stored [step][job]
+// (coalesced across the wave), traceback with the CRC accumulated on the fly.
+constexpr int VROW = 436;   // LDS row per lane: 432 type-3 values, padded to 109 dwords (bank spread)
+
+template <int PAIRS>
+__device__ __forceinline__ void acs_pairs(int32_t (&pm)[16], const int8_t *row, uint16_t *sv, size_t sstride) {
+    // rate-2/3 puncturing: step 2g sees mother outputs (g1, g2) = type-3 (3g, 3g+1); step 2g+1 sees
+    // g1 = type-3 3g+2; the other mother outputs are erased.
+    for (int g = 0; g < PAIRS; ++g) {
+        const int32_t a = row[3 * g], b = row[3 * g + 1], c = row[3 * g + 2];
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            int32_t nm[16];
+            uint32_t bits = 0;
+#pragma unroll
+            for (int n = 0; n < 16; ++n) {
+                const int bb = n & 1, d0 = (n >> 1) & 1, d1 = (n >> 2) & 1, d2 = (n >> 3) & 1;
+                // branch metric for d3 = 0; d3 = 1 flips every generator output (negates it)
+                int32_t v;
+                if (half == 0) v = ((bb ^ d0) ? -a : a) + ((bb ^ d1 ^ d2) ? -b : b);
+                else v = (bb ^ d0) ? -c : c;
+                const int32_t m0 = pm[n >> 1] + v, m1 = pm[(n >> 1) | 8] - v;
+                const bool t1 = m1 > m0;
+                nm[n] = t1 ? m1 : m0;
+                bits |= (uint32_t)t1 << n;
+            }
+#pragma unroll
+            for (int n = 0; n < 16; ++n) pm[n] = nm[n];
+            sv[(size_t)(2 * g + half) * sstride] = (uint16_t)bits;
+        }
     }
-    const uint8_t *cscr = cell_scr + (size_t)ch * 432;
-    const int g = lane >> 4, st = lane & 15;
-    for (int j0 = 0; j0 < njob; j0 += 4) {
-        // --- descramble + deinterleave + depuncture into ms[g] (4 jobs, 16 lanes each)
-        const int j = j0 + g;
-        const bool act = j < njob;
-        const KindP P = kind_params(act ? jk[j] : 1);
-        const uint8_t *scr = (act && jk[j] == 2) ? bsch_scr : cscr;
-        if (act) {
-            for (int i = st; i < 4 * P.n2; i += 16) ms[g][i] = 0;
+}
+
+__global__ __launch_bounds__(64) void k_etsi_viterbi(const Job *__restrict__ jobs, const int32_t *__restrict__ jcount,
+                                                     int jmax, const int8_t *__restrict__ softbits, int smax,
+                                                     const uint8_t *__restrict__ cell_scr,
+                                                     const uint8_t *__restrict__ bsch_scr,
+                                                     uint16_t *__restrict__ surv, int32_t *__restrict__ blocks,
+                                                     uint8_t *__restrict__ type1) {
+    __shared__ __attribute__((aligned(16))) int8_t rows[64 * VROW];
+    const int lane = threadIdx.x;
+    const int j = blockIdx.x * 64 + lane;
+    const int nj = *jcount;
+    if (blockIdx.x * 64 >= nj) return;   // whole wave past the job count
+    const bool act = j < nj;
+    Job jb = act ? jobs[j] : Job{0, 0, 0, 0, 1, 0};
+    const KindP P = kind_params(jb.kind);
+    int8_t *row = rows + lane * VROW;
+    if (act) {
+        const int8_t *sb = softbits + (size_t)jb.ch * 2 * smax + jb.off;
+        const uint8_t *scr = jb.kind == 2 ? bsch_scr : cell_scr + (size_t)jb.ch * 432;
+        int r = 0;   // a*i mod K, incrementally
+        for (int i0 = 1; i0 <= P.K; i0 += 8) {   // K is a multiple of 8: gathers issued 8 ahead
+            int kk[8];
+            int8_t v[8];
+            uint8_t sc[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                r += P.a;
+                if (r >= P.K) r -= P.K;
+                kk[u] = r;   // 0-based type-5 index: k(i) - 1 = (a*i mod K)
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int pos = (jb.kind == 0 && kk[u] >= 216) ? kk[u] + 52 : kk[u];   // SCH/F: BKN2 268 after BKN1
+                v[u] = sb[pos];
+                sc[u] = scr[kk[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) row[i0 - 1 + u] = sc[u] ? (int8_t)(-v[u]) : v[u];
         }
-        __syncthreads();
-        if (act) {
-            const int o = joff[j];
-            const bool two = jk[j] == 0;   // SCH/F: BKN1 (14..229) ++ BKN2 (282..497)
-            for (int i = 1 + st; i <= P.K; i += 16) {
-                const int k = 1 + (int)(((long)P.a * i) % P.K);
-                const int pos = two ? (k - 1 < 216 ? o + (k - 1) : o + 268 + (k - 1 - 216)) + 0 : o + (k - 1);
-                const int8_t v = sb[pos];
-                const int8_t d = scr[k - 1] ? (int8_t)(-v) : v;
-                ms[g][punct_index(i) - 1] = d;
+    }
+    int32_t pm[16];
+#pragma unroll
+    for (int n = 0; n < 16; ++n) pm[n] = n == 0 ? 0 : -(1 << 28);
+    uint16_t *sv = surv + j;
+    const size_t ss = (size_t)jmax;
+    if (act) {
+        if (P.n2 == 288) acs_pairs<144>(pm, row, sv, ss);
+        else if (P.n2 == 144) acs_pairs<72>(pm, row, sv, ss);
+        else acs_pairs<40>(pm, row, sv, ss);
+        // traceback from state 0 (tail bits), CRC over type-1 + CRC bits on the fly
+        const int L = P.n1 + 16;
+        uint32_t c = CRC_TAB.init[L];
+        int s2 = 0;
+        uint8_t *op = type1 + ((size_t)jb.ch * ETSI_MAXJ + jb.slot) * 268;
+        for (int t0 = P.n2 - 1; t0 >= 0; t0 -= 8) {   // n2 is a multiple of 8
+            uint32_t w[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) w[u] = sv[(size_t)(t0 - u) * ss];   // independent of the state
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int t = t0 - u;
+                const int bit = s2 & 1;
+                if (t < P.n1) op[t] = (uint8_t)bit;
+                if (bit && t < L) c ^= CRC_TAB.t[L - 1 - t];
+                s2 = (s2 >> 1) | ((int)((w[u] >> s2) & 1u) << 3);
             }
         }
-        __syncthreads();
-        // --- ACS: lane (g, st) holds the metric of state st
-        int32_t pm = st == 0 ? 0 : -(1 << 28);
-        const int n2max = 288;
-        const int b = st & 1, d0 = (st >> 1) & 1, d1 = (st >> 2) & 1, d2 = (st >> 3) & 1;
-        for (int t = 0; t < n2max; ++t) {
-            const bool live = act && t < P.n2;
-            int32_t v0 = 0, v1 = 0;
-            if (live) {
-                const int8_t *m = ms[g] + 4 * t;
-                const int32_t m0 = m[0], m1 = m[1], m2 = m[2], m3 = m[3];
-                // d3 = 0
-                v0 = ((b ^ d0) ? -m0 : m0) + ((b ^ d1 ^ d2) ? -m1 : m1) + ((b ^ d0 ^ d1) ? -m2 : m2) +
-                     ((b ^ d0 ^ d2) ? -m3 : m3);
-                // d3 = 1 flips every generator output
-                v1 = -v0;
-            }
-            const int p0 = (st >> 1), p1 = (st >> 1) | 8;
-            const int32_t a0 = __shfl(pm, (lane & ~15) + p0, 64) + v0;
-            const int32_t a1 = __shfl(pm, (lane & ~15) + p1, 64) + v1;
-            const bool take1 = a1 > a0;
-            const unsigned long long sv = __ballot(take1);
-            if (live) pm = take1 ? a1 : a0;
-            if (lane == 0) surv[t] = sv;
-            if (__all(!live)) break;
-        }
-        __syncthreads();
-        // --- traceback (lane 0 of each group) and CRC
-        if (act && st == 0) {
-            int s2 = 0;
-            for (int t = P.n2 - 1; t >= 0; --t) {
-                t2[g][t] = (uint8_t)(s2 & 1);
-                const int d3 = (int)((surv[t] >> (16 * g + s2)) & 1ull);
-                s2 = (s2 >> 1) | (d3 << 3);
-            }
-            uint32_t c = 0xFFFF;
-            for (int i = 0; i < P.n1 + 16; ++i) {
-                c ^= (uint32_t)t2[g][i] << 15;
-                c = (c & 0x8000u) ? ((c << 1) ^ 0x1021u) : (c << 1);
-                c &= 0xFFFFu;
-            }
-            int32_t *bm = blocks + ((size_t)ch * ETSI_MAXJ + j) * 4;
-            bm[0] = jk[j];
-            bm[1] = c == 0x1D0Fu;
-            bm[2] = jb[j];
-            bm[3] = jblk[j];
-        }
-        __syncthreads();
-        if (act) {
-            uint8_t *op = type1 + ((size_t)ch * ETSI_MAXJ + j) * 268;
-            for (int i = st; i < P.n1; i += 16) op[i] = t2[g][i];
-        }
-        __syncthreads();
+        int32_t *bm = blocks + ((size_t)jb.ch * ETSI_MAXJ + jb.slot) * 4;
+        bm[0] = jb.kind;
+        bm[1] = c == 0x1D0Fu;
+        bm[2] = jb.burst;
+        bm[3] = jb.blk;
     }
 }
 
@@ -470,7 +524,7 @@ __global__ __launch_bounds__(64) void k_lmac_etsi(const int8_t *__restrict__ sof
 __global__ __launch_bounds__(64) void k_decode_blocks(const int8_t *__restrict__ soft5, int F, int kind,
                                                       const uint8_t *__restrict__ scr /*[F][K]*/,
                                                       uint8_t *__restrict__ type1, uint8_t *__restrict__ crc_ok) {
-    __shared__ int8_t ms[4][4 * 288];
+    __shared__ __attribute__((aligned(16))) int8_t ms[4][4 * 288];
     __shared__ uint64_t surv[288];
     __shared__ uint8_t t2[4][288];
     const int lane = threadIdx.x, g = lane >> 4, st = lane & 15;
@@ -676,29 +730,6 @@ int tetra_demod_etsi(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *iq, s
     return st.finish();
 }
 
-int tetra_lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard, const int32_t *nsym, size_t C,
-                    size_t smax, int32_t *nburst, int32_t *bursts, int32_t *nblock, int32_t *blocks, uint8_t *type1) {
-    if (!ctx || C == 0) return TETRA_E_INVALID;
-    if (ctx->cells < C) return tetra_fail(ctx, TETRA_E_INVALID, "tetra_etsi_set_cells() for %zu channels first", C);
-    if (2 * smax > LMAC_MAXBITS + 4) return tetra_fail(ctx, TETRA_E_INVALID, "chunk too long for tetra_lmac_etsi");
-    Staging st(ctx);
-    const int8_t *sb = (const int8_t *)st.in(softbits, C * smax * 2);
-    const uint8_t *hd = (const uint8_t *)st.in(hard, C * smax);
-    const int32_t *ns = (const int32_t *)st.in(nsym, C * 4);
-    int32_t *nbo = (int32_t *)st.out(nburst, C * 4);
-    int32_t *bo = (int32_t *)st.out(bursts, C * ETSI_MAXB * 2 * 4);
-    int32_t *nko = (int32_t *)st.out(nblock, C * 4);
-    int32_t *ko = (int32_t *)st.out(blocks, C * ETSI_MAXJ * 4 * 4);
-    uint8_t *to = (uint8_t *)st.out(type1, C * ETSI_MAXJ * 268);
-    if (!sb || !hd || !ns || !nbo || !bo || !nko || !ko || !to) return st.finish();
-    const uint8_t *cells = (const uint8_t *)ctx->slot[S_W5].p;
-    {
-        PROF(ctx, "etsi_lmac");
-        hipLaunchKernelGGL(k_lmac_etsi, dim3((unsigned)C), dim3(64), 0, ctx->stream, sb, hd, ns, (int)smax, cells,
-                           cells + ctx->cells * 432, nbo, bo, nko, ko, to);
-    }
-    return st.finish();
-}
 
 int tetra_etsi_decode_blocks(tetra_ctx *ctx, const int8_t *soft5, size_t F, int kind, const uint32_t *scramb_init,
                              uint8_t *type1, uint8_t *crc_ok) {
@@ -739,6 +770,42 @@ int tetra_etsi_encode_blocks(tetra_ctx *ctx, const uint8_t *type1, size_t F, int
     if (!t || !scr || !o) return st.finish();
     hipLaunchKernelGGL(k_encode_blocks, dim3((unsigned)((F + 63) / 64)), dim3(64), 0, ctx->stream, t, (int)F, kind, scr,
                        o);
+    return st.finish();
+}
+
+int tetra_lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard, const int32_t *nsym, size_t C,
+                    size_t smax, int32_t *nburst, int32_t *bursts, int32_t *nblock, int32_t *blocks, uint8_t *type1) {
+    if (!ctx || C == 0) return TETRA_E_INVALID;
+    if (ctx->cells < C) return tetra_fail(ctx, TETRA_E_INVALID, "tetra_etsi_set_cells() for %zu channels first", C);
+    if (2 * smax > LMAC_MAXBITS + 4) return tetra_fail(ctx, TETRA_E_INVALID, "chunk too long for tetra_lmac_etsi");
+    Staging st(ctx);
+    const int8_t *sb = (const int8_t *)st.in(softbits, C * smax * 2);
+    const uint8_t *hd = (const uint8_t *)st.in(hard, C * smax);
+    const int32_t *ns = (const int32_t *)st.in(nsym, C * 4);
+    int32_t *nbo = (int32_t *)st.out(nburst, C * 4);
+    int32_t *bo = (int32_t *)st.out(bursts, C * ETSI_MAXB * 2 * 4);
+    int32_t *nko = (int32_t *)st.out(nblock, C * 4);
+    int32_t *ko = (int32_t *)st.out(blocks, C * ETSI_MAXJ * 4 * 4);
+    uint8_t *to = (uint8_t *)st.out(type1, C * ETSI_MAXJ * 268);
+    const size_t jmax = C * ETSI_MAXJ;
+    // workspace: [job counter (16 B)] [jobs] [survivors: 288 steps x jmax]
+    char *w = (char *)ws(ctx, S_W7, 16 + jmax * sizeof(Job) + 288 * jmax * 2);
+    if (!sb || !hd || !ns || !nbo || !bo || !nko || !ko || !to || !w) return st.finish();
+    int32_t *jcount = (int32_t *)w;
+    Job *jobs = (Job *)(w + 16);
+    uint16_t *surv = (uint16_t *)(w + 16 + jmax * sizeof(Job));
+    const uint8_t *cells = (const uint8_t *)ctx->slot[S_W5].p;
+    {
+        PROF(ctx, "etsi_sync");
+        HIP_TRY(ctx, hipMemsetAsync(jcount, 0, 16, ctx->stream));
+        hipLaunchKernelGGL(k_etsi_sync, dim3((unsigned)C), dim3(64), 0, ctx->stream, hd, ns, (int)smax, nbo, bo, nko,
+                           jcount, jobs);
+    }
+    {
+        PROF(ctx, "etsi_viterbi");
+        hipLaunchKernelGGL(k_etsi_viterbi, dim3((unsigned)((jmax + 63) / 64)), dim3(64), 0, ctx->stream, jobs, jcount,
+                           (int)jmax, sb, (int)smax, cells, cells + ctx->cells * 432, surv, ko, to);
+    }
     return st.finish();
 }
 
