@@ -29,6 +29,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from tetraear import _hip  # noqa: E402
+from tetraear.shard import aggregate_msps, max_over_ranks, rank_seed  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 FS = 2.4e6
@@ -155,10 +156,10 @@ def main():
     C, N = a.channels, a.samples
     if a.chain == "etsi":
         from tetraear.signal.etsi import BenchStep as EtsiStep
-        step = EtsiStep(c, C, N, FS, seed=1000 + rank, device=dev)
+        step = EtsiStep(c, C, N, FS, seed=rank_seed(1000, rank), device=dev)
     else:
         g = torch.Generator(device=dev)
-        g.manual_seed(1000 + rank)
+        g.manual_seed(rank_seed(1000, rank))
         iq = (0.25 * torch.randn((C, N, 2), generator=g, device=dev, dtype=torch.float32))
         iq = torch.round(iq * 32768) / 32768   # SC16 grid, like capture.py:259-269
         step = CompatStep(c, iq, C, N)
@@ -181,13 +182,9 @@ def main():
     elapsed = time.perf_counter() - t0
     prof = read_profile(c)
     c.check(c.lib.tetra_profile(c.handle, 0), "profile")
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, dev)   # slowest rank (RCCL all_reduce MAX); identity at N=1
     ms_step = elapsed / a.steps * 1e3
-    total_samples = C * N * world * a.steps
-    value = total_samples / elapsed / 1e6
+    value = aggregate_msps(C * N, world, a.steps, elapsed)
 
     if rank == 0:
         name, per_sample, ksym = step.dominant()
