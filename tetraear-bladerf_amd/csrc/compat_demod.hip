@@ -70,7 +70,16 @@ __global__ __launch_bounds__(256) void k_sos_fwd(const T *__restrict__ x, Lay lx
     const size_t ss = ls.s_n;
     long j = 0;
     for (; j < pad; ++j) sp[(size_t)j * ss] = sos_step(c, z, two * x0 - xp[(size_t)(pad - j) * sx]);
-    for (long n = 0; n < N; ++n, ++j) sp[(size_t)j * ss] = sos_step(c, z, xp[(size_t)n * sx]);
+    // body: 16 input loads issued ahead of the dependent recursion (latency, not bandwidth, bound)
+    long n = 0;
+    for (; n + 16 <= N; n += 16, j += 16) {
+        T xs[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) xs[u] = xp[(size_t)(n + u) * sx];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) sp[(size_t)(j + u) * ss] = sos_step(c, z, xs[u]);
+    }
+    for (; n < N; ++n, ++j) sp[(size_t)j * ss] = sos_step(c, z, xp[(size_t)n * sx]);
     for (long k = 0; k < pad; ++k, ++j) sp[(size_t)j * ss] = sos_step(c, z, two * xl - xp[(size_t)(N - 2 - k) * sx]);
 }
 
@@ -97,6 +106,20 @@ __global__ __launch_bounds__(256) void k_sos_bwd(const T *__restrict__ scr, Lay 
     // output y[t] for t = j - pad with t % q == 0 (decimate's y[::q])
     long t = N - 1;
     int cnt = (int)(t % q);
+    for (; t >= 15; t -= 16, j -= 16) {   // 16 scratch loads ahead of the recursion
+        T ys[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) ys[u] = sp[(size_t)(j - u) * ss];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const T v = sos_step(c, z, ys[u]);
+            if (cnt == 0) {
+                op[(size_t)((t - u) / q) * so] = v;
+                cnt = q;
+            }
+            --cnt;
+        }
+    }
     for (; t >= 0; --t, --j) {
         T v = sos_step(c, z, sp[(size_t)j * ss]);
         if (cnt == 0) {
@@ -168,8 +191,7 @@ __global__ __launch_bounds__(256) void k_lf_fwd(const TIn *__restrict__ x, Lay l
     for (int k = 0; k < nt - 1; ++k) z[k] = zi[k] * e0;
     double *sp = scr + ls.off(ch, 0) + comp;
     const size_t ss = ls.s_n;
-    for (long j = 0; j < L; ++j) {
-        const double xn = lf_ext(xp, sx, M, pad, j, comp, mix, c, fs);
+    auto step = [&](long j, double xn) {
         // scipy lfilter (DF-II-T): y = z0 + b0*x; z_k = (z_{k+1} + x*b_{k+1}) - y*a_{k+1}
         const double yn = z[0] + bb[0] * xn;
 #pragma unroll
@@ -180,7 +202,17 @@ __global__ __launch_bounds__(256) void k_lf_fwd(const TIn *__restrict__ x, Lay l
         for (int k = 0; k < MAXTAP - 1; ++k)
             if (k == nt - 2) z[k] = xn * bb[k + 1] - yn * aa[k + 1];
         sp[(size_t)j * ss] = yn;
+    };
+    long j = 0;
+    for (; j < pad; ++j) step(j, lf_ext(xp, sx, M, pad, j, comp, mix, c, fs));
+    for (; j + 16 <= pad + M; j += 16) {   // inputs (and mixer phases) computed ahead of the recursion
+        double xs[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) xs[u] = mixed_val(xp, sx, j + u - pad, comp, mix, c, fs);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) step(j + u, xs[u]);
     }
+    for (; j < L; ++j) step(j, lf_ext(xp, sx, M, pad, j, comp, mix, c, fs));
 }
 
 __global__ __launch_bounds__(256) void k_lf_bwd(const double *__restrict__ scr, Lay ls, int C, long M, int pad, int nt,
@@ -198,8 +230,7 @@ __global__ __launch_bounds__(256) void k_lf_bwd(const double *__restrict__ scr, 
     for (int k = 0; k < nt - 1; ++k) z[k] = zi[k] * y0;
     double *op = out + lo.off(ch, 0) + comp;
     const size_t so = lo.s_n;
-    for (long j = L - 1; j >= 0; --j) {
-        const double xn = sp[(size_t)j * ss];
+    auto step = [&](long j, double xn) {
         const double yn = z[0] + bb[0] * xn;
 #pragma unroll
         for (int k = 0; k < MAXTAP - 2; ++k)
@@ -209,7 +240,16 @@ __global__ __launch_bounds__(256) void k_lf_bwd(const double *__restrict__ scr, 
             if (k == nt - 2) z[k] = xn * bb[k + 1] - yn * aa[k + 1];
         const long t = j - pad;
         if (t >= 0 && t < M) op[(size_t)t * so] = yn;
+    };
+    long j = L - 1;
+    for (; j >= 15; j -= 16) {   // 16 scratch loads ahead of the recursion
+        double xs[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) xs[u] = sp[(size_t)(j - u) * ss];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) step(j - u, xs[u]);
     }
+    for (; j >= 0; --j) step(j, sp[(size_t)j * ss]);
 }
 
 // frequency_shift alone (component API, and the unfiltered-but-shifted process() path).
