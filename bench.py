@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--samples", type=int, default=131072, help="samples per channel chunk")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (rank 0)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="etsi: run the whole chain on one stream (no front/back-end overlap across batches)")
     return ap.parse_args()
 
 
@@ -66,6 +68,13 @@ def traffic_from_profiles(kernel, workload_key):
 
 
 def read_profile(c):
+    if isinstance(c, (list, tuple)):
+        out = {}
+        for x in c:
+            for k, (ms, n) in read_profile(x).items():
+                m0, n0 = out.get(k, (0.0, 0))
+                out[k] = (m0 + ms, n0 + n)
+        return out
     names = ctypes.create_string_buffer(4096)
     ms = (ctypes.c_double * 64)()
     cnt = (ctypes.c_int64 * 64)()
@@ -157,6 +166,8 @@ def main():
     if a.chain == "etsi":
         from tetraear.signal.etsi import BenchStep as EtsiStep
         step = EtsiStep(c, C, N, FS, seed=rank_seed(1000, rank), device=dev)
+        if not a.no_pipeline:
+            step.pipeline()
     else:
         g = torch.Generator(device=dev)
         g.manual_seed(rank_seed(1000, rank))
@@ -164,12 +175,14 @@ def main():
         iq = torch.round(iq * 32768) / 32768   # SC16 grid, like capture.py:259-269
         step = CompatStep(c, iq, C, N)
     torch.cuda.synchronize(dev)
+    ctxs = step.contexts() if hasattr(step, "contexts") else [c]
 
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
-    c.check(c.lib.tetra_profile(c.handle, 1), "profile")
-    read_profile(c)   # drop warm-up records
+    for x in ctxs:
+        x.check(x.lib.tetra_profile(x.handle, 1), "profile")
+    read_profile(ctxs)   # drop warm-up records
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -180,8 +193,9 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    prof = read_profile(c)
-    c.check(c.lib.tetra_profile(c.handle, 0), "profile")
+    prof = read_profile(ctxs)
+    for x in ctxs:
+        x.check(x.lib.tetra_profile(x.handle, 0), "profile")
     elapsed = max_over_ranks(elapsed, dev)   # slowest rank (RCCL all_reduce MAX); identity at N=1
     ms_step = elapsed / a.steps * 1e3
     value = aggregate_msps(C * N, world, a.steps, elapsed)
@@ -210,6 +224,7 @@ def main():
                 "workload": f"C5 shard: {C} channels x {N} cf32 samples @2.4 MSps per GPU, chain={a.chain}",
                 "channels_per_gpu": C, "samples_per_channel": N, "sample_rate": FS,
                 "parallelism": f"channel-sharded x{world}",
+                "pipeline": bool(getattr(step, "pipelined", False)),
             },
             "realtime_channels": int(value * 1e6 / FS),
             "roofline": {

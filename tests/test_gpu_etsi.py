@@ -142,3 +142,27 @@ def test_full_size_round_trip():
                     assert tuple(np.pad(b["bits"], (0, 268 - len(b["bits"])))) in sent
     assert nblk >= 3 * C
     assert nok / nblk > 0.97, (nok, nblk)
+
+
+def test_bench_pipeline_matches_serial():
+    """bench.py's two-stream pipeline (front: chanfilt, back: timing + lower MAC, double-buffered
+    72 kHz intermediate) gives the same per-step results as the single-stream chain."""
+    import torch
+    from tetraear import _hip
+    from tetraear.signal.etsi import BenchStep
+    dev = torch.device("cuda", 0)
+    c = _hip.ctx()
+    c.check(c.lib.tetra_set_stream(c.handle, None), "set_stream")
+    outs = []
+    for pipe in (False, True):
+        st = BenchStep(c, 64, 131072, 2.4e6, seed=11, device=dev)
+        if pipe:
+            st.pipeline()
+        for _ in range(3):
+            st()
+        torch.cuda.synchronize(dev)
+        outs.append([t.cpu().clone() for t in (st.soft, st.hard, st.nsym, st.nburst, st.bursts, st.nblock,
+                                               st.blocks, st.type1)])
+        assert st.quality()["crc_ok"] > 64
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

@@ -4,18 +4,22 @@
 // north_star asks for, restating oracle/etsi_oracle.c operation for operation (explicit fmaf,
 // emulated 64-lane reductions, a libm-free atan2), so GPU and oracle results are bit-identical.
 //
-//   k_chanfilt   stage 1: 48-tap decimate-by-q1 FIR (2.4 MSps -> 240 kHz), stage 2: polyphase RRC
-//                (alpha 0.35) resampler x3/10 -> 72 kHz = 4 samples/symbol.  One workgroup streams
-//                one channel: 2560-sample input tiles (float4 loads, register prefetch one tile
-//                ahead), stage-1 outputs in an LDS ring, stage-2 outputs stored coalesced.
-//                HBM-bound: ~8 B read per input sample, 0.24 B written.
+//   k_chanfilt   stage 1: 48-tap decimate-by-10 FIR (2.4 MSps -> 240 kHz), stage 2: polyphase RRC
+//                (alpha 0.35, 321 taps at 720 kHz) resampler x3/10 -> 72 kHz = 4 samples/symbol.
+//                One workgroup streams one channel: 2560-sample input tiles (float4 loads, register
+//                prefetch two tiles deep), stage-1 outputs in a polyphase LDS ring, stage 2 every 8
+//                tiles as output triples (one per thread, wave-uniform taps from the scalar cache,
+//                packed fp32 FMA), outputs held in LDS and stored in one burst per channel.
+//                HBM-bound: 8 B read per input sample, 0.24 B written.
 //   k_timing     one wave per channel: Oerder-Meyr timing phase (wave reduction), block Gardner
 //                tracking (64 symbols per block = one per lane; error summed by xor-butterfly),
 //                cubic interpolation, differential decision, 4th-power CFO estimate, int8 soft bits.
-//   k_lmac_etsi  one wave per channel: burst sync on packed hard bits (head/training/tail
-//                correlation by XOR+popcount, ballot greedy scan), then per block: descramble,
-//                deinterleave, depuncture (rate 2/3), 16-state Viterbi (one lane per state, 4 blocks
-//                per wave, survivors as 64-bit ballots in LDS), traceback, CRC-16.
+//   k_etsi_sync  one wave per channel: hard bits packed by ballots, head/training/tail correlation
+//                by XOR+popcount, greedy burst scan, one decode job per coded block (dense atomic
+//                allocation).
+//   k_etsi_viterbi  one lane per job: descramble + deinterleave + depuncture gathers from an LDS
+//                row, 16-state rate-1/4 Viterbi with metrics in registers, survivors coalesced in
+//                global scratch, traceback with the CRC-16 folded in.
 #include "common.h"
 
 namespace {
@@ -25,7 +29,6 @@ constexpr int ETSI_MAXJ = 16;   // coded blocks per channel chunk (2 per burst)
 constexpr int TILE_K = 256;     // stage-1 outputs per tile (one per thread)
 constexpr int TILE_IN = TILE_K * 10;   // new input samples per tile (q1 = 10)
 constexpr int HALO = 48;
-constexpr int RING = 1024;      // stage-1 ring (power of two)
 
 struct KindP { int K, a, n2, n1; };
 __host__ __device__ inline KindP kind_params(int kind) {
@@ -33,87 +36,139 @@ __host__ __device__ inline KindP kind_params(int kind) {
 }
 
 // --------------------------------------------------------------------------- E1 channel filter
-// plan arrays in constant-ish global memory (read through the scalar cache)
+// The input tile is a linear float4 image (2 samples per entry, ds_write_b128 / ds_read_b128: a
+// 20-dword lane stride is conflict-free for b128's lane groups).  The stage-1 ring is polyphase:
+// x240[k] sits at [k % 10][k / 10], so stage 2's stride-10 reads are unit-stride across lanes.
+constexpr int RP = 224;         // row length of the stage-1 ring (10 x 224 = 2240 outputs kept)
+constexpr int S2_EVERY = 8;     // stage 2 runs every 8 tiles: ~205 output triples, one per thread
+constexpr int TPP = 107;        // RRC taps per polyphase branch (Lp = 321 = 3 x 107)
+constexpr int PFD = 2;          // input tiles in flight per workgroup (register prefetch depth;
+                                // 3 measured no faster)
+constexpr int YLDS = 4096;        // stage-2 outputs held in LDS before a flush (a 131072-sample chunk
+                                // has 3932)
+constexpr int HQ = 120;         // row of the per-branch tap table, indexed by r = j + off_c
+
+// Packed fp32 (v_pk_fma_f32): one real tap times a complex sample, each half a correctly rounded
+// fma -- the same per-component arithmetic as two fmaf calls.
+typedef float pf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pf2 pfma(float h, pf2 x, pf2 acc) { return __builtin_elementwise_fma(pf2{h, h}, x, acc); }
+__device__ __forceinline__ int rslot(int k) { return (k % 10) * RP + (k / 10) % RP; }
+
+// h1[48] stage-1 taps; hq[3][HQ]: branch c of stage 2, output m = 3u + c = sum_j hp[i0(c) - 3j] *
+// x240[10u + off_c + j] with i0 = {320, 318, 319}, off_c = {0, 4, 7}, stored at r = off_c + j
+// (zeros elsewhere).  Both tables are read with wave-uniform addresses (scalar loads).
 __global__ __launch_bounds__(256) void k_chanfilt(const float4 *__restrict__ iq, long N, int M1, int M2,
-                                                  const float *__restrict__ h1, const float *__restrict__ hp,
-                                                  int Lp, float2 *__restrict__ y) {
-    __shared__ float2 xin[TILE_IN + HALO];
-    __shared__ float2 ring[RING];
-    __shared__ float hps[384];
+                                                  const float *__restrict__ h1, const float *__restrict__ hq,
+                                                  float2 *__restrict__ y) {
+    __shared__ float4 xin[(HALO + TILE_IN) / 2];
+    __shared__ float2 ring[10 * RP];
+    // Stage-2 outputs collect in LDS and go out in one coalesced burst when the channel is done
+    // (or when YLDS fills): stores interleaved with the input stream cost ~0.3 ms per 8192-channel
+    // batch (HBM read/write turnarounds, and store acks inside the prefetch's in-order vmcnt).
+    __shared__ pf2 yb[YLDS];
     const int ch = blockIdx.x;
     const int tid = threadIdx.x;
-    for (int i = tid; i < Lp; i += 256) hps[i] = hp[i];
     const float4 *xp = iq + (size_t)ch * (N / 2);   // N even: 2 complex samples per float4
     float2 *yp = y + (size_t)ch * M2;
-    float hr[48];
-#pragma unroll
-    for (int j = 0; j < 48; ++j) hr[j] = h1[j];
-    // register prefetch of tile 0: samples [0, 2560) land at xin[48 + i]
-    float4 pf[5];
-    auto load_tile = [&](int t) {
+    int ybase = 0;   // y index of yb[0]
+    auto flush = [&](int mend) {
+        for (int i = tid; i < mend - ybase; i += 256) yp[ybase + i] = make_float2(yb[i].x, yb[i].y);
+        ybase = mend;
+    };
+    for (int i = tid; i < 10 * RP; i += 256) ring[i] = make_float2(0.f, 0.f);   // finite x 0-tap
+    // register prefetch PFD tiles deep (40 KiB in flight per workgroup): tile t's samples
+    // [2560 t, 2560 t + 2560) land at image sample HALO + i
+    // Loads are unconditional (index clamped) so the wait before a tile's LDS write can leave the
+    // next tile's loads in flight.  Clamped samples past the end only feed stage-1 outputs k >= M1,
+    // which are never computed (10 (M1-1) + 47 <= N-1).
+    const long nq = N / 2;
+    auto load_tile = [&](float4 (&pf)[5], int t) __attribute__((always_inline)) {
 #pragma unroll
         for (int r = 0; r < 5; ++r) {
             const long q = (long)t * (TILE_IN / 2) + r * 256 + tid;   // float4 index
-            pf[r] = (2 * q + 1 < N) ? xp[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+            pf[r] = xp[min(q, nq - 1)];
         }
     };
-    load_tile(0);
-    int m_done = 0;
-    for (int t = 0;; ++t) {
+    int u_done = 0;   // stage-2 output triples [0, u_done) are stored
+    auto tile = [&](int t, float4 (&pf)[5]) __attribute__((always_inline)) {
         const int kfirst = TILE_K * t - 4;   // stage-1 output of thread 0 in this tile
-        if (kfirst >= M1) break;
 #pragma unroll
-        for (int r = 0; r < 5; ++r) {
-            const int i = 2 * (r * 256 + tid);
-            xin[HALO + i] = make_float2(pf[r].x, pf[r].y);
-            xin[HALO + i + 1] = make_float2(pf[r].z, pf[r].w);
-        }
-        load_tile(t + 1);   // next tile in flight during compute
+        for (int r = 0; r < 5; ++r) xin[HALO / 2 + r * 256 + tid] = make_float4(pf[r].x, pf[r].y, pf[r].z, pf[r].w);
+        // keep the re-load after the LDS writes so pf's registers are reused in place (otherwise
+        // the scheduler hoists it and the loop latch copies registers under a full vmcnt(0))
+        __builtin_amdgcn_sched_barrier(0);
+        load_tile(pf, t + PFD);   // tile t+PFD in flight during compute (t+1.. already are)
         __syncthreads();
-        // stage 1: x240[k] = sum_j h1[j] * x[10k + j], k = kfirst + tid
+        // stage 1: x240[k] = sum_j h1[j] * x[10k + j], k = kfirst + tid; x[10k + j] is sample
+        // 10 tid + 8 + j of the image
         const int k = kfirst + tid;
         if (k >= 0 && k < M1) {
-            const float2 *w = xin + 10 * tid + 8;
-            float ar = 0.f, ai = 0.f;
+            const float4 *w = xin + 5 * tid + 4;
+            pf2 a = {0.f, 0.f};
 #pragma unroll
-            for (int j = 0; j < 48; ++j) {
-                const float2 v = w[j];
-                ar = fmaf(hr[j], v.x, ar);
-                ai = fmaf(hr[j], v.y, ai);
+            for (int jj = 0; jj < 24; ++jj) {
+                const float4 v = w[jj];
+                a = pfma(h1[2 * jj], pf2{v.x, v.y}, a);
+                a = pfma(h1[2 * jj + 1], pf2{v.z, v.w}, a);
             }
-            ring[k & (RING - 1)] = make_float2(ar, ai);
+            ring[rslot(k)] = make_float2(a.x, a.y);
         }
         __syncthreads();
-        // halo for the next tile: its xin[0..48) = this tile's xin[2560..2608)
-        if (tid < HALO) xin[tid] = xin[TILE_IN + tid];
-        // stage 2 (every third tile, so ~230 of 256 threads have an output): outputs m whose
-        // taps end at or before the last stage-1 output available
-        const int kav = min(kfirst + TILE_K - 1, M1 - 1);
-        if (t % 3 == 2 || kav == M1 - 1) {
-            const int num = 3 * kav + 2 - (Lp - 1);   // largest m with floor((Lp-1+10m)/3) <= kav
-            int m_hi = num >= 0 ? num / 10 : -1;
-            if (m_hi > M2 - 1) m_hi = M2 - 1;
-            for (int m0 = m_done; m0 <= m_hi; m0 += 256) {
-                const int m = m0 + tid;
-                if (m <= m_hi) {
-                    const int n = (Lp - 1) + 10 * m;
-                    const int kmin = (10 * m + 2) / 3, kmax = n / 3;
-                    float ar = 0.f, ai = 0.f;
-                    int i = n - 3 * kmin;   // tap index, decreasing by 3 as k ascends
-#pragma unroll 8
-                    for (int kk = kmin; kk <= kmax; ++kk, i -= 3) {
-                        const float h = hps[i];
-                        const float2 v = ring[kk & (RING - 1)];
-                        ar = fmaf(h, v.x, ar);
-                        ai = fmaf(h, v.y, ai);
+        // halo for the next tile: image samples [0, 48) = this tile's [2560, 2608)
+        if (tid < HALO / 2) xin[tid] = xin[TILE_IN / 2 + tid];
+        const int kav = min(kfirst + TILE_K - 1, M1 - 1);   // last stage-1 output available
+        const bool last = kav == M1 - 1;
+        if (t % S2_EVERY == S2_EVERY - 1 || last) {
+            // stage 2: triples u whose three outputs have all taps available (all of them at the end)
+            const int num = 3 * kav + 2 - 320;   // largest m with floor((320 + 10m)/3) <= kav
+            const int m_hi = num >= 0 ? min(num / 10, M2 - 1) : -1;
+            const int u_hi = last ? (M2 - 1) / 3 : (m_hi >= 2 ? (m_hi - 2) / 3 : -1);
+            for (int u0 = u_done; u0 <= u_hi; u0 += 256) {
+                if (min(3 * min(u0 + 256, u_hi + 1), M2) - ybase > YLDS) {   // chunk would not fit
+                    flush(3 * u0);
+                    __syncthreads();
+                }
+                const int u = u0 + tid;
+                if (u <= u_hi) {
+                    // r-major over the 114 stage-1 inputs of the triple; each branch's zero-padded
+                    // taps leave its accumulation order exactly that of the oracle (kk ascending)
+                    pf2 a0 = {0.f, 0.f}, a1 = {0.f, 0.f}, a2 = {0.f, 0.f};
+                    auto tap = [&](int r, float2 v) {
+                        const pf2 x = {v.x, v.y};
+                        a0 = pfma(hq[r], x, a0);
+                        a1 = pfma(hq[HQ + r], x, a1);
+                        a2 = pfma(hq[2 * HQ + r], x, a2);
+                    };
+#pragma unroll 1
+                    for (int q = 0; q < 11; ++q) {
+                        const int row = (u + q) % RP;
+#pragma unroll
+                        for (int p = 0; p < 10; ++p) tap(10 * q + p, ring[p * RP + row]);
                     }
-                    yp[m] = make_float2(ar, ai);
+                    const int row = (u + 11) % RP;
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) tap(110 + p, ring[p * RP + row]);
+                    const int m = 3 * u;
+                    if (m < M2) yb[m - ybase] = a0;
+                    if (m + 1 < M2) yb[m + 1 - ybase] = a1;
+                    if (m + 2 < M2) yb[m + 2 - ybase] = a2;
                 }
             }
-            if (m_hi + 1 > m_done) m_done = m_hi + 1;
+            if (u_hi + 1 > u_done) u_done = u_hi + 1;
         }
         __syncthreads();
+    };
+    const int ntile = (M1 + 4 + TILE_K - 1) / TILE_K;   // tiles with kfirst < M1
+    float4 pa[5], pb[5];
+    load_tile(pa, 0);
+    load_tile(pb, 1);
+    int t = 0;
+    for (; t + 1 < ntile; t += 2) {
+        tile(t, pa);
+        tile(t + 1, pb);
     }
+    if (t < ntile) tile(t, pa);
+    flush(M2);   // the last tile ended with a barrier
 }
 
 // --------------------------------------------------------------------------- E2 timing
@@ -620,8 +675,29 @@ static void scramble_seq(uint32_t r, int n, uint8_t *out) {
 
 static int etsi_check(tetra_ctx *ctx, const tetra_etsi_plan *P) {
     if (!P) return tetra_fail(ctx, TETRA_E_INVALID, "plan is NULL");
-    if (P->q1 != 10 || P->L1 != 48 || P->up != 3 || P->down != 10 || P->Lp < 16 || P->Lp > 384)
-        return tetra_fail(ctx, TETRA_E_INVALID, "unsupported ETSI plan (q1=10, L1=48, 3/10, Lp<=384 required)");
+    if (P->q1 != 10 || P->L1 != 48 || P->up != 3 || P->down != 10 || P->Lp != 3 * TPP)
+        return tetra_fail(ctx, TETRA_E_INVALID, "unsupported ETSI plan (q1=10, L1=48, 3/10, Lp=321 required)");
+    return TETRA_OK;
+}
+
+// Stage-1 taps and the per-branch stage-2 tap table (k_chanfilt), then the launch.
+static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *x, size_t C, size_t N, int64_t M1,
+                           int64_t M2, float2 *y) {
+    float *coef = (float *)ws(ctx, S_W6, (64 + 3 * HQ) * 4);
+    if (!coef) return TETRA_E_NOMEM;
+    float *hc = ctx->coef_etsi;
+    static const int i0[3] = {320, 318, 319}, off[3] = {0, 4, 7};
+    for (int j = 0; j < 64; ++j) hc[j] = j < 48 ? P->h1[j] : 0.f;
+    for (int c = 0; c < 3; ++c)
+        for (int r = 0; r < HQ; ++r) {
+            const int j = r - off[c];
+            hc[64 + c * HQ + r] = j >= 0 && j < TPP ? P->hp[i0[c] - 3 * j] : 0.f;
+        }
+    HIP_TRY(ctx, hipMemcpyAsync(coef, hc, (64 + 3 * HQ) * 4, hipMemcpyHostToDevice, ctx->stream));
+    PROF(ctx, "etsi_chanfilt");
+    hipLaunchKernelGGL(k_chanfilt, dim3((unsigned)C), dim3(256), 0, ctx->stream, (const float4 *)x, (long)N, (int)M1,
+                       (int)M2, coef, coef + 64, y);
+    HIP_TRY(ctx, hipGetLastError());
     return TETRA_OK;
 }
 
@@ -663,15 +739,9 @@ int tetra_etsi_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *iq
     Staging st(ctx);
     const void *x = st.in(iq, C * N * 8);
     void *yo = st.out(y, C * (size_t)M2 * 8);
-    float *coef = (float *)ws(ctx, S_W6, (64 + 384) * 4);
-    if (!x || !yo || !coef) return st.finish();
-    HIP_TRY(ctx, hipMemcpyAsync(coef, P->h1, 64 * 4, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(coef + 64, P->hp, 384 * 4, hipMemcpyHostToDevice, ctx->stream));
-    {
-        PROF(ctx, "etsi_chanfilt");
-        hipLaunchKernelGGL(k_chanfilt, dim3((unsigned)C), dim3(256), 0, ctx->stream, (const float4 *)x, (long)N,
-                           (int)M1, (int)M2, coef, coef + 64, P->Lp, (float2 *)yo);
-    }
+    if (!x || !yo) return st.finish();
+    rc = launch_chanfilt(ctx, P, x, C, N, M1, M2, (float2 *)yo);
+    if (rc) return rc;
     return st.finish();
 }
 
@@ -711,17 +781,11 @@ int tetra_demod_etsi(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *iq, s
     uint8_t *ho = (uint8_t *)st.out(hard, C * smax);
     int32_t *no = (int32_t *)st.out(nsym, C * 4);
     float *dg = diag ? (float *)st.out(diag, C * 16) : nullptr;
-    float *coef = (float *)ws(ctx, S_W6, (64 + 384) * 4);
     float2 *yb = (float2 *)ws(ctx, S_W3, C * (size_t)M2 * 8);
     float2 *dscr = (float2 *)ws(ctx, S_W4, C * smax * 8);
-    if (!x || !so || !sbo || !ho || !no || !coef || !yb || !dscr) return st.finish();
-    HIP_TRY(ctx, hipMemcpyAsync(coef, P->h1, 64 * 4, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(coef + 64, P->hp, 384 * 4, hipMemcpyHostToDevice, ctx->stream));
-    {
-        PROF(ctx, "etsi_chanfilt");
-        hipLaunchKernelGGL(k_chanfilt, dim3((unsigned)C), dim3(256), 0, ctx->stream, (const float4 *)x, (long)N,
-                           (int)M1, (int)M2, coef, coef + 64, P->Lp, yb);
-    }
+    if (!x || !so || !sbo || !ho || !no || !yb || !dscr) return st.finish();
+    rc = launch_chanfilt(ctx, P, x, C, N, M1, M2, yb);
+    if (rc) return rc;
     {
         PROF(ctx, "etsi_timing");
         hipLaunchKernelGGL(k_timing, dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yb, (int)M2, P->gain,

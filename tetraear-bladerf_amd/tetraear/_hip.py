@@ -112,6 +112,13 @@ def lib():
                 if not os.path.exists(LIB_PATH):
                     raise TetraHipError(f"libtetra_hip.so not found at {LIB_PATH}: build it with "
                                         f"`make -C tetraear-bladerf_amd` (no CPU fallback exists)")
+                # One HIP runtime per process: torch bundles its own libamdhip64.so.7 (same SONAME as
+                # /opt/rocm's).  Whichever loads first serves both, and torch only initialises on
+                # its own build, so let torch load it before this library binds to it.
+                try:
+                    import torch  # noqa: F401
+                except ImportError:
+                    pass
                 _lib = _bind(ctypes.CDLL(LIB_PATH))
     return _lib
 

@@ -164,14 +164,62 @@ class BenchStep:
         self.blocks = torch.empty((C, _hip.ETSI_MAXJ, 4), dtype=torch.int32, device=device)
         self.type1 = torch.empty((C, _hip.ETSI_MAXJ, 268), dtype=torch.uint8, device=device)
 
-    def __call__(self):
-        c = self.c
-        c.check(c.lib.tetra_demod_etsi(c.handle, self.plan, _hip.ptr(self.iq), self.C, self.N, _hip.ptr(self.sym),
-                                       _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.smax, None),
-                "demod_etsi")
+        self.pipelined = False
+
+    def pipeline(self):
+        """Stream the batches through a two-stage software pipeline: the HBM-bound channel filter of
+        batch k+1 runs on a front stream while the latency-bound back end (timing, sync, Viterbi) of
+        batch k runs on a back stream.  The 72 kHz intermediate is double-buffered; each stage waits
+        only on the event that protects its buffer.  Every step still does the whole chain."""
+        import torch
+        dev = self.iq.device
+        self.back = _hip.Context()
+        self.s_front = torch.cuda.current_stream(dev)
+        self.s_back = torch.cuda.Stream(device=dev)
+        self.back.check(self.back.lib.tetra_set_stream(self.back.handle, ctypes.c_void_p(self.s_back.cuda_stream)),
+                        "set_stream")
+        self.back.check(self.back.lib.tetra_etsi_set_cells(self.back.handle, _hip.ptr(self.cells), self.C), "set_cells")
+        self.y = [torch.empty((self.C, self.M2, 2), dtype=torch.float32, device=dev) for _ in range(2)]
+        self.ev_front = [torch.cuda.Event() for _ in range(2)]
+        self.ev_back = [torch.cuda.Event() for _ in range(2)]
+        for e in self.ev_back:
+            e.record(self.s_back)
+        self.k = 0
+        self.pipelined = True
+        return self
+
+    def contexts(self):
+        return [self.c] + ([self.back] if self.pipelined else [])
+
+    def _back_end(self, c, y):
+        c.check(c.lib.tetra_etsi_timing(c.handle, self.plan, _hip.ptr(y), self.C, self.M2, _hip.ptr(self.sym),
+                                        _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.smax,
+                                        None), "etsi_timing")
         c.check(c.lib.tetra_lmac_etsi(c.handle, _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.C,
                                       self.smax, _hip.ptr(self.nburst), _hip.ptr(self.bursts), _hip.ptr(self.nblock),
                                       _hip.ptr(self.blocks), _hip.ptr(self.type1)), "lmac_etsi")
+
+    def __call__(self):
+        c = self.c
+        if not self.pipelined:
+            c.check(c.lib.tetra_demod_etsi(c.handle, self.plan, _hip.ptr(self.iq), self.C, self.N,
+                                           _hip.ptr(self.sym), _hip.ptr(self.soft), _hip.ptr(self.hard),
+                                           _hip.ptr(self.nsym), self.smax, None), "demod_etsi")
+            c.check(c.lib.tetra_lmac_etsi(c.handle, _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym),
+                                          self.C, self.smax, _hip.ptr(self.nburst), _hip.ptr(self.bursts),
+                                          _hip.ptr(self.nblock), _hip.ptr(self.blocks), _hip.ptr(self.type1)),
+                    "lmac_etsi")
+            return
+        i = self.k & 1
+        self.k += 1
+        y = self.y[i]
+        self.s_front.wait_event(self.ev_back[i])        # back end of batch k-2 has consumed y[i]
+        c.check(c.lib.tetra_etsi_chanfilt(c.handle, self.plan, _hip.ptr(self.iq), self.C, self.N, _hip.ptr(y)),
+                "etsi_chanfilt")
+        self.ev_front[i].record(self.s_front)
+        self.s_back.wait_event(self.ev_front[i])
+        self._back_end(self.back, y)
+        self.ev_back[i].record(self.s_back)
 
     def dominant(self):
         # k_chanfilt: reads 8 B per input sample, writes 8 B per 72 kHz output (3/100 per input)
