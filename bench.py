@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--samples", type=int, default=131072, help="samples per channel chunk")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (rank 0)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--iq", choices=("cf32", "sc16"), default="cf32",
+                    help="etsi: input sample format in HBM (sc16 = the BladeRF wire format, 4 B/sample)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="etsi: run the whole chain on one stream (no front/back-end overlap across batches)")
     return ap.parse_args()
@@ -165,7 +167,7 @@ def main():
     C, N = a.channels, a.samples
     if a.chain == "etsi":
         from tetraear.signal.etsi import BenchStep as EtsiStep
-        step = EtsiStep(c, C, N, FS, seed=rank_seed(1000, rank), device=dev)
+        step = EtsiStep(c, C, N, FS, seed=rank_seed(1000, rank), device=dev, iq_format=a.iq)
         if not a.no_pipeline:
             step.pipeline()
     else:
@@ -221,7 +223,8 @@ def main():
             "dtype": step.dtype if hasattr(step, "dtype") else "f32/f64",
             "data": "synthetic (device-generated, seeded per rank)",
             "config": {
-                "workload": f"C5 shard: {C} channels x {N} cf32 samples @2.4 MSps per GPU, chain={a.chain}",
+                "workload": f"C5 shard: {C} channels x {N} {a.iq if a.chain == 'etsi' else 'cf32'} samples "
+                            f"@2.4 MSps per GPU, chain={a.chain}",
                 "channels_per_gpu": C, "samples_per_channel": N, "sample_rate": FS,
                 "parallelism": f"channel-sharded x{world}",
                 "pipeline": bool(getattr(step, "pipelined", False)),
@@ -230,7 +233,7 @@ def main():
             "roofline": {
                 "bound": "hbm", "kernel": name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic_from_profiles(ksym, f"{C} channels x {N}"),
+                "traffic": traffic_from_profiles(ksym, f"{C} channels x {N} {a.iq if a.chain == 'etsi' else 'cf32'}"),
                 "launch_ms": round(launch_ms, 4), "algorithmic_bytes_per_launch": per_sample * units_per_launch,
                 "kernel_symbol": ksym,
             },

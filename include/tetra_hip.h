@@ -41,8 +41,9 @@ enum {
     TETRA_E_NOMEM = -4
 };
 
-/* Sample formats of input arrays. */
-enum { TETRA_CF32 = 0, TETRA_CF64 = 1 };
+/* Sample formats of input arrays.  TETRA_SC16: interleaved int16 (I, Q), the BladeRF wire format,
+ * scaled by 1/32768 as capture.py:241-269 does (exact in fp32); ETSI channel filter only. */
+enum { TETRA_CF32 = 0, TETRA_CF64 = 1, TETRA_SC16 = 2 };
 
 typedef struct tetra_ctx tetra_ctx;
 
@@ -207,6 +208,13 @@ int tetra_etsi_timing(tetra_ctx *ctx, const tetra_etsi_plan *plan, const void *y
 /* Fused demod (chanfilt + timing) over a batch. */
 int tetra_demod_etsi(tetra_ctx *ctx, const tetra_etsi_plan *plan, const void *iq, size_t C, size_t N,
                      void *soft, int8_t *softbits, uint8_t *hard, int32_t *nsym, size_t smax, float *diag);
+/* The same two entry points for an explicit input format (TETRA_CF32 or TETRA_SC16); the
+ * format-less forms above take cf32. */
+int tetra_etsi_chanfilt_fmt(tetra_ctx *ctx, const tetra_etsi_plan *plan, const void *iq, int iq_fmt, size_t C,
+                            size_t N, void *y);
+int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *plan, const void *iq, int iq_fmt, size_t C,
+                         size_t N, void *soft, int8_t *softbits, uint8_t *hard, int32_t *nsym, size_t smax,
+                         float *diag);
 /* Cell configuration: scrambling code init per channel ((MCC<<20|MNC<<6|CC)<<2|3). */
 int tetra_etsi_set_cells(tetra_ctx *ctx, const uint32_t *scramb_init, size_t C);
 /* Lower MAC: burst sync + descramble + deinterleave + depuncture + Viterbi + CRC per channel.

@@ -538,6 +538,7 @@ int tetra_decimate(tetra_ctx *ctx, const tetra_compat_plan *P, const void *iq, i
     int rc = check_plan(ctx, P);
     if (rc) return rc;
     if (P->q < 2 || N <= 27 || C == 0) return tetra_fail(ctx, TETRA_E_INVALID, "decimate needs q>=2 and N>27");
+    if (fmt != TETRA_CF32 && fmt != TETRA_CF64) return tetra_fail(ctx, TETRA_E_INVALID, "compat path takes cf32/cf64");
     const size_t es = fmt == TETRA_CF64 ? 8 : 4;
     const long M = ceil_div((long)N, P->q);
     Staging st(ctx);
@@ -556,6 +557,7 @@ int tetra_frequency_shift(tetra_ctx *ctx, const void *iq, int fmt, size_t C, siz
                           void *out) {
     if (!ctx || C == 0) return TETRA_E_INVALID;
     if (N == 0) return TETRA_OK;
+    if (fmt != TETRA_CF32 && fmt != TETRA_CF64) return tetra_fail(ctx, TETRA_E_INVALID, "compat path takes cf32/cf64");
     const size_t es = fmt == TETRA_CF64 ? 8 : 4;
     Staging st(ctx);
     const void *x = st.in(iq, C * N * 2 * es);
@@ -576,6 +578,7 @@ int tetra_filtfilt(tetra_ctx *ctx, const tetra_compat_plan *P, const void *iq, i
     if (!ctx) return TETRA_E_INVALID;
     if (!P || (long)N <= 3 * P->ntaps || C == 0)
         return tetra_fail(ctx, TETRA_E_INVALID, "filtfilt needs N > padlen");
+    if (fmt != TETRA_CF32 && fmt != TETRA_CF64) return tetra_fail(ctx, TETRA_E_INVALID, "compat path takes cf32/cf64");
     const size_t es = fmt == TETRA_CF64 ? 8 : 4;
     Staging st(ctx);
     const void *x = st.in(iq, C * N * 2 * es);
@@ -596,6 +599,7 @@ int tetra_extract_symbols(tetra_ctx *ctx, const void *x, int fmt, size_t C, size
                           int32_t *nsym, int32_t *bestph, size_t smax) {
     if (!ctx || C == 0 || N == 0 || sps < 1 || step < 1) return tetra_fail(ctx, TETRA_E_INVALID, "bad extract args");
     if ((sps + step - 1) / step > 16) return tetra_fail(ctx, TETRA_E_INVALID, "more than 16 phases");
+    if (fmt != TETRA_CF32 && fmt != TETRA_CF64) return tetra_fail(ctx, TETRA_E_INVALID, "compat path takes cf32/cf64");
     const size_t es = fmt == TETRA_CF64 ? 8 : 4;
     Staging st(ctx);
     const void *xd = st.in(x, C * N * 2 * es);
@@ -615,6 +619,7 @@ int tetra_extract_symbols(tetra_ctx *ctx, const void *x, int fmt, size_t C, size
 int tetra_demod_dqpsk(tetra_ctx *ctx, const void *sym, int fmt, size_t C, size_t S, const double *thr4, uint8_t *hard) {
     if (!ctx || !thr4) return TETRA_E_INVALID;
     if (S < 2 || C == 0) return TETRA_OK;
+    if (fmt != TETRA_CF32 && fmt != TETRA_CF64) return tetra_fail(ctx, TETRA_E_INVALID, "compat path takes cf32/cf64");
     const size_t es = fmt == TETRA_CF64 ? 8 : 4;
     Staging st(ctx);
     const void *sd = st.in(sym, C * S * 2 * es);
@@ -639,6 +644,7 @@ int tetra_demod_compat(tetra_ctx *ctx, const tetra_compat_plan *P, const void *i
     if (dec && (int)(fmt == TETRA_CF64) != P->dec_f64) return tetra_fail(ctx, TETRA_E_INVALID, "plan/iq precision mismatch");
     const long M = dec ? ceil_div((long)N, P->q) : (long)N;
     if ((long)smax < M / P->sps + 1 && (long)smax < M) return tetra_fail(ctx, TETRA_E_INVALID, "smax too small");
+    if (fmt != TETRA_CF32 && fmt != TETRA_CF64) return tetra_fail(ctx, TETRA_E_INVALID, "compat path takes cf32/cf64");
     const size_t es = fmt == TETRA_CF64 ? 8 : 4;
     Staging st(ctx);
     const void *x = st.in(iq, C * N * 2 * es);

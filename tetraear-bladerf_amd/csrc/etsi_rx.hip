@@ -57,7 +57,18 @@ __device__ __forceinline__ int rslot(int k) { return (k % 10) * RP + (k / 10) % 
 // h1[48] stage-1 taps; hq[3][HQ]: branch c of stage 2, output m = 3u + c = sum_j hp[i0(c) - 3j] *
 // x240[10u + off_c + j] with i0 = {320, 318, 319}, off_c = {0, 4, 7}, stored at r = off_c + j
 // (zeros elsewhere).  Both tables are read with wave-uniform addresses (scalar loads).
-__global__ __launch_bounds__(256) void k_chanfilt(const float4 *__restrict__ iq, long N, int M1, int M2,
+// Input pairs: one load = two complex samples -- float4 for cf32, uint2 (4 x int16) for SC16, the
+// BladeRF wire format (capture.py:241-269 scales by 1/32768, exact in fp32), so an SC16 capture is
+// filtered straight from its 4 B/sample form.
+__device__ __forceinline__ float4 pair_f32(float4 v) { return v; }
+__device__ __forceinline__ float4 pair_f32(uint2 v) {
+    constexpr float s = 1.0f / 32768.0f;
+    return make_float4((float)(int16_t)(v.x & 0xffffu) * s, (float)(int16_t)(v.x >> 16) * s,
+                       (float)(int16_t)(v.y & 0xffffu) * s, (float)(int16_t)(v.y >> 16) * s);
+}
+
+template <typename In>
+__global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, long N, int M1, int M2,
                                                   const float *__restrict__ h1, const float *__restrict__ hq,
                                                   float2 *__restrict__ y) {
     __shared__ float4 xin[(HALO + TILE_IN) / 2];
@@ -68,7 +79,7 @@ __global__ __launch_bounds__(256) void k_chanfilt(const float4 *__restrict__ iq,
     __shared__ pf2 yb[YLDS];
     const int ch = blockIdx.x;
     const int tid = threadIdx.x;
-    const float4 *xp = iq + (size_t)ch * (N / 2);   // N even: 2 complex samples per float4
+    const In *xp = iq + (size_t)ch * (N / 2);   // N even: 2 complex samples per load
     float2 *yp = y + (size_t)ch * M2;
     int ybase = 0;   // y index of yb[0]
     auto flush = [&](int mend) {
@@ -82,18 +93,21 @@ __global__ __launch_bounds__(256) void k_chanfilt(const float4 *__restrict__ iq,
     // next tile's loads in flight.  Clamped samples past the end only feed stage-1 outputs k >= M1,
     // which are never computed (10 (M1-1) + 47 <= N-1).
     const long nq = N / 2;
-    auto load_tile = [&](float4 (&pf)[5], int t) __attribute__((always_inline)) {
+    auto load_tile = [&](In (&pf)[5], int t) __attribute__((always_inline)) {
 #pragma unroll
         for (int r = 0; r < 5; ++r) {
-            const long q = (long)t * (TILE_IN / 2) + r * 256 + tid;   // float4 index
+            const long q = (long)t * (TILE_IN / 2) + r * 256 + tid;   // sample-pair index
             pf[r] = xp[min(q, nq - 1)];
         }
     };
     int u_done = 0;   // stage-2 output triples [0, u_done) are stored
-    auto tile = [&](int t, float4 (&pf)[5]) __attribute__((always_inline)) {
+    auto tile = [&](int t, In (&pf)[5]) __attribute__((always_inline)) {
         const int kfirst = TILE_K * t - 4;   // stage-1 output of thread 0 in this tile
 #pragma unroll
-        for (int r = 0; r < 5; ++r) xin[HALO / 2 + r * 256 + tid] = make_float4(pf[r].x, pf[r].y, pf[r].z, pf[r].w);
+        for (int r = 0; r < 5; ++r) {
+            const float4 v = pair_f32(pf[r]);
+            xin[HALO / 2 + r * 256 + tid] = make_float4(v.x, v.y, v.z, v.w);
+        }
         // keep the re-load after the LDS writes so pf's registers are reused in place (otherwise
         // the scheduler hoists it and the loop latch copies registers under a full vmcnt(0))
         __builtin_amdgcn_sched_barrier(0);
@@ -159,7 +173,7 @@ __global__ __launch_bounds__(256) void k_chanfilt(const float4 *__restrict__ iq,
         __syncthreads();
     };
     const int ntile = (M1 + 4 + TILE_K - 1) / TILE_K;   // tiles with kfirst < M1
-    float4 pa[5], pb[5];
+    In pa[5], pb[5];
     load_tile(pa, 0);
     load_tile(pb, 1);
     int t = 0;
@@ -681,8 +695,8 @@ static int etsi_check(tetra_ctx *ctx, const tetra_etsi_plan *P) {
 }
 
 // Stage-1 taps and the per-branch stage-2 tap table (k_chanfilt), then the launch.
-static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *x, size_t C, size_t N, int64_t M1,
-                           int64_t M2, float2 *y) {
+static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *x, int fmt, size_t C, size_t N,
+                           int64_t M1, int64_t M2, float2 *y) {
     float *coef = (float *)ws(ctx, S_W6, (64 + 3 * HQ) * 4);
     if (!coef) return TETRA_E_NOMEM;
     float *hc = ctx->coef_etsi;
@@ -695,8 +709,12 @@ static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void 
         }
     HIP_TRY(ctx, hipMemcpyAsync(coef, hc, (64 + 3 * HQ) * 4, hipMemcpyHostToDevice, ctx->stream));
     PROF(ctx, "etsi_chanfilt");
-    hipLaunchKernelGGL(k_chanfilt, dim3((unsigned)C), dim3(256), 0, ctx->stream, (const float4 *)x, (long)N, (int)M1,
-                       (int)M2, coef, coef + 64, y);
+    if (fmt == TETRA_SC16)
+        hipLaunchKernelGGL(k_chanfilt<uint2>, dim3((unsigned)C), dim3(256), 0, ctx->stream, (const uint2 *)x, (long)N,
+                           (int)M1, (int)M2, coef, coef + 64, y);
+    else
+        hipLaunchKernelGGL(k_chanfilt<float4>, dim3((unsigned)C), dim3(256), 0, ctx->stream, (const float4 *)x,
+                           (long)N, (int)M1, (int)M2, coef, coef + 64, y);
     HIP_TRY(ctx, hipGetLastError());
     return TETRA_OK;
 }
@@ -729,18 +747,24 @@ int tetra_etsi_set_cells(tetra_ctx *ctx, const uint32_t *scramb_init, size_t C) 
 }
 
 int tetra_etsi_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *iq, size_t C, size_t N, void *y) {
+    return tetra_etsi_chanfilt_fmt(ctx, P, iq, TETRA_CF32, C, N, y);
+}
+
+int tetra_etsi_chanfilt_fmt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *iq, int fmt, size_t C, size_t N,
+                            void *y) {
     if (!ctx) return TETRA_E_INVALID;
     int rc = etsi_check(ctx, P);
     if (rc) return rc;
     if (N % 2 || C == 0) return tetra_fail(ctx, TETRA_E_INVALID, "N must be even");
+    if (fmt != TETRA_CF32 && fmt != TETRA_SC16) return tetra_fail(ctx, TETRA_E_INVALID, "iq_fmt must be cf32 or sc16");
     int64_t M1, M2, smax;
     tetra_etsi_lengths(P, N, &M1, &M2, &smax);
     if (M2 <= 0) return tetra_fail(ctx, TETRA_E_INVALID, "chunk too short for the channel filter");
     Staging st(ctx);
-    const void *x = st.in(iq, C * N * 8);
+    const void *x = st.in(iq, C * N * (fmt == TETRA_SC16 ? 4 : 8));
     void *yo = st.out(y, C * (size_t)M2 * 8);
     if (!x || !yo) return st.finish();
-    rc = launch_chanfilt(ctx, P, x, C, N, M1, M2, (float2 *)yo);
+    rc = launch_chanfilt(ctx, P, x, fmt, C, N, M1, M2, (float2 *)yo);
     if (rc) return rc;
     return st.finish();
 }
@@ -767,15 +791,21 @@ int tetra_etsi_timing(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *y, s
 
 int tetra_demod_etsi(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *iq, size_t C, size_t N, void *soft,
                      int8_t *softbits, uint8_t *hard, int32_t *nsym, size_t smax, float *diag) {
+    return tetra_demod_etsi_fmt(ctx, P, iq, TETRA_CF32, C, N, soft, softbits, hard, nsym, smax, diag);
+}
+
+int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *iq, int fmt, size_t C, size_t N,
+                         void *soft, int8_t *softbits, uint8_t *hard, int32_t *nsym, size_t smax, float *diag) {
     if (!ctx) return TETRA_E_INVALID;
     int rc = etsi_check(ctx, P);
     if (rc) return rc;
     int64_t M1, M2, sm;
     tetra_etsi_lengths(P, N, &M1, &M2, &sm);
     if (M2 <= 0 || N % 2 || C == 0) return tetra_fail(ctx, TETRA_E_INVALID, "bad chunk for the ETSI demod");
+    if (fmt != TETRA_CF32 && fmt != TETRA_SC16) return tetra_fail(ctx, TETRA_E_INVALID, "iq_fmt must be cf32 or sc16");
     if ((int64_t)smax < sm) return tetra_fail(ctx, TETRA_E_INVALID, "smax < %ld", (long)sm);
     Staging st(ctx);
-    const void *x = st.in(iq, C * N * 8);
+    const void *x = st.in(iq, C * N * (fmt == TETRA_SC16 ? 4 : 8));
     void *so = st.out(soft, C * smax * 8);
     int8_t *sbo = (int8_t *)st.out(softbits, C * smax * 2);
     uint8_t *ho = (uint8_t *)st.out(hard, C * smax);
@@ -784,7 +814,7 @@ int tetra_demod_etsi(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *iq, s
     float2 *yb = (float2 *)ws(ctx, S_W3, C * (size_t)M2 * 8);
     float2 *dscr = (float2 *)ws(ctx, S_W4, C * smax * 8);
     if (!x || !so || !sbo || !ho || !no || !yb || !dscr) return st.finish();
-    rc = launch_chanfilt(ctx, P, x, C, N, M1, M2, yb);
+    rc = launch_chanfilt(ctx, P, x, fmt, C, N, M1, M2, yb);
     if (rc) return rc;
     {
         PROF(ctx, "etsi_timing");

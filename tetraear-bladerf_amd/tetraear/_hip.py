@@ -13,7 +13,7 @@ import numpy as np
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TETRA_HIP_LIB", os.path.join(os.path.dirname(_PKG), "lib", "libtetra_hip.so"))
 
-TETRA_CF32, TETRA_CF64 = 0, 1
+TETRA_CF32, TETRA_CF64, TETRA_SC16 = 0, 1, 2
 MAX_SYNC = 16
 F_POS, F_START, F_VALID, F_NBITS, F_NUMBER, F_BTYPE, F_CRC, F_HDR, F_FIELDS = range(9)
 
@@ -88,6 +88,9 @@ def _bind(L):
         "tetra_etsi_chanfilt": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _sz, _sz, _vp]),
         "tetra_etsi_timing": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _sz, _sz, _vp, _vp, _vp, _vp, _sz, _vp]),
         "tetra_demod_etsi": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _sz, _sz, _vp, _vp, _vp, _vp, _sz, _vp]),
+        "tetra_etsi_chanfilt_fmt": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _i32, _sz, _sz, _vp]),
+        "tetra_demod_etsi_fmt": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _i32, _sz, _sz, _vp, _vp, _vp, _vp, _sz,
+                                        _vp]),
         "tetra_etsi_set_cells": (_i32, [_vp, _vp, _sz]),
         "tetra_lmac_etsi": (_i32, [_vp, _vp, _vp, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp]),
         "tetra_etsi_decode_blocks": (_i32, [_vp, _vp, _sz, _i32, _vp, _vp, _vp]),

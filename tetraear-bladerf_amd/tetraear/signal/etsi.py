@@ -79,9 +79,17 @@ class EtsiReceiver:
         self.diag = None
 
     def demod_batch(self, iq):
-        """[C, N] complex -> (hard [C, smax] u8, soft_bits [C, 2*smax] i8, symbols [C, smax] c64, nsym [C])."""
-        x = np.ascontiguousarray(iq, dtype=np.complex64)
-        C, N = x.shape
+        """[C, N] complex, or [C, N, 2] int16 SC16 capture samples (scaled 1/32768 in the channel
+        filter, as capture.py:241-269 scales them) -> (hard [C, smax] u8, soft_bits [C, 2*smax] i8,
+        symbols [C, smax] c64, nsym [C])."""
+        iq = np.asarray(iq)
+        if iq.dtype == np.int16:
+            if iq.ndim != 3 or iq.shape[-1] != 2:
+                raise ValueError("SC16 input must be [C, N, 2] int16")
+            fmt, x = _hip.TETRA_SC16, np.ascontiguousarray(iq)
+        else:
+            fmt, x = _hip.TETRA_CF32, np.ascontiguousarray(iq, dtype=np.complex64)
+        C, N = x.shape[:2]
         if N % 2:
             x = np.ascontiguousarray(x[:, :N - 1])
             N -= 1
@@ -92,8 +100,9 @@ class EtsiReceiver:
         ns = np.zeros(C, np.int32)
         diag = np.zeros((C, 4), np.float32)
         c = _hip.ctx()
-        c.check(c.lib.tetra_demod_etsi(c.handle, self.plan, _hip.ptr(x), C, N, _hip.ptr(sym), _hip.ptr(soft),
-                                       _hip.ptr(hard), _hip.ptr(ns), smax, _hip.ptr(diag)), "tetra_demod_etsi")
+        c.check(c.lib.tetra_demod_etsi_fmt(c.handle, self.plan, _hip.ptr(x), fmt, C, N, _hip.ptr(sym),
+                                           _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(ns), smax, _hip.ptr(diag)),
+                "tetra_demod_etsi")
         self.diag = diag
         return hard, soft, sym, ns
 
@@ -140,9 +149,10 @@ class BenchStep:
 
     dtype = "f32 (DSP), int8/int32 (Viterbi)"
 
-    def __init__(self, c, C, N, fs, seed, device, snr_db=18.0):
+    def __init__(self, c, C, N, fs, seed, device, snr_db=18.0, iq_format="cf32"):
         import torch
         self.c, self.C, self.N, self.fs = c, C, N, fs
+        self.fmt = {"cf32": _hip.TETRA_CF32, "sc16": _hip.TETRA_SC16}[iq_format]
         self.plan = etsi_plan(fs)
         _, self.M2, self.smax = lengths(self.plan, N)
         nb = c.lib.tetra_synth_bursts_per_channel(N, fs)
@@ -153,6 +163,8 @@ class BenchStep:
         c.check(c.lib.tetra_synth_etsi(c.handle, C, N, fs, seed, snr_db, 600.0, _hip.ptr(self.iq), _hip.ptr(self.cells),
                                        _hip.ptr(self.kinds), _hip.ptr(self.payload), None), "synth")
         c.check(c.lib.tetra_etsi_set_cells(c.handle, _hip.ptr(self.cells), C), "set_cells")
+        if self.fmt == _hip.TETRA_SC16:   # the synth output is on the SC16 grid: exact
+            self.iq = torch.round(self.iq * 32768).clamp_(-32768, 32767).to(torch.int16)
         sm = self.smax
         self.sym = torch.empty((C, sm, 2), dtype=torch.float32, device=device)
         self.soft = torch.empty((C, 2 * sm), dtype=torch.int8, device=device)
@@ -202,9 +214,9 @@ class BenchStep:
     def __call__(self):
         c = self.c
         if not self.pipelined:
-            c.check(c.lib.tetra_demod_etsi(c.handle, self.plan, _hip.ptr(self.iq), self.C, self.N,
-                                           _hip.ptr(self.sym), _hip.ptr(self.soft), _hip.ptr(self.hard),
-                                           _hip.ptr(self.nsym), self.smax, None), "demod_etsi")
+            c.check(c.lib.tetra_demod_etsi_fmt(c.handle, self.plan, _hip.ptr(self.iq), self.fmt, self.C, self.N,
+                                               _hip.ptr(self.sym), _hip.ptr(self.soft), _hip.ptr(self.hard),
+                                               _hip.ptr(self.nsym), self.smax, None), "demod_etsi")
             c.check(c.lib.tetra_lmac_etsi(c.handle, _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym),
                                           self.C, self.smax, _hip.ptr(self.nburst), _hip.ptr(self.bursts),
                                           _hip.ptr(self.nblock), _hip.ptr(self.blocks), _hip.ptr(self.type1)),
@@ -214,16 +226,17 @@ class BenchStep:
         self.k += 1
         y = self.y[i]
         self.s_front.wait_event(self.ev_back[i])        # back end of batch k-2 has consumed y[i]
-        c.check(c.lib.tetra_etsi_chanfilt(c.handle, self.plan, _hip.ptr(self.iq), self.C, self.N, _hip.ptr(y)),
-                "etsi_chanfilt")
+        c.check(c.lib.tetra_etsi_chanfilt_fmt(c.handle, self.plan, _hip.ptr(self.iq), self.fmt, self.C, self.N,
+                                              _hip.ptr(y)), "etsi_chanfilt")
         self.ev_front[i].record(self.s_front)
         self.s_back.wait_event(self.ev_front[i])
         self._back_end(self.back, y)
         self.ev_back[i].record(self.s_back)
 
     def dominant(self):
-        # k_chanfilt: reads 8 B per input sample, writes 8 B per 72 kHz output (3/100 per input)
-        return ("etsi_chanfilt", 8.0 + 8.0 * 0.03, "k_chanfilt")
+        # k_chanfilt: reads 8 B (cf32) or 4 B (SC16) per input sample, writes 8 B per 72 kHz output
+        # (3/100 per input)
+        return ("etsi_chanfilt", (4.0 if self.fmt == _hip.TETRA_SC16 else 8.0) + 8.0 * 0.03, "k_chanfilt")
 
     def quality(self):
         """Decoded-block statistics of the last step (device results, checked on the host)."""
@@ -239,7 +252,10 @@ class BenchStep:
         repo = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
         sys.path.insert(0, os.path.join(repo, "oracle"))
         import etsi as oracle   # the CPU restatement (cpu_baseline leg only)
-        x = self.iq[:4].cpu().numpy().view(np.complex64)[..., 0]
+        x = self.iq[:4].float().cpu().numpy()
+        if self.fmt == _hip.TETRA_SC16:
+            x = x / 32768   # the oracle filters cf32; SC16 -> cf32 is exact
+        x = np.ascontiguousarray(x, np.float32).view(np.complex64)[..., 0]
         cells = self.cells[:4].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
         rx = oracle.Receiver(self.fs)
         t0 = time.perf_counter()

@@ -21,7 +21,7 @@ def _csv(d, name):
 
 def short(n):
     n = n.replace("(anonymous namespace)::", "")
-    return n.split("(")[0]
+    return n.split("(")[0].split("<")[0].replace("void ", "")
 
 
 def main():
