@@ -31,7 +31,7 @@ constexpr int TILE_IN = TILE_K * 10;   // new input samples per tile (q1 = 10)
 constexpr int HALO = 48;
 
 struct KindP { int K, a, n2, n1; };
-__host__ __device__ inline KindP kind_params(int kind) {
+__host__ __device__ constexpr KindP kind_params(int kind) {
     return kind == 0 ? KindP{432, 103, 288, 268} : kind == 1 ? KindP{216, 101, 144, 124} : KindP{120, 11, 80, 60};
 }
 
@@ -395,17 +395,30 @@ struct Job {
     int ch, slot, burst, blk, kind, off;
 };
 
+// Job regions, one per block kind, so every Viterbi wave runs a single trellis length:
+// SCH/F [0, 8C), SCH/HD [8C, 24C), BSCH [24C, 32C) (<= 8 bursts per channel chunk).
+__host__ __device__ inline size_t job_base(int kind, size_t C) { return kind == 0 ? 0 : kind == 1 ? 8 * C : 24 * C; }
+__host__ __device__ inline size_t job_cap(int kind, size_t C) { return kind == 1 ? 16 * C : 8 * C; }
+
 // One wave per channel: pack hard bits, greedy burst scan, then allocate this channel's coded
-// blocks a dense range of job indices (one atomic per channel; outputs are indexed by
-// (channel, slot), so results do not depend on the allocation order).
-__global__ __launch_bounds__(64) void k_etsi_sync(const uint8_t *__restrict__ hard, const int32_t *__restrict__ nsym,
+// blocks dense job indices in each kind's region (one atomic per kind per channel; outputs are
+// indexed by (channel, slot), so results do not depend on the allocation order).
+constexpr int SYNC_WAVES = 4;   // channels per workgroup: one job-counter atomic per workgroup
+
+__global__ __launch_bounds__(64 * SYNC_WAVES) void k_etsi_sync(const uint8_t *__restrict__ hard, const int32_t *__restrict__ nsym,
                                                   int smax, int32_t *__restrict__ nburst, int32_t *__restrict__ bursts,
-                                                  int32_t *__restrict__ nblock, int32_t *__restrict__ jcount,
-                                                  Job *__restrict__ jobs) {
-    const int ch = blockIdx.x, lane = threadIdx.x;
-    __shared__ uint64_t words[LMAC_MAXBITS / 64 + 2];
-    __shared__ int bstart[ETSI_MAXB], bkind[ETSI_MAXB];
-    const int S = nsym[ch];
+                                                  int32_t *__restrict__ nblock,
+                                                  unsigned long long *__restrict__ jcount, Job *__restrict__ jobs,
+                                                  int C) {
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ch = blockIdx.x * SYNC_WAVES + wv;
+    __shared__ uint64_t words_all[SYNC_WAVES][LMAC_MAXBITS / 64 + 2];
+    __shared__ int bstart_all[SYNC_WAVES][ETSI_MAXB], bkind_all[SYNC_WAVES][ETSI_MAXB];
+    __shared__ int per_all[SYNC_WAVES][3];
+    __shared__ unsigned long long block_old;
+    uint64_t *words = words_all[wv];
+    int *bstart = bstart_all[wv], *bkind = bkind_all[wv];
+    const int S = ch < C ? nsym[ch] : 0;
     int nbits = 2 * (S > 1 ? S - 1 : 0);
     if (nbits > LMAC_MAXBITS) nbits = LMAC_MAXBITS;
     const uint8_t *hp = hard + (size_t)ch * smax;
@@ -455,25 +468,45 @@ __global__ __launch_bounds__(64) void k_etsi_sync(const uint8_t *__restrict__ ha
         }
     }
     __syncthreads();
-    if (lane == 0) {
-        int njob = 0;
-        for (int b = 0; b < nb; ++b) njob += bkind[b] == 0 ? 1 : 2;
+    int per[3] = {0, 0, 0};
+    if (lane == 0) {   // blocks per kind: normal-n 1 SCH/F; normal-p 2 SCH/HD; sync BSCH + SCH/HD
+        for (int b = 0; b < nb; ++b) {
+            if (bkind[b] == 0) ++per[0];
+            else if (bkind[b] == 1) per[1] += 2;
+            else { ++per[2]; ++per[1]; }
+        }
+        for (int k = 0; k < 3; ++k) per_all[wv][k] = per[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {   // the workgroup's three kind counters, packed 21 bits apart: one atomic
+        unsigned long long inc = 0;
+        for (int w = 0; w < SYNC_WAVES; ++w)
+            inc += (unsigned long long)per_all[w][0] | ((unsigned long long)per_all[w][1] << 21) |
+                   ((unsigned long long)per_all[w][2] << 42);
+        block_old = inc ? atomicAdd(jcount, inc) : 0ull;
+    }
+    __syncthreads();
+    if (lane == 0 && ch < C) {
         nburst[ch] = nb;
-        nblock[ch] = njob;
-        const int base = njob ? atomicAdd(jcount, njob) : 0;
+        nblock[ch] = per[0] + per[1] + per[2];
+        int next[3];
+        for (int k = 0; k < 3; ++k) {
+            next[k] = (int)job_base(k, C) + (int)((block_old >> (21 * k)) & 0x1FFFFFull);
+            for (int w = 0; w < wv; ++w) next[k] += per_all[w][k];
+        }
         int q = 0;
         for (int b = 0; b < nb; ++b) {
             const int s = bstart[b], k = bkind[b];
             bursts[((size_t)ch * ETSI_MAXB + b) * 2] = s;
             bursts[((size_t)ch * ETSI_MAXB + b) * 2 + 1] = k;
             if (k == 0) {
-                jobs[base + q] = Job{ch, q, b, 0, 0, s + 14}; ++q;
+                jobs[next[0]++] = Job{ch, q, b, 0, 0, s + 14}; ++q;
             } else if (k == 1) {
-                jobs[base + q] = Job{ch, q, b, 0, 1, s + 14}; ++q;
-                jobs[base + q] = Job{ch, q, b, 1, 1, s + 282}; ++q;
+                jobs[next[1]++] = Job{ch, q, b, 0, 1, s + 14}; ++q;
+                jobs[next[1]++] = Job{ch, q, b, 1, 1, s + 282}; ++q;
             } else {
-                jobs[base + q] = Job{ch, q, b, 0, 2, s + 94}; ++q;
-                jobs[base + q] = Job{ch, q, b, 1, 1, s + 282}; ++q;
+                jobs[next[2]++] = Job{ch, q, b, 0, 2, s + 94}; ++q;
+                jobs[next[1]++] = Job{ch, q, b, 1, 1, s + 282}; ++q;
             }
         }
     }
@@ -514,24 +547,23 @@ __device__ __forceinline__ void acs_pairs(int32_t (&pm)[16], const int8_t *row, 
     }
 }
 
-__global__ __launch_bounds__(64) void k_etsi_viterbi(const Job *__restrict__ jobs, const int32_t *__restrict__ jcount,
-                                                     int jmax, const int8_t *__restrict__ softbits, int smax,
-                                                     const uint8_t *__restrict__ cell_scr,
-                                                     const uint8_t *__restrict__ bsch_scr,
-                                                     uint16_t *__restrict__ surv, int32_t *__restrict__ blocks,
-                                                     uint8_t *__restrict__ type1) {
-    __shared__ __attribute__((aligned(16))) int8_t rows[64 * VROW];
+template <int KIND>
+__device__ __forceinline__ void viterbi_wave(int8_t *rows, const Job *__restrict__ jobs, int nj, size_t jbase, int lb,
+                                             size_t ss, const int8_t *__restrict__ softbits, int smax,
+                                             const uint8_t *__restrict__ cell_scr,
+                                             const uint8_t *__restrict__ bsch_scr, uint16_t *__restrict__ surv,
+                                             int32_t *__restrict__ blocks, uint8_t *__restrict__ type1) {
+    constexpr KindP P = kind_params(KIND);
     const int lane = threadIdx.x;
-    const int j = blockIdx.x * 64 + lane;
-    const int nj = *jcount;
-    if (blockIdx.x * 64 >= nj) return;   // whole wave past the job count
-    const bool act = j < nj;
-    Job jb = act ? jobs[j] : Job{0, 0, 0, 0, 1, 0};
-    const KindP P = kind_params(jb.kind);
+    const int jl = lb * 64 + lane;
+    if (lb * 64 >= nj) return;   // whole wave past this kind's job count
+    const bool act = jl < nj;
+    const size_t j = jbase + jl;
+    const Job jb = act ? jobs[j] : Job{0, 0, 0, 0, KIND, 0};
     int8_t *row = rows + lane * VROW;
     if (act) {
         const int8_t *sb = softbits + (size_t)jb.ch * 2 * smax + jb.off;
-        const uint8_t *scr = jb.kind == 2 ? bsch_scr : cell_scr + (size_t)jb.ch * 432;
+        const uint8_t *scr = KIND == 2 ? bsch_scr : cell_scr + (size_t)jb.ch * 432;
         int r = 0;   // a*i mod K, incrementally
         for (int i0 = 1; i0 <= P.K; i0 += 8) {   // K is a multiple of 8: gathers issued 8 ahead
             int kk[8];
@@ -545,7 +577,7 @@ __global__ __launch_bounds__(64) void k_etsi_viterbi(const Job *__restrict__ job
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                const int pos = (jb.kind == 0 && kk[u] >= 216) ? kk[u] + 52 : kk[u];   // SCH/F: BKN2 268 after BKN1
+                const int pos = (KIND == 0 && kk[u] >= 216) ? kk[u] + 52 : kk[u];   // SCH/F: BKN2 268 after BKN1
                 v[u] = sb[pos];
                 sc[u] = scr[kk[u]];
             }
@@ -557,13 +589,10 @@ __global__ __launch_bounds__(64) void k_etsi_viterbi(const Job *__restrict__ job
 #pragma unroll
     for (int n = 0; n < 16; ++n) pm[n] = n == 0 ? 0 : -(1 << 28);
     uint16_t *sv = surv + j;
-    const size_t ss = (size_t)jmax;
     if (act) {
-        if (P.n2 == 288) acs_pairs<144>(pm, row, sv, ss);
-        else if (P.n2 == 144) acs_pairs<72>(pm, row, sv, ss);
-        else acs_pairs<40>(pm, row, sv, ss);
+        acs_pairs<P.n2 / 2>(pm, row, sv, ss);
         // traceback from state 0 (tail bits), CRC over type-1 + CRC bits on the fly
-        const int L = P.n1 + 16;
+        constexpr int L = P.n1 + 16;
         uint32_t c = CRC_TAB.init[L];
         int s2 = 0;
         uint8_t *op = type1 + ((size_t)jb.ch * ETSI_MAXJ + jb.slot) * 268;
@@ -581,11 +610,35 @@ __global__ __launch_bounds__(64) void k_etsi_viterbi(const Job *__restrict__ job
             }
         }
         int32_t *bm = blocks + ((size_t)jb.ch * ETSI_MAXJ + jb.slot) * 4;
-        bm[0] = jb.kind;
+        bm[0] = KIND;
         bm[1] = c == 0x1D0Fu;
         bm[2] = jb.burst;
         bm[3] = jb.blk;
     }
+}
+
+// Grid: the SCH/F region's waves, then SCH/HD's, then BSCH's (one trellis length per wave).
+__global__ __launch_bounds__(64) void k_etsi_viterbi(const Job *__restrict__ jobs,
+                                                     const unsigned long long *__restrict__ jcount, int C, const int8_t *__restrict__ softbits, int smax,
+                                                     const uint8_t *__restrict__ cell_scr,
+                                                     const uint8_t *__restrict__ bsch_scr,
+                                                     uint16_t *__restrict__ surv, int32_t *__restrict__ blocks,
+                                                     uint8_t *__restrict__ type1) {
+    __shared__ __attribute__((aligned(16))) int8_t rows[64 * VROW];
+    const int b = blockIdx.x;
+    const int nb0 = (int)((job_cap(0, C) + 63) / 64), nb1 = (int)((job_cap(1, C) + 63) / 64);
+    const size_t ss = 32 * (size_t)C;
+    const unsigned long long cnt = *jcount;
+    const int n0 = (int)(cnt & 0x1FFFFFull), n1 = (int)((cnt >> 21) & 0x1FFFFFull), n2 = (int)(cnt >> 42);
+    if (b < nb0)
+        viterbi_wave<0>(rows, jobs, n0, job_base(0, C), b, ss, softbits, smax, cell_scr, bsch_scr, surv, blocks,
+                        type1);
+    else if (b < nb0 + nb1)
+        viterbi_wave<1>(rows, jobs, n1, job_base(1, C), b - nb0, ss, softbits, smax, cell_scr, bsch_scr, surv,
+                        blocks, type1);
+    else
+        viterbi_wave<2>(rows, jobs, n2, job_base(2, C), b - nb0 - nb1, ss, softbits, smax, cell_scr, bsch_scr,
+                        surv, blocks, type1);
 }
 
 // --------------------------------------------------------------------------- component kernels
@@ -881,24 +934,25 @@ int tetra_lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard,
     int32_t *nko = (int32_t *)st.out(nblock, C * 4);
     int32_t *ko = (int32_t *)st.out(blocks, C * ETSI_MAXJ * 4 * 4);
     uint8_t *to = (uint8_t *)st.out(type1, C * ETSI_MAXJ * 268);
-    const size_t jmax = C * ETSI_MAXJ;
-    // workspace: [job counter (16 B)] [jobs] [survivors: 288 steps x jmax]
-    char *w = (char *)ws(ctx, S_W7, 16 + jmax * sizeof(Job) + 288 * jmax * 2);
+    const size_t jtot = 32 * C;   // the three job regions (job_base / job_cap)
+    // workspace: [job counters per kind (16 B)] [jobs] [survivors: 288 steps x jtot]
+    char *w = (char *)ws(ctx, S_W7, 16 + jtot * sizeof(Job) + 288 * jtot * 2);
     if (!sb || !hd || !ns || !nbo || !bo || !nko || !ko || !to || !w) return st.finish();
-    int32_t *jcount = (int32_t *)w;
+    unsigned long long *jcount = (unsigned long long *)w;
     Job *jobs = (Job *)(w + 16);
-    uint16_t *surv = (uint16_t *)(w + 16 + jmax * sizeof(Job));
+    uint16_t *surv = (uint16_t *)(w + 16 + jtot * sizeof(Job));
     const uint8_t *cells = (const uint8_t *)ctx->slot[S_W5].p;
     {
         PROF(ctx, "etsi_sync");
         HIP_TRY(ctx, hipMemsetAsync(jcount, 0, 16, ctx->stream));
-        hipLaunchKernelGGL(k_etsi_sync, dim3((unsigned)C), dim3(64), 0, ctx->stream, hd, ns, (int)smax, nbo, bo, nko,
-                           jcount, jobs);
+        hipLaunchKernelGGL(k_etsi_sync, dim3((unsigned)((C + SYNC_WAVES - 1) / SYNC_WAVES)), dim3(64 * SYNC_WAVES), 0,
+                           ctx->stream, hd, ns, (int)smax, nbo, bo, nko, jcount, jobs, (int)C);
     }
     {
         PROF(ctx, "etsi_viterbi");
-        hipLaunchKernelGGL(k_etsi_viterbi, dim3((unsigned)((jmax + 63) / 64)), dim3(64), 0, ctx->stream, jobs, jcount,
-                           (int)jmax, sb, (int)smax, cells, cells + ctx->cells * 432, surv, ko, to);
+        const unsigned nblk = (unsigned)((job_cap(0, C) + 63) / 64 + (job_cap(1, C) + 63) / 64 + (job_cap(2, C) + 63) / 64);
+        hipLaunchKernelGGL(k_etsi_viterbi, dim3(nblk), dim3(64), 0, ctx->stream, jobs, jcount, (int)C, sb, (int)smax,
+                           cells, cells + ctx->cells * 432, surv, ko, to);
     }
     return st.finish();
 }
