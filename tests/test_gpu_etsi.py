@@ -41,7 +41,17 @@ def test_chanfilt_and_timing_bit_exact(synth_small):
     y = np.zeros((C, M2), np.complex64)
     c = _hip.ctx()
     c.check(c.lib.tetra_etsi_chanfilt(c.handle, plan, _hip.ptr(iq), C, N, _hip.ptr(y)))
-    hard, soft, sym, ns = EtsiReceiver().demod_batch(iq)
+    hard, soft, sym, ns = EtsiReceiver().demod_batch(iq)   # fused: y stays in LDS
+    # the component path (chanfilt -> y in HBM -> k_timing) gives the same symbols
+    sym2 = np.zeros_like(sym)
+    soft2, hard2, ns2 = np.zeros_like(soft), np.zeros_like(hard), np.zeros_like(ns)
+    c.check(c.lib.tetra_etsi_timing(c.handle, plan, _hip.ptr(y), C, M2, _hip.ptr(sym2), _hip.ptr(soft2),
+                                    _hip.ptr(hard2), _hip.ptr(ns2), smax, None))
+    assert np.array_equal(ns, ns2)
+    for ch in range(C):
+        n = int(ns[ch])
+        assert np.array_equal(sym[ch, :n], sym2[ch, :n]) and np.array_equal(hard[ch, :n - 1], hard2[ch, :n - 1])
+        assert np.array_equal(soft[ch, :2 * (n - 1)], soft2[ch, :2 * (n - 1)])
     for ch in range(C):
         yo = rx.chanfilt(iq[ch])
         assert len(yo) == M2 and np.array_equal(y[ch], yo), ch

@@ -35,6 +35,192 @@ __host__ __device__ constexpr KindP kind_params(int kind) {
     return kind == 0 ? KindP{432, 103, 288, 268} : kind == 1 ? KindP{216, 101, 144, 124} : KindP{120, 11, 80, 60};
 }
 
+// --------------------------------------------------------------------------- E2 timing
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
+    return v;
+}
+
+__device__ __forceinline__ float pat2(float y, float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    const float a = mx == 0.0f ? 0.0f : mn / mx;
+    const float s = a * a;
+    float r = fmaf(fmaf(fmaf(fmaf(fmaf(-0.0117212f, s, 0.05265332f), s, -0.11643287f), s, 0.19354346f), s,
+                        -0.33262347f), s, 0.99997726f) * a;
+    if (ay > ax) r = 1.57079637f - r;
+    if (x < 0.0f) r = 3.14159274f - r;
+    if (y < 0.0f) r = -r;
+    return r;
+}
+
+// Cubic Lagrange interpolation of y at t (y[n] at w[n - w0]).
+__device__ __forceinline__ float2 interp(const float2 *w, int w0, float t) {
+    const float K6 = 1.0f / 6.0f;
+    const float fi = floorf(t);
+    const int i = (int)fi;
+    const float f = t - fi;
+    const float fm1 = f - 1.0f, fm2 = f - 2.0f, fp1 = f + 1.0f;
+    const float cm = -(f * fm1 * fm2) * K6;
+    const float c0 = (fp1 * fm1 * fm2) * 0.5f;
+    const float c1 = -(fp1 * f * fm2) * 0.5f;
+    const float c2 = (fp1 * f * fm1) * K6;
+    const float2 a = w[i - 1 - w0], b = w[i - w0], c = w[i + 1 - w0], d = w[i + 2 - w0];
+    float r = cm * a.x, q = cm * a.y;
+    r = fmaf(c0, b.x, r); q = fmaf(c0, b.y, q);
+    r = fmaf(c1, c.x, r); q = fmaf(c1, c.y, q);
+    r = fmaf(c2, d.x, r); q = fmaf(c2, d.y, q);
+    return make_float2(r, q);
+}
+
+__device__ __forceinline__ float2 csqrt_p(float x, float y) {
+    const float r = sqrtf(fmaf(x, x, y * y));
+    if (r == 0.0f) return make_float2(0.f, 0.f);
+    if (x >= 0.0f) {
+        const float s = sqrtf((r + x) * 0.5f);
+        return make_float2(s, y / (2.0f * s));
+    }
+    float s = sqrtf((r - x) * 0.5f);
+    if (y < 0.0f) s = -s;
+    return make_float2(y / (2.0f * s), s);
+}
+
+// The timing + decision stage for one channel, run by one wave (lane = 0..63).  y / dp may point
+// to global memory (k_timing) or LDS (k_demod_fused); every cross-lane exchange is a wave
+// reduction or shuffle, so no workgroup barrier is needed.
+__device__ __forceinline__ void timing_wave(const float2 *y, int M2, float gain, float soft_scale, float2 *sp,
+                                            float2 *dp, int8_t *sb, uint8_t *hp, int32_t *nsym_ch, float4 *diag_ch,
+                                            int smax, int lane) {
+    if (M2 < 16) {
+        if (lane == 0) *nsym_ch = 0;
+        return;
+    }
+    // Oerder-Meyr: class sums of |y|^2 over n mod 4 (loads issued 8 ahead; same summation order)
+    float s = 0.f;
+    for (int n0 = lane; n0 < M2; n0 += 8 * 64) {
+        float2 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = n0 + 64 * u < M2 ? y[n0 + 64 * u] : make_float2(0.f, 0.f);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (n0 + 64 * u < M2) s += fmaf(v[u].x, v[u].x, v[u].y * v[u].y);
+    }
+#pragma unroll
+    for (int off = 32; off >= 4; off >>= 1) s = s + __shfl_xor(s, off, 64);
+    const float A0 = __shfl(s, 0, 64), A1 = __shfl(s, 1, 64), A2 = __shfl(s, 2, 64), A3 = __shfl(s, 3, 64);
+    const float Xr = A0 - A2, Xi = A3 - A1;
+    const float p = -0.63661977236758134f * pat2(Xi, Xr);
+    float base = p < 0.0f ? p + 4.0f : p;
+    if (base >= 4.0f) base -= 4.0f;
+    const int kstart = base >= 3.0f ? 0 : 1;
+    float delta = 0.0f;
+    int S = 0;
+    float2 prev = make_float2(0.f, 0.f);
+    bool have_prev = false;
+    for (int kb = kstart;; kb += 64) {
+        const float off = base + delta;
+        const float t = (float)(4 * (kb + lane)) + off;
+        const bool valid = (t - 3.0f >= 0.0f) && (t + 2.0f <= (float)(M2 - 1)) && (S + lane < smax);
+        const unsigned long long bal = __ballot(!valid);
+        const int nv = bal ? (__ffsll((long long)bal) - 1) : 64;
+        float2 on = make_float2(0.f, 0.f), mid = make_float2(0.f, 0.f);
+        if (lane < nv) {
+            on = interp(y, 0, t);
+            mid = interp(y, 0, t - 2.0f);
+        }
+        float2 pv = make_float2(__shfl_up(on.x, 1, 64), __shfl_up(on.y, 1, 64));
+        bool hp_ = true;
+        if (lane == 0) { pv = prev; hp_ = have_prev; }
+        float ev = 0.f, pw = 0.f;
+        if (lane < nv) {
+            pw = fmaf(on.x, on.x, on.y * on.y);
+            if (hp_) {
+                const float dr = on.x - pv.x, di = on.y - pv.y;
+                ev = fmaf(dr, mid.x, di * mid.y);
+                const int j = S + lane;
+                dp[j - 1] = make_float2(fmaf(on.x, pv.x, on.y * pv.y), fmaf(on.y, pv.x, -(on.x * pv.y)));
+            }
+            sp[S + lane] = on;
+        }
+        if (nv > 0) {
+            const float E = wave_sum(ev), W = wave_sum(pw);
+            if (W > 0.0f) delta = delta - gain * (E / W);
+            if (delta > 1.5f) delta = 1.5f;
+            if (delta < -1.5f) delta = -1.5f;
+            prev = make_float2(__shfl(on.x, nv - 1, 64), __shfl(on.y, nv - 1, 64));
+            have_prev = true;
+        }
+        S += nv;
+        if (nv < 64) break;
+    }
+    __threadfence_block();   // dp written by other lanes above is read below
+    // CFO (4th power) and soft scale; lane l owns d_j with j & 63 == l, ascending j
+    float zr = 0.f, zi = 0.f, am = 0.f;
+    for (int j0 = lane; j0 < S; j0 += 4 * 64) {   // j = j0 + 64u, j >= 1; loads issued 4 ahead
+        float2 dv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + 64 * u;
+            dv[u] = (j >= 1 && j < S) ? dp[j - 1] : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + 64 * u;
+            if (j >= 1 && j < S) {
+                const float2 d = dv[u];
+                const float sr = fmaf(d.x, d.x, -(d.y * d.y)), si = (d.x * d.y) * 2.0f;
+                const float qr = fmaf(sr, sr, -(si * si)), qi = (sr * si) * 2.0f;
+                zr += qr;
+                zi += qi;
+                am += sqrtf(fmaf(d.x, d.x, d.y * d.y));
+            }
+        }
+    }
+    const float Zr = wave_sum(zr), Zi = wave_sum(zi), A = wave_sum(am);
+    float rr = 1.0f, ri = 0.0f;
+    const float zm = sqrtf(fmaf(Zr, Zr, Zi * Zi));
+    if (zm > 0.0f) {
+        const float2 v = csqrt_p(-Zr / zm, -Zi / zm);
+        const float2 w = csqrt_p(v.x, v.y);
+        rr = w.x;
+        ri = -w.y;
+    }
+    const float sc = (S > 1 && A > 0.0f) ? soft_scale / (A / (float)(S - 1)) : 0.0f;
+    for (int j0 = 1 + lane; j0 < S; j0 += 4 * 64) {
+        float2 dv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) dv[u] = j0 + 64 * u < S ? dp[j0 + 64 * u - 1] : make_float2(0.f, 0.f);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+        const int j = j0 + 64 * u;
+        if (j >= S) break;
+        const float2 d = dv[u];
+        const float xr = fmaf(d.x, rr, -(d.y * ri)), xi = fmaf(d.x, ri, d.y * rr);
+        float q1 = rintf(xi * sc), q2 = rintf(xr * sc);
+        q1 = q1 > 127.f ? 127.f : (q1 < -127.f ? -127.f : q1);
+        q2 = q2 > 127.f ? 127.f : (q2 < -127.f ? -127.f : q2);
+        sb[2 * (j - 1)] = (int8_t)q1;
+        sb[2 * (j - 1) + 1] = (int8_t)q2;
+        hp[j - 1] = (uint8_t)(((xi < 0.0f) << 1) | (xr < 0.0f));
+        }
+    }
+    if (lane == 0) {
+        *nsym_ch = S;
+        if (diag_ch) *diag_ch = make_float4(base, delta, rr, ri);
+    }
+}
+
+__global__ __launch_bounds__(64) void k_timing(const float2 *__restrict__ yall, int M2, float gain, float soft_scale,
+                                               float2 *__restrict__ sym, float2 *__restrict__ dscr,
+                                               int8_t *__restrict__ softbits, uint8_t *__restrict__ hard,
+                                               int32_t *__restrict__ nsym, int smax, float4 *__restrict__ diag) {
+    const int ch = blockIdx.x;
+    timing_wave(yall + (size_t)ch * M2, M2, gain, soft_scale, sym + (size_t)ch * smax, dscr + (size_t)ch * smax,
+                softbits + (size_t)ch * 2 * smax, hard + (size_t)ch * smax, nsym + ch, diag ? diag + ch : nullptr,
+                smax, threadIdx.x);
+}
+
 // --------------------------------------------------------------------------- E1 channel filter
 // The input tile is a linear float4 image (2 samples per entry, ds_write_b128 / ds_read_b128: a
 // 20-dword lane stride is conflict-free for b128's lane groups).  The stage-1 ring is polyphase:
@@ -67,10 +253,22 @@ __device__ __forceinline__ float4 pair_f32(uint2 v) {
                        (float)(int16_t)(v.y & 0xffffu) * s, (float)(int16_t)(v.y >> 16) * s);
 }
 
-template <typename In>
+// Timing outputs of the fused demod (FUSE = true: y never leaves LDS; wave 0 runs the timing
+// stage on it after the last tile, with the input image as its scratch).
+struct TimingOut {
+    float gain, soft_scale;
+    float2 *sym;
+    int8_t *softbits;
+    uint8_t *hard;
+    int32_t *nsym;
+    float4 *diag;
+    int smax;
+};
+
+template <typename In, bool FUSE>
 __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, long N, int M1, int M2,
                                                   const float *__restrict__ h1, const float *__restrict__ hq,
-                                                  float2 *__restrict__ y) {
+                                                  float2 *__restrict__ y, TimingOut to) {
     __shared__ float4 xin[(HALO + TILE_IN) / 2];
     __shared__ float2 ring[10 * RP];
     // Stage-2 outputs collect in LDS and go out in one coalesced burst when the channel is done
@@ -80,7 +278,7 @@ __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, lon
     const int ch = blockIdx.x;
     const int tid = threadIdx.x;
     const In *xp = iq + (size_t)ch * (N / 2);   // N even: 2 complex samples per load
-    float2 *yp = y + (size_t)ch * M2;
+    float2 *yp = FUSE ? nullptr : y + (size_t)ch * M2;
     int ybase = 0;   // y index of yb[0]
     auto flush = [&](int mend) {
         for (int i = tid; i < mend - ybase; i += 256) yp[ybase + i] = make_float2(yb[i].x, yb[i].y);
@@ -182,160 +380,16 @@ __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, lon
         tile(t + 1, pb);
     }
     if (t < ntile) tile(t, pa);
-    flush(M2);   // the last tile ended with a barrier
-}
-
-// --------------------------------------------------------------------------- E2 timing
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
-    return v;
-}
-
-__device__ __forceinline__ float pat2(float y, float x) {
-    const float ax = fabsf(x), ay = fabsf(y);
-    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
-    const float a = mx == 0.0f ? 0.0f : mn / mx;
-    const float s = a * a;
-    float r = fmaf(fmaf(fmaf(fmaf(fmaf(-0.0117212f, s, 0.05265332f), s, -0.11643287f), s, 0.19354346f), s,
-                        -0.33262347f), s, 0.99997726f) * a;
-    if (ay > ax) r = 1.57079637f - r;
-    if (x < 0.0f) r = 3.14159274f - r;
-    if (y < 0.0f) r = -r;
-    return r;
-}
-
-__device__ __forceinline__ float2 interp(const float2 *y, float t) {
-    const float K6 = 1.0f / 6.0f;
-    const float fi = floorf(t);
-    const int i = (int)fi;
-    const float f = t - fi;
-    const float fm1 = f - 1.0f, fm2 = f - 2.0f, fp1 = f + 1.0f;
-    const float cm = -(f * fm1 * fm2) * K6;
-    const float c0 = (fp1 * fm1 * fm2) * 0.5f;
-    const float c1 = -(fp1 * f * fm2) * 0.5f;
-    const float c2 = (fp1 * f * fm1) * K6;
-    const float2 a = y[i - 1], b = y[i], c = y[i + 1], d = y[i + 2];
-    float r = cm * a.x, q = cm * a.y;
-    r = fmaf(c0, b.x, r); q = fmaf(c0, b.y, q);
-    r = fmaf(c1, c.x, r); q = fmaf(c1, c.y, q);
-    r = fmaf(c2, d.x, r); q = fmaf(c2, d.y, q);
-    return make_float2(r, q);
-}
-
-__device__ __forceinline__ float2 csqrt_p(float x, float y) {
-    const float r = sqrtf(fmaf(x, x, y * y));
-    if (r == 0.0f) return make_float2(0.f, 0.f);
-    if (x >= 0.0f) {
-        const float s = sqrtf((r + x) * 0.5f);
-        return make_float2(s, y / (2.0f * s));
-    }
-    float s = sqrtf((r - x) * 0.5f);
-    if (y < 0.0f) s = -s;
-    return make_float2(y / (2.0f * s), s);
-}
-
-__global__ __launch_bounds__(64) void k_timing(const float2 *__restrict__ yall, int M2, float gain, float soft_scale,
-                                               float2 *__restrict__ sym, float2 *__restrict__ dscr,
-                                               int8_t *__restrict__ softbits, uint8_t *__restrict__ hard,
-                                               int32_t *__restrict__ nsym, int smax, float4 *__restrict__ diag) {
-    const int ch = blockIdx.x, lane = threadIdx.x;
-    const float2 *y = yall + (size_t)ch * M2;
-    float2 *sp = sym + (size_t)ch * smax;
-    float2 *dp = dscr + (size_t)ch * smax;
-    int8_t *sb = softbits + (size_t)ch * 2 * smax;
-    uint8_t *hp = hard + (size_t)ch * smax;
-    if (M2 < 16) {
-        if (lane == 0) nsym[ch] = 0;
-        return;
-    }
-    // Oerder-Meyr: class sums of |y|^2 over n mod 4
-    float s = 0.f;
-    for (int n = lane; n < M2; n += 64) {
-        const float2 v = y[n];
-        s += fmaf(v.x, v.x, v.y * v.y);
-    }
-#pragma unroll
-    for (int off = 32; off >= 4; off >>= 1) s = s + __shfl_xor(s, off, 64);
-    const float A0 = __shfl(s, 0, 64), A1 = __shfl(s, 1, 64), A2 = __shfl(s, 2, 64), A3 = __shfl(s, 3, 64);
-    const float Xr = A0 - A2, Xi = A3 - A1;
-    const float p = -0.63661977236758134f * pat2(Xi, Xr);
-    float base = p < 0.0f ? p + 4.0f : p;
-    if (base >= 4.0f) base -= 4.0f;
-    const int kstart = base >= 3.0f ? 0 : 1;
-    float delta = 0.0f;
-    int S = 0;
-    float2 prev = make_float2(0.f, 0.f);
-    bool have_prev = false;
-    for (int kb = kstart;; kb += 64) {
-        const float off = base + delta;
-        const float t = (float)(4 * (kb + lane)) + off;
-        const bool valid = (t - 3.0f >= 0.0f) && (t + 2.0f <= (float)(M2 - 1)) && (S + lane < smax);
-        const unsigned long long bal = __ballot(!valid);
-        const int nv = bal ? (__ffsll((long long)bal) - 1) : 64;
-        float2 on = make_float2(0.f, 0.f), mid = make_float2(0.f, 0.f);
-        if (lane < nv) {
-            on = interp(y, t);
-            mid = interp(y, t - 2.0f);
+    // the last tile ended with a barrier: yb holds y[0, M2) (FUSE requires M2 <= YLDS)
+    if constexpr (FUSE) {
+        if (tid < 64) {
+            const size_t so = (size_t)ch * to.smax;
+            timing_wave(reinterpret_cast<const float2 *>(yb), M2, to.gain, to.soft_scale, to.sym + so,
+                        reinterpret_cast<float2 *>(xin), to.softbits + 2 * so, to.hard + so, to.nsym + ch,
+                        to.diag ? to.diag + ch : nullptr, to.smax, tid);
         }
-        float2 pv = make_float2(__shfl_up(on.x, 1, 64), __shfl_up(on.y, 1, 64));
-        bool hp_ = true;
-        if (lane == 0) { pv = prev; hp_ = have_prev; }
-        float ev = 0.f, pw = 0.f;
-        if (lane < nv) {
-            pw = fmaf(on.x, on.x, on.y * on.y);
-            if (hp_) {
-                const float dr = on.x - pv.x, di = on.y - pv.y;
-                ev = fmaf(dr, mid.x, di * mid.y);
-                const int j = S + lane;
-                dp[j - 1] = make_float2(fmaf(on.x, pv.x, on.y * pv.y), fmaf(on.y, pv.x, -(on.x * pv.y)));
-            }
-            sp[S + lane] = on;
-        }
-        if (nv > 0) {
-            const float E = wave_sum(ev), W = wave_sum(pw);
-            if (W > 0.0f) delta = delta - gain * (E / W);
-            if (delta > 1.5f) delta = 1.5f;
-            if (delta < -1.5f) delta = -1.5f;
-            prev = make_float2(__shfl(on.x, nv - 1, 64), __shfl(on.y, nv - 1, 64));
-            have_prev = true;
-        }
-        S += nv;
-        if (nv < 64) break;
-    }
-    // CFO (4th power) and soft scale; lane l owns d_j with j & 63 == l, ascending j
-    float zr = 0.f, zi = 0.f, am = 0.f;
-    for (int j = (lane == 0 ? 64 : lane); j < S; j += 64) {
-        const float2 d = dp[j - 1];
-        const float sr = fmaf(d.x, d.x, -(d.y * d.y)), si = (d.x * d.y) * 2.0f;
-        const float qr = fmaf(sr, sr, -(si * si)), qi = (sr * si) * 2.0f;
-        zr += qr;
-        zi += qi;
-        am += sqrtf(fmaf(d.x, d.x, d.y * d.y));
-    }
-    const float Zr = wave_sum(zr), Zi = wave_sum(zi), A = wave_sum(am);
-    float rr = 1.0f, ri = 0.0f;
-    const float zm = sqrtf(fmaf(Zr, Zr, Zi * Zi));
-    if (zm > 0.0f) {
-        const float2 v = csqrt_p(-Zr / zm, -Zi / zm);
-        const float2 w = csqrt_p(v.x, v.y);
-        rr = w.x;
-        ri = -w.y;
-    }
-    const float sc = (S > 1 && A > 0.0f) ? soft_scale / (A / (float)(S - 1)) : 0.0f;
-    for (int j = 1 + lane; j < S; j += 64) {
-        const float2 d = dp[j - 1];
-        const float xr = fmaf(d.x, rr, -(d.y * ri)), xi = fmaf(d.x, ri, d.y * rr);
-        float q1 = rintf(xi * sc), q2 = rintf(xr * sc);
-        q1 = q1 > 127.f ? 127.f : (q1 < -127.f ? -127.f : q1);
-        q2 = q2 > 127.f ? 127.f : (q2 < -127.f ? -127.f : q2);
-        sb[2 * (j - 1)] = (int8_t)q1;
-        sb[2 * (j - 1) + 1] = (int8_t)q2;
-        hp[j - 1] = (uint8_t)(((xi < 0.0f) << 1) | (xr < 0.0f));
-    }
-    if (lane == 0) {
-        nsym[ch] = S;
-        if (diag) diag[ch] = make_float4(base, delta, rr, ri);
+    } else {
+        flush(M2);
     }
 }
 
@@ -749,7 +803,7 @@ static int etsi_check(tetra_ctx *ctx, const tetra_etsi_plan *P) {
 
 // Stage-1 taps and the per-branch stage-2 tap table (k_chanfilt), then the launch.
 static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *x, int fmt, size_t C, size_t N,
-                           int64_t M1, int64_t M2, float2 *y) {
+                           int64_t M1, int64_t M2, float2 *y, const TimingOut *fused = nullptr) {
     float *coef = (float *)ws(ctx, S_W6, (64 + 3 * HQ) * 4);
     if (!coef) return TETRA_E_NOMEM;
     float *hc = ctx->coef_etsi;
@@ -761,13 +815,21 @@ static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void 
             hc[64 + c * HQ + r] = j >= 0 && j < TPP ? P->hp[i0[c] - 3 * j] : 0.f;
         }
     HIP_TRY(ctx, hipMemcpyAsync(coef, hc, (64 + 3 * HQ) * 4, hipMemcpyHostToDevice, ctx->stream));
-    PROF(ctx, "etsi_chanfilt");
-    if (fmt == TETRA_SC16)
-        hipLaunchKernelGGL(k_chanfilt<uint2>, dim3((unsigned)C), dim3(256), 0, ctx->stream, (const uint2 *)x, (long)N,
-                           (int)M1, (int)M2, coef, coef + 64, y);
+    PROF(ctx, fused ? "etsi_demod" : "etsi_chanfilt");
+    const TimingOut to = fused ? *fused : TimingOut{};
+    const dim3 g((unsigned)C), b(256);
+    if (fmt == TETRA_SC16 && fused)
+        hipLaunchKernelGGL((k_chanfilt<uint2, true>), g, b, 0, ctx->stream, (const uint2 *)x, (long)N, (int)M1, (int)M2,
+                           coef, coef + 64, y, to);
+    else if (fmt == TETRA_SC16)
+        hipLaunchKernelGGL((k_chanfilt<uint2, false>), g, b, 0, ctx->stream, (const uint2 *)x, (long)N, (int)M1,
+                           (int)M2, coef, coef + 64, y, to);
+    else if (fused)
+        hipLaunchKernelGGL((k_chanfilt<float4, true>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1,
+                           (int)M2, coef, coef + 64, y, to);
     else
-        hipLaunchKernelGGL(k_chanfilt<float4>, dim3((unsigned)C), dim3(256), 0, ctx->stream, (const float4 *)x,
-                           (long)N, (int)M1, (int)M2, coef, coef + 64, y);
+        hipLaunchKernelGGL((k_chanfilt<float4, false>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1,
+                           (int)M2, coef, coef + 64, y, to);
     HIP_TRY(ctx, hipGetLastError());
     return TETRA_OK;
 }
@@ -864,9 +926,16 @@ int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *i
     uint8_t *ho = (uint8_t *)st.out(hard, C * smax);
     int32_t *no = (int32_t *)st.out(nsym, C * 4);
     float *dg = diag ? (float *)st.out(diag, C * 16) : nullptr;
+    if (!x || !so || !sbo || !ho || !no) return st.finish();
+    if (M2 <= YLDS && smax <= (HALO + TILE_IN)) {   // fused: the 72 kHz samples never leave LDS
+        const TimingOut to{P->gain, P->soft_scale, (float2 *)so, sbo, ho, no, (float4 *)dg, (int)smax};
+        rc = launch_chanfilt(ctx, P, x, fmt, C, N, M1, M2, nullptr, &to);
+        if (rc) return rc;
+        return st.finish();
+    }
     float2 *yb = (float2 *)ws(ctx, S_W3, C * (size_t)M2 * 8);
     float2 *dscr = (float2 *)ws(ctx, S_W4, C * smax * 8);
-    if (!x || !so || !sbo || !ho || !no || !yb || !dscr) return st.finish();
+    if (!yb || !dscr) return st.finish();
     rc = launch_chanfilt(ctx, P, x, fmt, C, N, M1, M2, yb);
     if (rc) return rc;
     {

@@ -145,7 +145,7 @@ def synth(C, N, fs=2.4e6, seed=1, snr_db=None, cfo_max=600.0, device_arrays=None
 
 
 class BenchStep:
-    """bench.py workload: device-resident synthetic capture -> demod -> lower MAC, all on one stream."""
+    """bench.py workload: device-resident synthetic capture -> fused demod -> lower MAC."""
 
     dtype = "f32 (DSP), int8/int32 (Viterbi)"
 
@@ -179,10 +179,11 @@ class BenchStep:
         self.pipelined = False
 
     def pipeline(self):
-        """Stream the batches through a two-stage software pipeline: the HBM-bound channel filter of
-        batch k+1 runs on a front stream while the latency-bound back end (timing, sync, Viterbi) of
-        batch k runs on a back stream.  The 72 kHz intermediate is double-buffered; each stage waits
-        only on the event that protects its buffer.  Every step still does the whole chain."""
+        """Stream the batches through a two-stage software pipeline: the fused demod (HBM-bound
+        channel filter + timing) of batch k+1 runs on a front stream while the lower MAC (sync,
+        Viterbi) of batch k runs on a back stream.  The symbol-rate outputs are double-buffered;
+        each stage waits only on the event that protects its buffer.  Every step still does the
+        whole chain."""
         import torch
         dev = self.iq.device
         self.back = _hip.Context()
@@ -191,7 +192,8 @@ class BenchStep:
         self.back.check(self.back.lib.tetra_set_stream(self.back.handle, ctypes.c_void_p(self.s_back.cuda_stream)),
                         "set_stream")
         self.back.check(self.back.lib.tetra_etsi_set_cells(self.back.handle, _hip.ptr(self.cells), self.C), "set_cells")
-        self.y = [torch.empty((self.C, self.M2, 2), dtype=torch.float32, device=dev) for _ in range(2)]
+        self.bufs = [(self.sym, self.soft, self.hard, self.nsym),
+                     tuple(torch.empty_like(t) for t in (self.sym, self.soft, self.hard, self.nsym))]
         self.ev_front = [torch.cuda.Event() for _ in range(2)]
         self.ev_back = [torch.cuda.Event() for _ in range(2)]
         for e in self.ev_back:
@@ -203,40 +205,35 @@ class BenchStep:
     def contexts(self):
         return [self.c] + ([self.back] if self.pipelined else [])
 
-    def _back_end(self, c, y):
-        c.check(c.lib.tetra_etsi_timing(c.handle, self.plan, _hip.ptr(y), self.C, self.M2, _hip.ptr(self.sym),
-                                        _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.smax,
-                                        None), "etsi_timing")
-        c.check(c.lib.tetra_lmac_etsi(c.handle, _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.C,
-                                      self.smax, _hip.ptr(self.nburst), _hip.ptr(self.bursts), _hip.ptr(self.nblock),
+    def _demod(self, c, sym, soft, hard, nsym):
+        c.check(c.lib.tetra_demod_etsi_fmt(c.handle, self.plan, _hip.ptr(self.iq), self.fmt, self.C, self.N,
+                                           _hip.ptr(sym), _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(nsym), self.smax,
+                                           None), "demod_etsi")
+
+    def _lmac(self, c, soft, hard, nsym):
+        c.check(c.lib.tetra_lmac_etsi(c.handle, _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(nsym), self.C, self.smax,
+                                      _hip.ptr(self.nburst), _hip.ptr(self.bursts), _hip.ptr(self.nblock),
                                       _hip.ptr(self.blocks), _hip.ptr(self.type1)), "lmac_etsi")
 
     def __call__(self):
-        c = self.c
         if not self.pipelined:
-            c.check(c.lib.tetra_demod_etsi_fmt(c.handle, self.plan, _hip.ptr(self.iq), self.fmt, self.C, self.N,
-                                               _hip.ptr(self.sym), _hip.ptr(self.soft), _hip.ptr(self.hard),
-                                               _hip.ptr(self.nsym), self.smax, None), "demod_etsi")
-            c.check(c.lib.tetra_lmac_etsi(c.handle, _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym),
-                                          self.C, self.smax, _hip.ptr(self.nburst), _hip.ptr(self.bursts),
-                                          _hip.ptr(self.nblock), _hip.ptr(self.blocks), _hip.ptr(self.type1)),
-                    "lmac_etsi")
+            self._demod(self.c, self.sym, self.soft, self.hard, self.nsym)
+            self._lmac(self.c, self.soft, self.hard, self.nsym)
             return
         i = self.k & 1
         self.k += 1
-        y = self.y[i]
-        self.s_front.wait_event(self.ev_back[i])        # back end of batch k-2 has consumed y[i]
-        c.check(c.lib.tetra_etsi_chanfilt_fmt(c.handle, self.plan, _hip.ptr(self.iq), self.fmt, self.C, self.N,
-                                              _hip.ptr(y)), "etsi_chanfilt")
+        sym, soft, hard, nsym = self.bufs[i]
+        self.s_front.wait_event(self.ev_back[i])        # lower MAC of batch k-2 has consumed buffer i
+        self._demod(self.c, sym, soft, hard, nsym)
         self.ev_front[i].record(self.s_front)
         self.s_back.wait_event(self.ev_front[i])
-        self._back_end(self.back, y)
+        self._lmac(self.back, soft, hard, nsym)
         self.ev_back[i].record(self.s_back)
 
     def dominant(self):
-        # k_chanfilt: reads 8 B (cf32) or 4 B (SC16) per input sample, writes 8 B per 72 kHz output
-        # (3/100 per input)
-        return ("etsi_chanfilt", (4.0 if self.fmt == _hip.TETRA_SC16 else 8.0) + 8.0 * 0.03, "k_chanfilt")
+        # fused k_chanfilt<.., true>: reads 8 B (cf32) or 4 B (SC16) per input sample; writes per
+        # symbol (0.0075 per input sample) 8 B cf32 symbol + 2 B soft bits + 1 B hard dibit
+        return ("etsi_demod", (4.0 if self.fmt == _hip.TETRA_SC16 else 8.0) + 11.0 * 18000.0 / self.fs, "k_chanfilt")
 
     def quality(self):
         """Decoded-block statistics of the last step (device results, checked on the host)."""
