@@ -48,87 +48,216 @@ __device__ __forceinline__ T sos_step(const T (&c)[NSEC * 6], T (&z)[NSEC * 2], 
     return xc;
 }
 
+// Skewed section pipeline: lane = (channel, component, section).  The 4 sections of one stream sit
+// in 4 adjacent lanes; at tick tau section s processes ext sample tau - s, and its input is the
+// output section s-1 produced at tick tau-1 (one DPP row shift).  Each lane runs one biquad per
+// tick, so a stream's 36-operation step becomes a 9-operation tick on 4x the lanes -- the
+// arithmetic (scipy _sosfilt's operation order per section and sample) is unchanged.
 template <typename T>
-__global__ __launch_bounds__(256) void k_sos_fwd(const T *__restrict__ x, Lay lx, int C, long N, int pad,
-                                                 const T *__restrict__ sos, const T *__restrict__ zi,
-                                                 T *__restrict__ scr, Lay ls) {
-    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-    const int ch = gid >> 1, comp = gid & 1;
-    if (ch >= C) return;
-    T c[NSEC * 6], z[NSEC * 2];
-#pragma unroll
-    for (int i = 0; i < NSEC * 6; ++i) c[i] = sos[i];
-    const T *xp = x + lx.off(ch, 0) + comp;
-    const size_t sx = lx.s_n;
-    const T two = 2, x0 = xp[0], xl = xp[(size_t)(N - 1) * sx];
-    // odd extension (scipy _arraytools.odd_ext): ext[j] = 2*x0 - x[pad-j] (j<pad), x[j-pad],
-    // 2*x[N-1] - x[N-2-(j-pad-N)] (j >= pad+N)
-    const T e0 = two * x0 - xp[(size_t)pad * sx];
-#pragma unroll
-    for (int i = 0; i < NSEC * 2; ++i) z[i] = zi[i] * e0;
-    T *sp = scr + ls.off(ch, 0) + comp;
-    const size_t ss = ls.s_n;
-    long j = 0;
-    for (; j < pad; ++j) sp[(size_t)j * ss] = sos_step(c, z, two * x0 - xp[(size_t)(pad - j) * sx]);
-    // body: 16 input loads issued ahead of the dependent recursion (latency, not bandwidth, bound)
-    long n = 0;
-    for (; n + 16 <= N; n += 16, j += 16) {
-        T xs[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) xs[u] = xp[(size_t)(n + u) * sx];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) sp[(size_t)(j + u) * ss] = sos_step(c, z, xs[u]);
+__device__ __forceinline__ T from_left(T v) {   // lane l receives v of lane l-1 (row shift, DPP)
+    if constexpr (sizeof(T) == 4) {
+        return __builtin_bit_cast(T, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, true));
+    } else {
+        const long long b = __builtin_bit_cast(long long, v);
+        const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), 0x111, 0xf, 0xf, true);
+        const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x111, 0xf, 0xf, true);
+        return __builtin_bit_cast(T, ((long long)hi << 32) | (unsigned int)lo);
     }
-    for (; n < N; ++n, ++j) sp[(size_t)j * ss] = sos_step(c, z, xp[(size_t)n * sx]);
-    for (long k = 0; k < pad; ++k, ++j) sp[(size_t)j * ss] = sos_step(c, z, two * xl - xp[(size_t)(N - 2 - k) * sx]);
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void k_sos_bwd(const T *__restrict__ scr, Lay ls, int C, long N, int pad, int q,
-                                                 const T *__restrict__ sos, const T *__restrict__ zi,
-                                                 T *__restrict__ out, Lay lo) {
-    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-    const int ch = gid >> 1, comp = gid & 1;
-    if (ch >= C) return;
-    T c[NSEC * 6], z[NSEC * 2];
-#pragma unroll
-    for (int i = 0; i < NSEC * 6; ++i) c[i] = sos[i];
-    const T *sp = scr + ls.off(ch, 0) + comp;
-    const size_t ss = ls.s_n;
+struct Biquad {
+    T b0, b1, b2, a1, a2, z0, z1;
+    __device__ __forceinline__ T step(T x) {   // scipy _sosfilt, one section
+        const T xn = b0 * x + z0;
+        z0 = (b1 * x - a1 * xn) + z1;
+        z1 = b2 * x - a2 * xn;
+        return xn;
+    }
+};
+
+template <typename T>
+__device__ __forceinline__ Biquad<T> load_section(const T *sos, const T *zi, int s, T x0) {
+    return Biquad<T>{sos[6 * s], sos[6 * s + 1], sos[6 * s + 2], sos[6 * s + 4], sos[6 * s + 5], zi[2 * s] * x0,
+                     zi[2 * s + 1] * x0};
+}
+
+constexpr int SKB = 32;   // ticks per prefetch batch (a multiple of every vector width below)
+
+// 16-byte vectors: the decimator's memory traffic goes through as few VMEM instructions as
+// possible -- with one wave per SIMD the per-wave limit on outstanding VMEM operations, not
+// bandwidth or arithmetic, sets the tick rate when every tick loads and stores.
+template <typename T> struct Vec16;
+template <> struct Vec16<float> { using type = float4; static constexpr int n = 4; };
+template <> struct Vec16<double> { using type = double2; static constexpr int n = 2; };
+template <typename V> __device__ __forceinline__ auto velt(const V &v, int i) {   // i compile-time after unroll
+    if constexpr (sizeof(V) == 4 * sizeof(v.x)) return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
+    else return i == 0 ? v.x : v.y;
+}
+
+// Forward pass over the odd extension ext[0, L) of one stream, L = N + 2 pad.  Scratch is
+// stream-major: stream g = 2 ch + comp at scr[g * Lp + j] (Lp a multiple of 4), so a lane's
+// consecutive outputs are one vector store.  Input rows are complex [C][N]; a vector load holds
+// CPV consecutive complex samples of both components (CPV = 2 for complex64 rows of even length).
+template <typename T, int CPV>
+__global__ __launch_bounds__(64) void k_sos_fwd(const T *__restrict__ x, int C, long N, int pad,
+                                                const T *__restrict__ sos, const T *__restrict__ zi,
+                                                T *__restrict__ scr, long Lp, T *__restrict__ sink) {
+    using V = typename Vec16<T>::type;
+    constexpr int VW = Vec16<T>::n;           // outputs per vector store
+    const int gid = blockIdx.x * 64 + threadIdx.x;
+    const int g = gid >> 2, sec = gid & 3;
+    const int ch = min(g >> 1, C - 1), comp = g & 1;   // tail lanes shadow the last stream, store to sink
+    const bool own = (g >> 1) < C;
+    const bool st = own && sec == 3;
+    const T *xr = x + (size_t)ch * N * 2;      // complex row
     const long L = N + 2 * pad;
-    const T y0 = sp[(size_t)(L - 1) * ss];
+    auto xat = [&](long n) { return xr[2 * n + comp]; };
+    const T two = 2, x0 = xat(0), xl = xat(N - 1);
+    auto ext = [&](long j) -> T {   // scipy _arraytools.odd_ext
+        if (j < pad) return two * x0 - xat(pad - j);
+        if (j < pad + N) return xat(j - pad);
+        return two * xl - xat(N - 2 - (j - pad - N));
+    };
+    Biquad<T> bq = load_section(sos, zi, sec, ext(0));
+    T *sp = scr + (size_t)(2 * ch + comp) * Lp;
+    V *vsink = reinterpret_cast<V *>(sink) + gid;
+    T y = 0;
+    auto tick = [&](long tau, T xin) __attribute__((always_inline)) {
+        const T left = from_left(y);
+        const long j = tau - sec;
+        if (j >= 0 && j < L) {
+            y = bq.step(sec == 0 ? xin : left);
+            if (st) sp[j] = y;
+        }
+    };
+    long tau = 0;
+    for (; tau < pad; ++tau) tick(tau, ext(tau));
+    // body: section 0 reads x[tau - pad] (vector loads of CPV complex samples, double-buffered one
+    // batch ahead); section 3 emits j = tau - 3, aligned to VW because pad - 3 = 24.
+    using PV = typename std::conditional<CPV * 2 * sizeof(T) == 16, V,
+                                         typename std::conditional<sizeof(T) == 4, float2, double2>::type>::type;
+    constexpr int NL = SKB / CPV;              // input vectors per batch
+    PV xa[NL], xb[NL];
+    auto ld = [&](PV (&v)[NL], long t0) __attribute__((always_inline)) {
+        const PV *src = reinterpret_cast<const PV *>(xr + 2 * (t0 - pad));
 #pragma unroll
-    for (int i = 0; i < NSEC * 2; ++i) z[i] = zi[i] * y0;
+        for (int k = 0; k < NL; ++k) v[k] = src[k];
+    };
+    auto run = [&](PV (&v)[NL], long t0) __attribute__((always_inline)) {
+        T o[VW];
+#pragma unroll
+        for (int u = 0; u < SKB; ++u) {
+            const PV &pv = v[u / CPV];
+            const T xin = velt(pv, 2 * (u % CPV) + comp);
+            const T left = from_left(y);
+            y = bq.step(sec == 0 ? xin : left);   // all sections active: pad >= 3
+            o[u % VW] = y;
+            if (u % VW == VW - 1) {
+                V w;
+                if constexpr (VW == 4) w = V{o[0], o[1], o[2], o[3]};
+                else w = V{o[0], o[1]};
+                V *dst = st ? reinterpret_cast<V *>(sp + (t0 + u - 3 - (VW - 1))) : vsink;
+                *dst = w;
+            }
+        }
+    };
+    if (N >= 2 * SKB) {
+        ld(xa, tau);
+        ld(xb, tau + SKB);
+        for (; tau + 4 * SKB <= pad + N; tau += 2 * SKB) {
+            run(xa, tau);
+            __builtin_amdgcn_sched_barrier(0);
+            ld(xa, tau + 2 * SKB);
+            run(xb, tau + SKB);
+            __builtin_amdgcn_sched_barrier(0);
+            ld(xb, tau + 3 * SKB);
+        }
+        run(xa, tau);
+        run(xb, tau + SKB);
+        tau += 2 * SKB;
+    }
+    for (; tau < L + 3; ++tau) tick(tau, tau < L ? ext(tau) : T(0));
+}
+
+// Reverse pass (sosfiltfilt's second sosfilt over the time-reversed forward output), keeping
+// decimate's y[::q]: output t (= ext index t + pad) when t % q == 0.
+template <typename T>
+__global__ __launch_bounds__(64) void k_sos_bwd(const T *__restrict__ scr, long Lp, int C, long N, int pad, int q,
+                                                const T *__restrict__ sos, const T *__restrict__ zi,
+                                                T *__restrict__ out, Lay lo) {
+    using V = typename Vec16<T>::type;
+    constexpr int VW = Vec16<T>::n;
+    const int gid = blockIdx.x * 64 + threadIdx.x;
+    const int g = gid >> 2, sec = gid & 3;
+    const int ch = min(g >> 1, C - 1), comp = g & 1;
+    const bool own = (g >> 1) < C;
+    const T *sp = scr + (size_t)(2 * ch + comp) * Lp;
+    const long L = N + 2 * pad;
+    Biquad<T> bq = load_section(sos, zi, sec, sp[L - 1]);
     T *op = out + lo.off(ch, 0) + comp;
     const size_t so = lo.s_n;
-    long j = L - 1;
-    for (; j >= pad + N; --j) sos_step(c, z, sp[(size_t)j * ss]);
-    // output y[t] for t = j - pad with t % q == 0 (decimate's y[::q])
-    long t = N - 1;
-    int cnt = (int)(t % q);
-    for (; t >= 15; t -= 16, j -= 16) {   // 16 scratch loads ahead of the recursion
-        T ys[16];
+    const bool st = own && sec == 3;
+    T y = 0;
+    // tick tau: section 0 reads scr[L-1-tau]; section s works on ext index j = L-1-(tau-s)
+    auto tick = [&](long tau, T xin) __attribute__((always_inline)) {
+        const T left = from_left(y);
+        const long k = tau - sec;
+        if (k >= 0 && k < L) {
+            y = bq.step(sec == 0 ? xin : left);
+            const int t = (int)(L - 1 - k - pad);
+            if (st && t >= 0 && t < N && t % q == 0) op[(size_t)(t / q) * so] = y;
+        }
+    };
+    // body batches start where the first vector load is aligned: (L - tau) % VW == 0, tau >= 3
+    long tau0 = 3;
+    while ((L - tau0) % VW) ++tau0;
+    long tau = 0;
+    for (; tau < tau0; ++tau) tick(tau, sp[L - 1 - tau]);
+    constexpr int NL = SKB / VW;
+    V xa[NL], xb[NL];
+    auto ld = [&](V (&v)[NL], long t0) __attribute__((always_inline)) {
+        // ticks t0 .. t0+SKB-1 read j = L-1-t0 down to L-t0-SKB; vector k covers
+        // [L - t0 - (k+1) VW, L - t0 - k VW)
 #pragma unroll
-        for (int u = 0; u < 16; ++u) ys[u] = sp[(size_t)(j - u) * ss];
+        for (int k = 0; k < NL; ++k) v[k] = *reinterpret_cast<const V *>(sp + (L - t0 - (k + 1) * VW));
+    };
+    // The output lanes' index t = L-1-(tau-3)-pad falls by one per tick and is the same for every
+    // stream (equal lengths), so t / q and t % q are wave-uniform scalars: the decimating store is
+    // a scalar branch, not per-lane arithmetic.
+    int tc = 0, tq = 0, tr = 0;
+    auto run = [&](V (&v)[NL], long t0) __attribute__((always_inline)) {
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const T v = sos_step(c, z, ys[u]);
-            if (cnt == 0) {
-                op[(size_t)((t - u) / q) * so] = v;
-                cnt = q;
+        for (int u = 0; u < SKB; ++u) {
+            const T xin = velt(v[u / VW], VW - 1 - (u % VW));
+            const T left = from_left(y);
+            y = bq.step(sec == 0 ? xin : left);
+            if (tr == 0 && tc >= 0 && tc < N) {
+                if (st) op[(size_t)tq * so] = y;
             }
-            --cnt;
+            --tc;
+            if (--tr < 0) { tr = q - 1; --tq; }
         }
-    }
-    for (; t >= 0; --t, --j) {
-        T v = sos_step(c, z, sp[(size_t)j * ss]);
-        if (cnt == 0) {
-            op[(size_t)(t / q) * so] = v;
-            cnt = q;
+    };
+    if (L - tau >= 2 * SKB) {
+        tc = __builtin_amdgcn_readfirstlane((int)(L - 1 - (tau - 3) - pad));   // >= 0 here
+        tq = __builtin_amdgcn_readfirstlane(tc / q);
+        tr = __builtin_amdgcn_readfirstlane(tc % q);
+        ld(xa, tau);
+        ld(xb, tau + SKB);
+        for (; tau + 4 * SKB <= L; tau += 2 * SKB) {
+            run(xa, tau);
+            __builtin_amdgcn_sched_barrier(0);
+            ld(xa, tau + 2 * SKB);
+            run(xb, tau + SKB);
+            __builtin_amdgcn_sched_barrier(0);
+            ld(xb, tau + 3 * SKB);
         }
-        --cnt;
+        run(xa, tau);
+        run(xb, tau + SKB);
+        tau += 2 * SKB;
     }
-    for (; j >= 0; --j) sos_step(c, z, sp[(size_t)j * ss]);
+    for (; tau < L + 3; ++tau) tick(tau, tau < L ? sp[L - 1 - tau] : T(0));
 }
 
 // ------------------------------------------------------------------ mixer + filtfilt (lfilter)
@@ -451,25 +580,38 @@ long ceil_div(long a, long b) { return (a + b - 1) / b; }
 // ----------------------------------------------------------------- host-side stage drivers
 template <typename T>
 int run_decimate(tetra_ctx *ctx, const tetra_compat_plan *P, const T *x, Lay lx, int C, long N, T *out, Lay lo) {
+    (void)lx;   // input rows are complex [C][N] (row_major)
     const int pad = 27;   // 3 * (2*4 + 1): sosfiltfilt default padlen for 4 sections
     const long L = N + 2 * pad;
-    T *scr = (T *)ws(ctx, S_W0, grouped_elems(C, L) * sizeof(T));
+    const long Lp = (L + 3) & ~3L;   // stream-major scratch rows, 16-byte aligned
+    T *scr = (T *)ws(ctx, S_W0, (size_t)2 * C * Lp * sizeof(T));
     T *coef = (T *)ws(ctx, S_W7, 32 * sizeof(T));
-    if (!scr || !coef) return TETRA_E_NOMEM;
+    T *sink = (T *)ws(ctx, S_W4, (size_t)8 * C * 16 + 1024);
+    if (!scr || !coef || !sink) return TETRA_E_NOMEM;
     T hc[32];
     for (int i = 0; i < 24; ++i) hc[i] = std::is_same<T, float>::value ? (T)P->sos_f32[i] : (T)P->sos_f64[i];
     for (int i = 0; i < 8; ++i) hc[24 + i] = std::is_same<T, float>::value ? (T)P->zi_f32[i] : (T)P->zi_f64[i];
     HIP_TRY(ctx, hipMemcpyAsync(coef, hc, sizeof hc, hipMemcpyHostToDevice, ctx->stream));
     const unsigned blk = 64;
+    const dim3 grid(grid_for((size_t)8 * C, blk));
     {
         PROF(ctx, "compat_sos_fwd");
-        hipLaunchKernelGGL(k_sos_fwd<T>, dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, x, lx, C, N, pad,
-                       coef, coef + 24, scr, grouped(L));
+        bool two = false;
+        if constexpr (std::is_same<T, float>::value) {
+            if (N % 2 == 0) {   // complex64 rows 16-byte aligned: 2 samples per load
+                two = true;
+                hipLaunchKernelGGL((k_sos_fwd<T, 2>), grid, dim3(blk), 0, ctx->stream, x, C, N, pad, coef, coef + 24,
+                                   scr, Lp, sink);
+            }
+        }
+        if (!two)
+            hipLaunchKernelGGL((k_sos_fwd<T, 1>), grid, dim3(blk), 0, ctx->stream, x, C, N, pad, coef, coef + 24, scr,
+                               Lp, sink);
     }
     {
         PROF(ctx, "compat_sos_bwd");
-        hipLaunchKernelGGL(k_sos_bwd<T>, dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, scr, grouped(L), C,
-                       N, pad, P->q, coef, coef + 24, out, lo);
+        hipLaunchKernelGGL(k_sos_bwd<T>, grid, dim3(blk), 0, ctx->stream, scr, Lp, C, N, pad, P->q, coef, coef + 24,
+                           out, lo);
     }
     return TETRA_OK;
 }
