@@ -38,8 +38,8 @@ FS = 2.4e6
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--chain", choices=("etsi", "compat"), default=os.environ.get("TETRA_BENCH_CHAIN", "etsi"))
     ap.add_argument("--channels", type=int, default=8192, help="channels per rank")
     ap.add_argument("--samples", type=int, default=131072, help="samples per channel chunk")
