@@ -225,7 +225,8 @@ __global__ __launch_bounds__(64) void k_timing(const float2 *__restrict__ yall, 
 // The input tile is a linear float4 image (2 samples per entry, ds_write_b128 / ds_read_b128: a
 // 20-dword lane stride is conflict-free for b128's lane groups).  The stage-1 ring is polyphase:
 // x240[k] sits at [k % 10][k / 10], so stage 2's stride-10 reads are unit-stride across lanes.
-constexpr int RP = 224;         // row length of the stage-1 ring (10 x 224 = 2240 outputs kept)
+constexpr int RP = 229;         // row length of the stage-1 ring (10 x 229 = 2290 outputs kept; odd, so
+                                // the ten phase rows of one write fall in distinct LDS banks)
 constexpr int S2_EVERY = 8;     // stage 2 runs every 8 tiles: ~205 output triples, one per thread
 constexpr int TPP = 107;        // RRC taps per polyphase branch (Lp = 321 = 3 x 107)
 constexpr int PFD = 2;          // input tiles in flight per workgroup (register prefetch depth;
