@@ -262,6 +262,16 @@ __global__ __launch_bounds__(64) void k_sos_bwd(const T *__restrict__ scr, long 
 
 // ------------------------------------------------------------------ mixer + filtfilt (lfilter)
 // Value of component `comp` of (possibly frequency-shifted) sample n, in double.
+__device__ __forceinline__ double mix_pair(double xr, double xi, long n, int comp, bool mix, double c, double fs) {
+    if (!mix) return comp ? xi : xr;
+    // numpy: t = arange/fs; arg = (-1j*2*pi*f)*t has real part 0, imag c*t; exp(arg) = (cos, sin)
+    const double th = c * ((double)n / fs);
+    double s, co;
+    sincos(th, &s, &co);
+    // numpy SIMD complex multiply: re = fma(xr, sr, -(xi*si)), im = fma(xr, si, xi*sr)
+    return comp ? fma(xr, s, xi * co) : fma(xr, co, -(xi * s));
+}
+
 template <typename TIn>
 __device__ __forceinline__ double mixed_val(const TIn *xp, size_t sx, long n, int comp, bool mix, double c,
                                             double fs) {
@@ -300,85 +310,129 @@ __device__ __forceinline__ double lf_ext(const TIn *xp, size_t sx, long M, int p
 
 constexpr int MAXTAP = 8;
 
-template <typename TIn>
-__global__ __launch_bounds__(256) void k_lf_fwd(const TIn *__restrict__ x, Lay lx, int C, long M, int pad, int nt,
-                                                const double *__restrict__ b, const double *__restrict__ a,
-                                                const double *__restrict__ zi, const double *__restrict__ mixc,
-                                                const uint8_t *__restrict__ mixon, double fs,
-                                                double *__restrict__ scr, Lay ls) {
+// scipy lfilter (DF-II-T) with NT taps, one stream (channel x re|im) per lane, in double:
+//   y = z0 + b0*x;  z_k = (z_{k+1} + x*b_{k+1}) - y*a_{k+1};  z_{NT-2} = x*b_{NT-1} - y*a_{NT-1}
+template <int NT>
+struct Lfilt {
+    double bb[NT], aa[NT], z[NT - 1];
+    __device__ __forceinline__ void init(const double *b, const double *a, const double *zi, double x0) {
+#pragma unroll
+        for (int k = 0; k < NT; ++k) { bb[k] = b[k]; aa[k] = a[k]; }
+#pragma unroll
+        for (int k = 0; k < NT - 1; ++k) z[k] = zi[k] * x0;
+    }
+    __device__ __forceinline__ double step(double xn) {
+        const double yn = z[0] + bb[0] * xn;
+#pragma unroll
+        for (int k = 0; k < NT - 2; ++k) z[k] = (z[k + 1] + xn * bb[k + 1]) - yn * aa[k + 1];
+        z[NT - 2] = xn * bb[NT - 1] - yn * aa[NT - 1];
+        return yn;
+    }
+};
+
+constexpr int LFB = 16;   // samples per load batch; batches double-buffered
+
+// Forward pass over the odd extension (filtfilt padlen 3*NT) of the (optionally mixed) input.
+template <typename TIn, int NT>
+__global__ __launch_bounds__(64) void k_lf_fwd(const TIn *__restrict__ x, Lay lx, int C, long M, int pad,
+                                               const double *__restrict__ b, const double *__restrict__ a,
+                                               const double *__restrict__ zi, const double *__restrict__ mixc,
+                                               const uint8_t *__restrict__ mixon, double fs,
+                                               double *__restrict__ scr, Lay ls) {
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
     const int ch = gid >> 1, comp = gid & 1;
     if (ch >= C) return;
-    double bb[MAXTAP], aa[MAXTAP], z[MAXTAP];
-    for (int k = 0; k < nt; ++k) { bb[k] = b[k]; aa[k] = a[k]; }
     const bool mix = mixon && mixon[ch];
     const double c = mix ? mixc[ch] : 0.0;
     const TIn *xp = x + lx.off(ch, 0);
     const size_t sx = lx.s_n;
     const long L = M + 2 * pad;
-    const double e0 = lf_ext(xp, sx, M, pad, 0, comp, mix, c, fs);
-    for (int k = 0; k < nt - 1; ++k) z[k] = zi[k] * e0;
+    Lfilt<NT> f;
+    f.init(b, a, zi, lf_ext(xp, sx, M, pad, 0, comp, mix, c, fs));
     double *sp = scr + ls.off(ch, 0) + comp;
     const size_t ss = ls.s_n;
-    auto step = [&](long j, double xn) {
-        // scipy lfilter (DF-II-T): y = z0 + b0*x; z_k = (z_{k+1} + x*b_{k+1}) - y*a_{k+1}
-        const double yn = z[0] + bb[0] * xn;
-#pragma unroll
-        for (int k = 0; k < MAXTAP - 2; ++k)
-            if (k < nt - 2) z[k] = (z[k + 1] + xn * bb[k + 1]) - yn * aa[k + 1];
-        // last delay
-#pragma unroll
-        for (int k = 0; k < MAXTAP - 1; ++k)
-            if (k == nt - 2) z[k] = xn * bb[k + 1] - yn * aa[k + 1];
-        sp[(size_t)j * ss] = yn;
-    };
     long j = 0;
-    for (; j < pad; ++j) step(j, lf_ext(xp, sx, M, pad, j, comp, mix, c, fs));
-    for (; j + 16 <= pad + M; j += 16) {   // inputs (and mixer phases) computed ahead of the recursion
-        double xs[16];
+    for (; j < pad; ++j) sp[(size_t)j * ss] = f.step(lf_ext(xp, sx, M, pad, j, comp, mix, c, fs));
+    // body: a batch's 16 (re, im) loads issue together, one batch ahead of the recursion; the
+    // mixer (a divergent sincos branch) runs between load and recursion
+    using P2 = typename std::conditional<sizeof(TIn) == 4, float2, double2>::type;
+    const P2 *xq = reinterpret_cast<const P2 *>(xp);   // (re, im) of sample n at xq[n * sx / 2]
+    const size_t sq = sx / 2;
+    P2 ra[LFB], rb[LFB];
+    auto ld = [&](P2 (&r)[LFB], long j0) __attribute__((always_inline)) {
 #pragma unroll
-        for (int u = 0; u < 16; ++u) xs[u] = mixed_val(xp, sx, j + u - pad, comp, mix, c, fs);
+        for (int u = 0; u < LFB; ++u) r[u] = xq[(size_t)(j0 + u - pad) * sq];
+    };
+    auto run = [&](P2 (&r)[LFB], long j0) __attribute__((always_inline)) {
+        double xs[LFB];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) step(j + u, xs[u]);
+        for (int u = 0; u < LFB; ++u) xs[u] = mix_pair((double)r[u].x, (double)r[u].y, j0 + u - pad, comp, mix, c, fs);
+#pragma unroll
+        for (int u = 0; u < LFB; ++u) sp[(size_t)(j0 + u) * ss] = f.step(xs[u]);
+    };
+    if (M >= 2 * LFB) {
+        ld(ra, j);
+        ld(rb, j + LFB);
+        for (; j + 4 * LFB <= pad + M; j += 2 * LFB) {
+            run(ra, j);
+            __builtin_amdgcn_sched_barrier(0);
+            ld(ra, j + 2 * LFB);
+            run(rb, j + LFB);
+            __builtin_amdgcn_sched_barrier(0);
+            ld(rb, j + 3 * LFB);
+        }
+        run(ra, j);
+        run(rb, j + LFB);
+        j += 2 * LFB;
     }
-    for (; j < L; ++j) step(j, lf_ext(xp, sx, M, pad, j, comp, mix, c, fs));
+    for (; j < L; ++j) sp[(size_t)j * ss] = f.step(lf_ext(xp, sx, M, pad, j, comp, mix, c, fs));
 }
 
-__global__ __launch_bounds__(256) void k_lf_bwd(const double *__restrict__ scr, Lay ls, int C, long M, int pad, int nt,
-                                                const double *__restrict__ b, const double *__restrict__ a,
-                                                const double *__restrict__ zi, double *__restrict__ out, Lay lo) {
+// Reverse pass: y[t] = output at ext index t + pad, t in [0, M).
+template <int NT>
+__global__ __launch_bounds__(64) void k_lf_bwd(const double *__restrict__ scr, Lay ls, int C, long M, int pad,
+                                               const double *__restrict__ b, const double *__restrict__ a,
+                                               const double *__restrict__ zi, double *__restrict__ out, Lay lo) {
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
     const int ch = gid >> 1, comp = gid & 1;
     if (ch >= C) return;
-    double bb[MAXTAP], aa[MAXTAP], z[MAXTAP];
-    for (int k = 0; k < nt; ++k) { bb[k] = b[k]; aa[k] = a[k]; }
     const double *sp = scr + ls.off(ch, 0) + comp;
     const size_t ss = ls.s_n;
     const long L = M + 2 * pad;
-    const double y0 = sp[(size_t)(L - 1) * ss];
-    for (int k = 0; k < nt - 1; ++k) z[k] = zi[k] * y0;
+    Lfilt<NT> f;
+    f.init(b, a, zi, sp[(size_t)(L - 1) * ss]);
     double *op = out + lo.off(ch, 0) + comp;
     const size_t so = lo.s_n;
-    auto step = [&](long j, double xn) {
-        const double yn = z[0] + bb[0] * xn;
-#pragma unroll
-        for (int k = 0; k < MAXTAP - 2; ++k)
-            if (k < nt - 2) z[k] = (z[k + 1] + xn * bb[k + 1]) - yn * aa[k + 1];
-#pragma unroll
-        for (int k = 0; k < MAXTAP - 1; ++k)
-            if (k == nt - 2) z[k] = xn * bb[k + 1] - yn * aa[k + 1];
-        const long t = j - pad;
-        if (t >= 0 && t < M) op[(size_t)t * so] = yn;
-    };
     long j = L - 1;
-    for (; j >= 15; j -= 16) {   // 16 scratch loads ahead of the recursion
-        double xs[16];
+    for (; j >= pad + M; --j) f.step(sp[(size_t)j * ss]);   // end padding: no output
+    double xa[LFB], xb[LFB];
+    auto ld = [&](double (&v)[LFB], long j0) __attribute__((always_inline)) {
 #pragma unroll
-        for (int u = 0; u < 16; ++u) xs[u] = sp[(size_t)(j - u) * ss];
+        for (int u = 0; u < LFB; ++u) v[u] = sp[(size_t)(j0 - u) * ss];
+    };
+    auto run = [&](double (&v)[LFB], long j0) __attribute__((always_inline)) {
 #pragma unroll
-        for (int u = 0; u < 16; ++u) step(j - u, xs[u]);
+        for (int u = 0; u < LFB; ++u) op[(size_t)(j0 - u - pad) * so] = f.step(v[u]);
+    };
+    if (j - 2 * LFB + 1 >= pad) {
+        ld(xa, j);
+        ld(xb, j - LFB);
+        for (; j - 4 * LFB + 1 >= pad; j -= 2 * LFB) {
+            run(xa, j);
+            __builtin_amdgcn_sched_barrier(0);
+            ld(xa, j - 2 * LFB);
+            run(xb, j - LFB);
+            __builtin_amdgcn_sched_barrier(0);
+            ld(xb, j - 3 * LFB);
+        }
+        run(xa, j);
+        run(xb, j - LFB);
+        j -= 2 * LFB;
     }
-    for (; j >= 0; --j) step(j, sp[(size_t)j * ss]);
+    for (; j >= 0; --j) {
+        const double yn = f.step(sp[(size_t)j * ss]);
+        if (j >= pad) op[(size_t)(j - pad) * so] = yn;
+    }
 }
 
 // frequency_shift alone (component API, and the unfiltered-but-shifted process() path).
@@ -620,7 +674,7 @@ template <typename TIn>
 int run_filtfilt(tetra_ctx *ctx, const tetra_compat_plan *P, const TIn *x, Lay lx, int C, long M,
                  const double *mixc, const uint8_t *mixon, double *out, Lay lo) {
     const int nt = P->ntaps, pad = 3 * nt;
-    if (nt < 2 || nt > MAXTAP) return tetra_fail(ctx, TETRA_E_INVALID, "ntaps %d unsupported", nt);
+    if (nt != 5) return tetra_fail(ctx, TETRA_E_INVALID, "ntaps %d unsupported (butter(4) has 5)", nt);
     const long L = M + 2 * pad;
     double *scr = (double *)ws(ctx, S_W2, grouped_elems(C, L) * sizeof(double));
     double *coef = (double *)ws(ctx, S_W6, 3 * MAXTAP * sizeof(double));
@@ -632,13 +686,13 @@ int run_filtfilt(tetra_ctx *ctx, const tetra_compat_plan *P, const TIn *x, Lay l
     const unsigned blk = 64;
     {
         PROF(ctx, "compat_filtfilt_fwd");
-        hipLaunchKernelGGL(k_lf_fwd<TIn>, dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, x, lx, C, M, pad,
-                       nt, coef, coef + MAXTAP, coef + 2 * MAXTAP, mixc, mixon, P->fs_dec, scr, grouped(L));
+        hipLaunchKernelGGL((k_lf_fwd<TIn, 5>), dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, x, lx, C, M,
+                           pad, coef, coef + MAXTAP, coef + 2 * MAXTAP, mixc, mixon, P->fs_dec, scr, grouped(L));
     }
     {
         PROF(ctx, "compat_filtfilt_bwd");
-        hipLaunchKernelGGL(k_lf_bwd, dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, scr, grouped(L), C, M,
-                       pad, nt, coef, coef + MAXTAP, coef + 2 * MAXTAP, out, lo);
+        hipLaunchKernelGGL(k_lf_bwd<5>, dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, scr, grouped(L), C,
+                           M, pad, coef, coef + MAXTAP, coef + 2 * MAXTAP, out, lo);
     }
     return TETRA_OK;
 }
