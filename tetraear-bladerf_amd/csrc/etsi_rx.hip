@@ -568,36 +568,49 @@ __global__ __launch_bounds__(64 * SYNC_WAVES) void k_etsi_sync(const uint8_t *__
 }
 
 // --------------------------------------------------------------------------- E4 Viterbi
-// One LANE per coded block: descramble + deinterleave into an LDS row, then the 16-state trellis
-// with all path metrics in registers (no cross-lane traffic), survivors stored [step][job]
-// (coalesced across the wave), traceback with the CRC accumulated on the fly.
-constexpr int VROW = 436;   // LDS row per lane: 432 type-3 values, padded to 109 dwords (bank spread)
+// Two LANES per coded block: lane h of the pair holds path metrics of states 8h..8h+7 in registers.
+// New state n = 8h + m has predecessors n>>1 = 4h + (m>>1) (half 0) and (n>>1)|8 (half 1, same
+// local index), so each step the pair swaps four metrics (one DPP quad permute each).  The pair
+// gathers (descramble + deinterleave) into one shared LDS row; each lane writes its 8 decision
+// bits as one byte of the step's 16-bit survivor word ([step][job], coalesced); both lanes trace
+// back (same path) and lane 0 writes the block with the CRC accumulated on the fly.  32 blocks per
+// 64-lane workgroup keep LDS at 14 KB, so Viterbi workgroups fit beside the demod's on a CU.
+constexpr int VROW = 436;   // LDS row per block: 432 type-3 values, padded to 109 dwords (bank spread)
+
+__device__ __forceinline__ int32_t pair_swap(int32_t v) {   // value of the other lane of the pair
+    return __builtin_amdgcn_update_dpp(0, v, 0xB1 /* quad_perm [1,0,3,2] */, 0xf, 0xf, false);
+}
 
 template <int PAIRS>
-__device__ __forceinline__ void acs_pairs(int32_t (&pm)[16], const int8_t *row, uint16_t *sv, size_t sstride) {
+__device__ __forceinline__ void acs_pairs2(int32_t (&pm)[8], int h, const int8_t *row, uint8_t *sv, size_t sstride) {
     // rate-2/3 puncturing: step 2g sees mother outputs (g1, g2) = type-3 (3g, 3g+1); step 2g+1 sees
     // g1 = type-3 3g+2; the other mother outputs are erased.
     for (int g = 0; g < PAIRS; ++g) {
         const int32_t a = row[3 * g], b = row[3 * g + 1], c = row[3 * g + 2];
+        const int32_t be = h ? -b : b;   // d2 = h flips the g2 term
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-            int32_t nm[16];
+            int32_t X[4], Y[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int32_t r = pair_swap(h ? pm[i] : pm[4 + i]);
+                X[i] = h ? r : pm[i];        // half-0 metric of state 4h + i
+                Y[i] = h ? pm[4 + i] : r;    // half-1 metric of state 8 + 4h + i
+            }
             uint32_t bits = 0;
 #pragma unroll
-            for (int n = 0; n < 16; ++n) {
-                const int bb = n & 1, d0 = (n >> 1) & 1, d1 = (n >> 2) & 1, d2 = (n >> 3) & 1;
+            for (int m = 0; m < 8; ++m) {
+                const int bb = m & 1, d0 = (m >> 1) & 1, d1 = (m >> 2) & 1;
                 // branch metric for d3 = 0; d3 = 1 flips every generator output (negates it)
                 int32_t v;
-                if (half == 0) v = ((bb ^ d0) ? -a : a) + ((bb ^ d1 ^ d2) ? -b : b);
+                if (half == 0) v = ((bb ^ d0) ? -a : a) + ((bb ^ d1) ? -be : be);
                 else v = (bb ^ d0) ? -c : c;
-                const int32_t m0 = pm[n >> 1] + v, m1 = pm[(n >> 1) | 8] - v;
+                const int32_t m0 = X[m >> 1] + v, m1 = Y[m >> 1] - v;
                 const bool t1 = m1 > m0;
-                nm[n] = t1 ? m1 : m0;
-                bits |= (uint32_t)t1 << n;
+                pm[m] = t1 ? m1 : m0;
+                bits |= (uint32_t)t1 << m;
             }
-#pragma unroll
-            for (int n = 0; n < 16; ++n) pm[n] = nm[n];
-            sv[(size_t)(2 * g + half) * sstride] = (uint16_t)bits;
+            sv[(size_t)(2 * g + half) * sstride] = (uint8_t)bits;
         }
     }
 }
@@ -609,18 +622,18 @@ __device__ __forceinline__ void viterbi_wave(int8_t *rows, const Job *__restrict
                                              const uint8_t *__restrict__ bsch_scr, uint16_t *__restrict__ surv,
                                              int32_t *__restrict__ blocks, uint8_t *__restrict__ type1) {
     constexpr KindP P = kind_params(KIND);
-    const int lane = threadIdx.x;
-    const int jl = lb * 64 + lane;
-    if (lb * 64 >= nj) return;   // whole wave past this kind's job count
+    const int lane = threadIdx.x, jw = lane >> 1, h = lane & 1;
+    const int jl = lb * 32 + jw;
+    if (lb * 32 >= nj) return;   // whole wave past this kind's job count
     const bool act = jl < nj;
     const size_t j = jbase + jl;
     const Job jb = act ? jobs[j] : Job{0, 0, 0, 0, KIND, 0};
-    int8_t *row = rows + lane * VROW;
-    if (act) {
+    int8_t *row = rows + jw * VROW;
+    if (act) {   // the pair splits the gather: lane h takes 8-position blocks 2q + h
         const int8_t *sb = softbits + (size_t)jb.ch * 2 * smax + jb.off;
         const uint8_t *scr = KIND == 2 ? bsch_scr : cell_scr + (size_t)jb.ch * 432;
-        int r = 0;   // a*i mod K, incrementally
-        for (int i0 = 1; i0 <= P.K; i0 += 8) {   // K is a multiple of 8: gathers issued 8 ahead
+        for (int i0 = 1 + 8 * h; i0 <= P.K; i0 += 16) {
+            int r = (int)(((long)P.a * (i0 - 1)) % P.K);   // a*i mod K, incrementally below
             int kk[8];
             int8_t v[8];
             uint8_t sc[8];
@@ -640,12 +653,14 @@ __device__ __forceinline__ void viterbi_wave(int8_t *rows, const Job *__restrict
             for (int u = 0; u < 8; ++u) row[i0 - 1 + u] = sc[u] ? (int8_t)(-v[u]) : v[u];
         }
     }
-    int32_t pm[16];
+    __syncthreads();   // the pair's row (one wave per workgroup)
+    int32_t pm[8];
 #pragma unroll
-    for (int n = 0; n < 16; ++n) pm[n] = n == 0 ? 0 : -(1 << 28);
+    for (int m = 0; m < 8; ++m) pm[m] = (h == 0 && m == 0) ? 0 : -(1 << 28);
     uint16_t *sv = surv + j;
     if (act) {
-        acs_pairs<P.n2 / 2>(pm, row, sv, ss);
+        acs_pairs2<P.n2 / 2>(pm, h, row, reinterpret_cast<uint8_t *>(sv) + h, 2 * ss);
+        __threadfence_block();   // the partner's survivor bytes are read below
         // traceback from state 0 (tail bits), CRC over type-1 + CRC bits on the fly
         constexpr int L = P.n1 + 16;
         uint32_t c = CRC_TAB.init[L];
@@ -659,29 +674,32 @@ __device__ __forceinline__ void viterbi_wave(int8_t *rows, const Job *__restrict
             for (int u = 0; u < 8; ++u) {
                 const int t = t0 - u;
                 const int bit = s2 & 1;
-                if (t < P.n1) op[t] = (uint8_t)bit;
+                if (h == 0 && t < P.n1) op[t] = (uint8_t)bit;
                 if (bit && t < L) c ^= CRC_TAB.t[L - 1 - t];
                 s2 = (s2 >> 1) | ((int)((w[u] >> s2) & 1u) << 3);
             }
         }
-        int32_t *bm = blocks + ((size_t)jb.ch * ETSI_MAXJ + jb.slot) * 4;
-        bm[0] = KIND;
-        bm[1] = c == 0x1D0Fu;
-        bm[2] = jb.burst;
-        bm[3] = jb.blk;
+        if (h == 0) {
+            int32_t *bm = blocks + ((size_t)jb.ch * ETSI_MAXJ + jb.slot) * 4;
+            bm[0] = KIND;
+            bm[1] = c == 0x1D0Fu;
+            bm[2] = jb.burst;
+            bm[3] = jb.blk;
+        }
     }
 }
 
 // Grid: the SCH/F region's waves, then SCH/HD's, then BSCH's (one trellis length per wave).
 __global__ __launch_bounds__(64) void k_etsi_viterbi(const Job *__restrict__ jobs,
-                                                     const unsigned long long *__restrict__ jcount, int C, const int8_t *__restrict__ softbits, int smax,
+                                                     const unsigned long long *__restrict__ jcount, int C,
+                                                     const int8_t *__restrict__ softbits, int smax,
                                                      const uint8_t *__restrict__ cell_scr,
                                                      const uint8_t *__restrict__ bsch_scr,
                                                      uint16_t *__restrict__ surv, int32_t *__restrict__ blocks,
                                                      uint8_t *__restrict__ type1) {
-    __shared__ __attribute__((aligned(16))) int8_t rows[64 * VROW];
+    __shared__ __attribute__((aligned(16))) int8_t rows[32 * VROW];
     const int b = blockIdx.x;
-    const int nb0 = (int)((job_cap(0, C) + 63) / 64), nb1 = (int)((job_cap(1, C) + 63) / 64);
+    const int nb0 = (int)((job_cap(0, C) + 31) / 32), nb1 = (int)((job_cap(1, C) + 31) / 32);
     const size_t ss = 32 * (size_t)C;
     const unsigned long long cnt = *jcount;
     const int n0 = (int)(cnt & 0x1FFFFFull), n1 = (int)((cnt >> 21) & 0x1FFFFFull), n2 = (int)(cnt >> 42);
@@ -1020,7 +1038,7 @@ int tetra_lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard,
     }
     {
         PROF(ctx, "etsi_viterbi");
-        const unsigned nblk = (unsigned)((job_cap(0, C) + 63) / 64 + (job_cap(1, C) + 63) / 64 + (job_cap(2, C) + 63) / 64);
+        const unsigned nblk = (unsigned)((job_cap(0, C) + 31) / 32 + (job_cap(1, C) + 31) / 32 + (job_cap(2, C) + 31) / 32);
         hipLaunchKernelGGL(k_etsi_viterbi, dim3(nblk), dim3(64), 0, ctx->stream, jobs, jcount, (int)C, sb, (int)smax,
                            cells, cells + ctx->cells * 432, surv, ko, to);
     }
