@@ -195,3 +195,21 @@ def test_sc16_ingest_matches_cf32(synth_small):
     d = rx.demod_batch(x[:2, :9001])
     for u, v in zip(c, d):
         assert np.array_equal(u, v)
+
+
+@pytest.mark.parametrize("N", [262144, 20000, 9001, 3000])
+def test_demod_lengths_vs_oracle(N):
+    """Chunk lengths around the kernel's structure: longer than the fused path's LDS output buffer
+    (component path), short, odd (trimmed to even like demod_batch does), and barely long enough."""
+    from tetraear.signal.etsi import synth, EtsiReceiver
+    C = 3
+    iq = synth(C, 262144, seed=9, snr_db=20.0)[0][:, :N]
+    rx = E.Receiver()
+    hard, soft, sym, ns = EtsiReceiver().demod_batch(iq)
+    Ne = N - N % 2
+    for ch in range(C):
+        so, sbo, ho, _ = rx.demod(iq[ch, :Ne])
+        n = int(ns[ch])
+        assert n == len(so), (N, ch)
+        assert np.array_equal(sym[ch, :n], so) and np.array_equal(hard[ch, :max(n - 1, 0)], ho)
+        assert np.array_equal(soft[ch, :2 * max(n - 1, 0)], sbo)
