@@ -568,44 +568,49 @@ __global__ __launch_bounds__(64 * SYNC_WAVES) void k_etsi_sync(const uint8_t *__
 }
 
 // --------------------------------------------------------------------------- E4 Viterbi
-// Two LANES per coded block: lane h of the pair holds path metrics of states 8h..8h+7 in registers.
-// New state n = 8h + m has predecessors n>>1 = 4h + (m>>1) (half 0) and (n>>1)|8 (half 1, same
-// local index), so each step the pair swaps four metrics (one DPP quad permute each).  The pair
-// gathers (descramble + deinterleave) into one shared LDS row; each lane writes its 8 decision
-// bits as one byte of the step's 16-bit survivor word ([step][job], coalesced); both lanes trace
-// back (same path) and lane 0 writes the block with the CRC accumulated on the fly.  32 blocks per
-// 64-lane workgroup keep LDS at 14 KB, so Viterbi workgroups fit beside the demod's on a CU.
+// Four LANES per coded block (one DPP quad): lane q holds the path metrics of states 4q..4q+3.
+// New state n = 4q + m has predecessors p = n>>1 = 2q + (m>>1), in lane q>>1 at local index
+// 2(q&1) + (m>>1), and p|8, in lane 2 + (q>>1) at the same index: each step a lane reads the four
+// metrics of both source lanes with quad-permute DPP and keeps the pair it needs.  The quad gathers
+// (descramble + deinterleave) into one shared LDS row; each lane stores its 4 decision bits as one
+// byte of the step's 32-bit survivor word ([step][job], coalesced); all four lanes trace back (same
+// path) and lane 0 writes the block with the CRC accumulated on the fly.  16 blocks per 64-lane
+// workgroup keep LDS at 7 KB, so Viterbi workgroups fit beside the demod's on a CU.
 constexpr int VROW = 436;   // LDS row per block: 432 type-3 values, padded to 109 dwords (bank spread)
 
-__device__ __forceinline__ int32_t pair_swap(int32_t v) {   // value of the other lane of the pair
-    return __builtin_amdgcn_update_dpp(0, v, 0xB1 /* quad_perm [1,0,3,2] */, 0xf, 0xf, false);
+template <int CTRL>
+__device__ __forceinline__ int32_t quad_perm(int32_t v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
 }
 
 template <int PAIRS>
-__device__ __forceinline__ void acs_pairs2(int32_t (&pm)[8], int h, const int8_t *row, uint8_t *sv, size_t sstride) {
+__device__ __forceinline__ void acs_pairs4(int32_t (&pm)[4], int q, const int8_t *row, uint8_t *sv, size_t sstride) {
     // rate-2/3 puncturing: step 2g sees mother outputs (g1, g2) = type-3 (3g, 3g+1); step 2g+1 sees
     // g1 = type-3 3g+2; the other mother outputs are erased.
+    const bool odd = q & 1;
+    const bool flip = ((q ^ (q >> 1)) & 1) != 0;   // d1 ^ d2 of this lane's states
     for (int g = 0; g < PAIRS; ++g) {
         const int32_t a = row[3 * g], b = row[3 * g + 1], c = row[3 * g + 2];
-        const int32_t be = h ? -b : b;   // d2 = h flips the g2 term
+        const int32_t be = flip ? -b : b;
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-            int32_t X[4], Y[4];
+            int32_t A[4], B[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int32_t r = pair_swap(h ? pm[i] : pm[4 + i]);
-                X[i] = h ? r : pm[i];        // half-0 metric of state 4h + i
-                Y[i] = h ? pm[4 + i] : r;    // half-1 metric of state 8 + 4h + i
+                A[i] = quad_perm<0x50 /* [0,0,1,1] */>(pm[i]);   // lane q>>1
+                B[i] = quad_perm<0xFA /* [2,2,3,3] */>(pm[i]);   // lane 2 + (q>>1)
             }
+            const int32_t X0 = odd ? A[2] : A[0], X1 = odd ? A[3] : A[1];
+            const int32_t Y0 = odd ? B[2] : B[0], Y1 = odd ? B[3] : B[1];
             uint32_t bits = 0;
 #pragma unroll
-            for (int m = 0; m < 8; ++m) {
-                const int bb = m & 1, d0 = (m >> 1) & 1, d1 = (m >> 2) & 1;
+            for (int m = 0; m < 4; ++m) {
+                const int bb = m & 1, d0 = (m >> 1) & 1;
                 // branch metric for d3 = 0; d3 = 1 flips every generator output (negates it)
                 int32_t v;
-                if (half == 0) v = ((bb ^ d0) ? -a : a) + ((bb ^ d1) ? -be : be);
+                if (half == 0) v = ((bb ^ d0) ? -a : a) + (bb ? -be : be);
                 else v = (bb ^ d0) ? -c : c;
-                const int32_t m0 = X[m >> 1] + v, m1 = Y[m >> 1] - v;
+                const int32_t m0 = ((m >> 1) ? X1 : X0) + v, m1 = ((m >> 1) ? Y1 : Y0) - v;
                 const bool t1 = m1 > m0;
                 pm[m] = t1 ? m1 : m0;
                 bits |= (uint32_t)t1 << m;
@@ -619,20 +624,20 @@ template <int KIND>
 __device__ __forceinline__ void viterbi_wave(int8_t *rows, const Job *__restrict__ jobs, int nj, size_t jbase, int lb,
                                              size_t ss, const int8_t *__restrict__ softbits, int smax,
                                              const uint8_t *__restrict__ cell_scr,
-                                             const uint8_t *__restrict__ bsch_scr, uint16_t *__restrict__ surv,
+                                             const uint8_t *__restrict__ bsch_scr, uint32_t *__restrict__ surv,
                                              int32_t *__restrict__ blocks, uint8_t *__restrict__ type1) {
     constexpr KindP P = kind_params(KIND);
-    const int lane = threadIdx.x, jw = lane >> 1, h = lane & 1;
-    const int jl = lb * 32 + jw;
-    if (lb * 32 >= nj) return;   // whole wave past this kind's job count
+    const int lane = threadIdx.x, jw = lane >> 2, q = lane & 3;
+    const int jl = lb * 16 + jw;
+    if (lb * 16 >= nj) return;   // whole wave past this kind's job count
     const bool act = jl < nj;
     const size_t j = jbase + jl;
     const Job jb = act ? jobs[j] : Job{0, 0, 0, 0, KIND, 0};
     int8_t *row = rows + jw * VROW;
-    if (act) {   // the pair splits the gather: lane h takes 8-position blocks 2q + h
+    if (act) {   // the quad splits the gather: lane q takes 8-position blocks 4k + q
         const int8_t *sb = softbits + (size_t)jb.ch * 2 * smax + jb.off;
         const uint8_t *scr = KIND == 2 ? bsch_scr : cell_scr + (size_t)jb.ch * 432;
-        for (int i0 = 1 + 8 * h; i0 <= P.K; i0 += 16) {
+        for (int i0 = 1 + 8 * q; i0 <= P.K; i0 += 32) {
             int r = (int)(((long)P.a * (i0 - 1)) % P.K);   // a*i mod K, incrementally below
             int kk[8];
             int8_t v[8];
@@ -653,14 +658,14 @@ __device__ __forceinline__ void viterbi_wave(int8_t *rows, const Job *__restrict
             for (int u = 0; u < 8; ++u) row[i0 - 1 + u] = sc[u] ? (int8_t)(-v[u]) : v[u];
         }
     }
-    __syncthreads();   // the pair's row (one wave per workgroup)
-    int32_t pm[8];
+    __syncthreads();   // the quad's row (one wave per workgroup)
+    int32_t pm[4];
 #pragma unroll
-    for (int m = 0; m < 8; ++m) pm[m] = (h == 0 && m == 0) ? 0 : -(1 << 28);
-    uint16_t *sv = surv + j;
+    for (int m = 0; m < 4; ++m) pm[m] = (q == 0 && m == 0) ? 0 : -(1 << 28);
+    uint32_t *sv = surv + j;
     if (act) {
-        acs_pairs2<P.n2 / 2>(pm, h, row, reinterpret_cast<uint8_t *>(sv) + h, 2 * ss);
-        __threadfence_block();   // the partner's survivor bytes are read below
+        acs_pairs4<P.n2 / 2>(pm, q, row, reinterpret_cast<uint8_t *>(sv) + q, 4 * ss);
+        __threadfence_block();   // the other lanes' survivor bytes are read below
         // traceback from state 0 (tail bits), CRC over type-1 + CRC bits on the fly
         constexpr int L = P.n1 + 16;
         uint32_t c = CRC_TAB.init[L];
@@ -674,12 +679,13 @@ __device__ __forceinline__ void viterbi_wave(int8_t *rows, const Job *__restrict
             for (int u = 0; u < 8; ++u) {
                 const int t = t0 - u;
                 const int bit = s2 & 1;
-                if (h == 0 && t < P.n1) op[t] = (uint8_t)bit;
+                if (q == 0 && t < P.n1) op[t] = (uint8_t)bit;
                 if (bit && t < L) c ^= CRC_TAB.t[L - 1 - t];
-                s2 = (s2 >> 1) | ((int)((w[u] >> s2) & 1u) << 3);
+                // state s2's decision: byte s2 >> 2 (lane), bit s2 & 3
+                s2 = (s2 >> 1) | ((int)((w[u] >> (8 * (s2 >> 2) + (s2 & 3))) & 1u) << 3);
             }
         }
-        if (h == 0) {
+        if (q == 0) {
             int32_t *bm = blocks + ((size_t)jb.ch * ETSI_MAXJ + jb.slot) * 4;
             bm[0] = KIND;
             bm[1] = c == 0x1D0Fu;
@@ -695,11 +701,11 @@ __global__ __launch_bounds__(64) void k_etsi_viterbi(const Job *__restrict__ job
                                                      const int8_t *__restrict__ softbits, int smax,
                                                      const uint8_t *__restrict__ cell_scr,
                                                      const uint8_t *__restrict__ bsch_scr,
-                                                     uint16_t *__restrict__ surv, int32_t *__restrict__ blocks,
+                                                     uint32_t *__restrict__ surv, int32_t *__restrict__ blocks,
                                                      uint8_t *__restrict__ type1) {
-    __shared__ __attribute__((aligned(16))) int8_t rows[32 * VROW];
+    __shared__ __attribute__((aligned(16))) int8_t rows[16 * VROW];
     const int b = blockIdx.x;
-    const int nb0 = (int)((job_cap(0, C) + 31) / 32), nb1 = (int)((job_cap(1, C) + 31) / 32);
+    const int nb0 = (int)((job_cap(0, C) + 15) / 16), nb1 = (int)((job_cap(1, C) + 15) / 16);
     const size_t ss = 32 * (size_t)C;
     const unsigned long long cnt = *jcount;
     const int n0 = (int)(cnt & 0x1FFFFFull), n1 = (int)((cnt >> 21) & 0x1FFFFFull), n2 = (int)(cnt >> 42);
@@ -1023,12 +1029,12 @@ int tetra_lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard,
     int32_t *ko = (int32_t *)st.out(blocks, C * ETSI_MAXJ * 4 * 4);
     uint8_t *to = (uint8_t *)st.out(type1, C * ETSI_MAXJ * 268);
     const size_t jtot = 32 * C;   // the three job regions (job_base / job_cap)
-    // workspace: [job counters per kind (16 B)] [jobs] [survivors: 288 steps x jtot]
-    char *w = (char *)ws(ctx, S_W7, 16 + jtot * sizeof(Job) + 288 * jtot * 2);
+    // workspace: [job counters per kind (16 B)] [jobs] [survivors: 288 steps x jtot x 32 bits]
+    char *w = (char *)ws(ctx, S_W7, 16 + jtot * sizeof(Job) + 288 * jtot * 4);
     if (!sb || !hd || !ns || !nbo || !bo || !nko || !ko || !to || !w) return st.finish();
     unsigned long long *jcount = (unsigned long long *)w;
     Job *jobs = (Job *)(w + 16);
-    uint16_t *surv = (uint16_t *)(w + 16 + jtot * sizeof(Job));
+    uint32_t *surv = (uint32_t *)(w + 16 + jtot * sizeof(Job));
     const uint8_t *cells = (const uint8_t *)ctx->slot[S_W5].p;
     {
         PROF(ctx, "etsi_sync");
@@ -1038,7 +1044,7 @@ int tetra_lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard,
     }
     {
         PROF(ctx, "etsi_viterbi");
-        const unsigned nblk = (unsigned)((job_cap(0, C) + 31) / 32 + (job_cap(1, C) + 31) / 32 + (job_cap(2, C) + 31) / 32);
+        const unsigned nblk = (unsigned)((job_cap(0, C) + 15) / 16 + (job_cap(1, C) + 15) / 16 + (job_cap(2, C) + 15) / 16);
         hipLaunchKernelGGL(k_etsi_viterbi, dim3(nblk), dim3(64), 0, ctx->stream, jobs, jcount, (int)C, sb, (int)smax,
                            cells, cells + ctx->cells * 432, surv, ko, to);
     }
