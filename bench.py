@@ -47,8 +47,11 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--iq", choices=("cf32", "sc16"), default="cf32",
                     help="etsi: input sample format in HBM (sc16 = the BladeRF wire format, 4 B/sample)")
-    ap.add_argument("--no-pipeline", action="store_true",
-                    help="etsi: run the whole chain on one stream (no front/back-end overlap across batches)")
+    ap.add_argument("--pipeline", choices=("auto", "on", "off"), default="auto",
+                    help="etsi: overlap the demod of batch k+1 with the lower MAC of batch k on two streams "
+                         "(auto: cf32 on; sc16 off -- its demod fills every CU's LDS, so the back-end "
+                         "kernels cannot co-reside and only slow it down)")
+    ap.add_argument("--no-pipeline", action="store_true", help="same as --pipeline off")
     return ap.parse_args()
 
 
@@ -168,7 +171,8 @@ def main():
     if a.chain == "etsi":
         from tetraear.signal.etsi import BenchStep as EtsiStep
         step = EtsiStep(c, C, N, FS, seed=rank_seed(1000, rank), device=dev, iq_format=a.iq)
-        if not a.no_pipeline:
+        pipe = "off" if a.no_pipeline else a.pipeline
+        if pipe == "on" or (pipe == "auto" and a.iq == "cf32"):
             step.pipeline()
     else:
         g = torch.Generator(device=dev)

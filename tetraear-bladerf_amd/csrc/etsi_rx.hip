@@ -225,14 +225,17 @@ __global__ __launch_bounds__(64) void k_timing(const float2 *__restrict__ yall, 
 // The input tile is a linear float4 image (2 samples per entry, ds_write_b128 / ds_read_b128: a
 // 20-dword lane stride is conflict-free for b128's lane groups).  The stage-1 ring is polyphase:
 // x240[k] sits at [k % 10][k / 10], so stage 2's stride-10 reads are unit-stride across lanes.
-constexpr int RP = 229;         // row length of the stage-1 ring (10 x 229 = 2290 outputs kept; odd, so
+constexpr int RP = 231;         // row length of the stage-1 ring (10 x 231 = 2310 outputs kept; odd, so
                                 // the ten phase rows of one write fall in distinct LDS banks)
 constexpr int S2_EVERY = 8;     // stage 2 runs every 8 tiles: ~205 output triples, one per thread
 constexpr int TPP = 107;        // RRC taps per polyphase branch (Lp = 321 = 3 x 107)
-constexpr int PFD = 2;          // input tiles in flight per workgroup (register prefetch depth;
-                                // 3 measured no faster)
-constexpr int YLDS = 4096;        // stage-2 outputs held in LDS before a flush (a 131072-sample chunk
-                                // has 3932)
+constexpr int PFD = 2;          // input tiles in flight per workgroup (register prefetch depth, pa/pb;
+                                // 3 and 4 measured no faster)
+constexpr int YLDS = 4096;      // cf32: stage-2 outputs held in LDS before a flush (a 131072-sample
+                                // chunk has 3932)
+constexpr int XIN4 = (HALO + TILE_IN) / 2;        // float4 entries of the input image
+constexpr int CF_LDS4 = XIN4 + (10 * RP + 1) / 2; // image + ring, in float4 (39,344 B)
+constexpr int CF_LDS2 = 2 * CF_LDS4;              // the same in float2 (SC16 fused: y + timing scratch)
 constexpr int HQ = 120;         // row of the per-branch tap table, indexed by r = j + off_c
 
 // Packed fp32 (v_pk_fma_f32): one real tap times a complex sample, each half a correctly rounded
@@ -270,17 +273,23 @@ template <typename In, bool FUSE>
 __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, long N, int M1, int M2,
                                                   const float *__restrict__ h1, const float *__restrict__ hq,
                                                   float2 *__restrict__ y, TimingOut to) {
-    __shared__ float4 xin[(HALO + TILE_IN) / 2];
-    __shared__ float2 ring[10 * RP];
-    // Stage-2 outputs collect in LDS and go out in one coalesced burst when the channel is done
-    // (or when YLDS fills): stores interleaved with the input stream cost ~0.3 ms per 8192-channel
-    // batch (HBM read/write turnarounds, and store acks inside the prefetch's in-order vmcnt).
-    __shared__ pf2 yb[YLDS];
+    // cf32 keeps y in LDS (yb, 71 KB: two workgroups per CU, no y traffic); SC16 streams half the
+    // bytes per sample and is bound by the workgroup's own LDS/issue chain instead, so it keeps
+    // only the image and the ring (39 KB: four workgroups per CU) and sends y through HBM/L2
+    constexpr bool YL = std::is_same<In, float4>::value;
+    __shared__ float4 lds[YL ? CF_LDS4 + YLDS / 2 : CF_LDS4];
+    float4 *xin = lds;
+    float2 *ring = reinterpret_cast<float2 *>(lds + XIN4);
+    pf2 *yb = reinterpret_cast<pf2 *>(lds + CF_LDS4);   // YL only
     const int ch = blockIdx.x;
     const int tid = threadIdx.x;
     const In *xp = iq + (size_t)ch * (N / 2);   // N even: 2 complex samples per load
-    float2 *yp = FUSE ? nullptr : y + (size_t)ch * M2;
+    float2 *yp = y + (size_t)ch * M2;           // (YL && FUSE: unused)
     int ybase = 0;   // y index of yb[0]
+    // Stage-2 outputs collect in yb and go out in one coalesced burst when the channel is done (or
+    // when YLDS fills): stores interleaved with the input stream cost ~0.3 ms per 8192-channel
+    // batch at two workgroups per CU (HBM read/write turnarounds, and store acks inside the
+    // prefetch's in-order vmcnt).
     auto flush = [&](int mend) {
         for (int i = tid; i < mend - ybase; i += 256) yp[ybase + i] = make_float2(yb[i].x, yb[i].y);
         ybase = mend;
@@ -337,34 +346,73 @@ __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, lon
             const int m_hi = num >= 0 ? min(num / 10, M2 - 1) : -1;
             const int u_hi = last ? (M2 - 1) / 3 : (m_hi >= 2 ? (m_hi - 2) / 3 : -1);
             for (int u0 = u_done; u0 <= u_hi; u0 += 256) {
-                if (min(3 * min(u0 + 256, u_hi + 1), M2) - ybase > YLDS) {   // chunk would not fit
+                if (YL && min(3 * min(u0 + 256, u_hi + 1), M2) - ybase > YLDS) {   // chunk would not fit
                     flush(3 * u0);
                     __syncthreads();
                 }
                 const int u = u0 + tid;
                 if (u <= u_hi) {
-                    // r-major over the 114 stage-1 inputs of the triple; each branch's zero-padded
-                    // taps leave its accumulation order exactly that of the oracle (kk ascending)
+                    // r-major over the 114 stage-1 inputs of the triple, rows loaded one block of
+                    // ten ahead of the FMAs (two register sets).  Taps outside a branch's 107 are
+                    // skipped where r is known at compile time (q = 0, q = 10 and the tail), so
+                    // each branch accumulates exactly its own taps in the oracle's order (kk
+                    // ascending); the zero entries left in the middle blocks do not exist.
                     pf2 a0 = {0.f, 0.f}, a1 = {0.f, 0.f}, a2 = {0.f, 0.f};
-                    auto tap = [&](int r, float2 v) {
-                        const pf2 x = {v.x, v.y};
-                        a0 = pfma(hq[r], x, a0);
-                        a1 = pfma(hq[HQ + r], x, a1);
-                        a2 = pfma(hq[2 * HQ + r], x, a2);
-                    };
-#pragma unroll 1
-                    for (int q = 0; q < 11; ++q) {
+                    auto ld = [&](float2 (&v)[10], int q, int n) __attribute__((always_inline)) {
                         const int row = (u + q) % RP;
 #pragma unroll
-                        for (int p = 0; p < 10; ++p) tap(10 * q + p, ring[p * RP + row]);
-                    }
-                    const int row = (u + 11) % RP;
+                        for (int p = 0; p < 10; ++p)
+                            if (p < n) v[p] = ring[p * RP + row];
+                    };
+                    // taps of block q; lo/hi: compile-time r window of each branch (r = 10q + p)
+                    auto blk = [&](const float2 (&v)[10], int q, int n, int lo1, int lo2, int hi0, int hi1)
+                        __attribute__((always_inline)) {
 #pragma unroll
-                    for (int p = 0; p < 4; ++p) tap(110 + p, ring[p * RP + row]);
+                        for (int p = 0; p < 10; ++p) {
+                            if (p >= n) continue;
+                            const pf2 x = {v[p].x, v[p].y};
+                            const int r = 10 * q + p;
+                            if (p <= hi0) a0 = pfma(hq[r], x, a0);
+                            if (p >= lo1 && p <= hi1) a1 = pfma(hq[HQ + r], x, a1);
+                            if (p >= lo2) a2 = pfma(hq[2 * HQ + r], x, a2);
+                        }
+                    };
+                    float2 v0[10], v1[10];
+                    ld(v0, 0, 10);
+                    ld(v1, 1, 10);
+                    blk(v0, 0, 10, 4, 7, 9, 9);   // branch 1 starts at r = 4, branch 2 at r = 7
+                    ld(v0, 2, 10);
+#pragma unroll 1
+                    for (int q = 1; q < 9; q += 2) {   // blocks 1..8
+                        blk(v1, q, 10, 0, 0, 9, 9);
+                        ld(v1, q + 2, 10);
+                        blk(v0, q + 1, 10, 0, 0, 9, 9);
+                        ld(v0, q + 3, 10);
+                    }
+                    blk(v1, 9, 10, 0, 0, 9, 9);
+                    ld(v1, 11, 4);
+                    blk(v0, 10, 10, 0, 0, 6, 9);   // branch 0 ends at r = 106
+                    blk(v1, 11, 4, 0, 0, -1, 0);   // r = 110..113: branch 1 ends at r = 110
                     const int m = 3 * u;
-                    if (m < M2) yb[m - ybase] = a0;
-                    if (m + 1 < M2) yb[m + 1 - ybase] = a1;
-                    if (m + 2 < M2) yb[m + 2 - ybase] = a2;
+                    if constexpr (YL) {
+                        if (m < M2) yb[m - ybase] = a0;
+                        if (m + 1 < M2) yb[m + 1 - ybase] = a1;
+                        if (m + 2 < M2) yb[m + 2 - ybase] = a2;
+                    } else {
+                        // staged in the consumed part of the image (past the halo), stored below
+                        pf2 *xs = reinterpret_cast<pf2 *>(xin + HALO / 2) + 3 * tid;
+                        xs[0] = a0;
+                        xs[1] = a1;
+                        xs[2] = a2;
+                    }
+                }
+                if constexpr (!YL) {
+                    // coalesced store of this chunk's outputs y[3 u0, 3 u0 + n)
+                    __syncthreads();
+                    const int n = min(3 * min(u0 + 256, u_hi + 1), M2) - 3 * u0;
+                    const pf2 *xs = reinterpret_cast<const pf2 *>(xin + HALO / 2);
+                    for (int i = tid; i < n; i += 256) yp[3 * u0 + i] = make_float2(xs[i].x, xs[i].y);
+                    if (u0 + 256 <= u_hi) __syncthreads();
                 }
             }
             if (u_hi + 1 > u_done) u_done = u_hi + 1;
@@ -381,15 +429,35 @@ __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, lon
         tile(t + 1, pb);
     }
     if (t < ntile) tile(t, pa);
-    // the last tile ended with a barrier: yb holds y[0, M2) (FUSE requires M2 <= YLDS)
+    // the last tile ended with a barrier
     if constexpr (FUSE) {
+        const float2 *ly = reinterpret_cast<const float2 *>(yb);   // YL: yb holds y[0, M2)
+        float2 *scr = reinterpret_cast<float2 *>(xin);
+        if constexpr (!YL) {
+            // y (this workgroup's stores) back into LDS, the timing scratch after it (the launch
+            // guarantees M2 + smax <= CF_LDS2).  Workgroup-scope fence: the stores and the loads
+            // share this CU's L1 (a device-scope fence would write back the whole L2 per channel).
+            __threadfence_block();
+            __syncthreads();
+            float2 *yl = reinterpret_cast<float2 *>(lds);
+            for (int i0 = tid; i0 < M2; i0 += 4 * 256) {
+                float2 v[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = i0 + 256 * e < M2 ? yp[i0 + 256 * e] : make_float2(0.f, 0.f);
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (i0 + 256 * e < M2) yl[i0 + 256 * e] = v[e];
+            }
+            __syncthreads();
+            ly = yl;
+            scr = yl + M2;
+        }
         if (tid < 64) {
             const size_t so = (size_t)ch * to.smax;
-            timing_wave(reinterpret_cast<const float2 *>(yb), M2, to.gain, to.soft_scale, to.sym + so,
-                        reinterpret_cast<float2 *>(xin), to.softbits + 2 * so, to.hard + so, to.nsym + ch,
-                        to.diag ? to.diag + ch : nullptr, to.smax, tid);
+            timing_wave(ly, M2, to.gain, to.soft_scale, to.sym + so, scr, to.softbits + 2 * so, to.hard + so,
+                        to.nsym + ch, to.diag ? to.diag + ch : nullptr, to.smax, tid);
         }
-    } else {
+    } else if constexpr (YL) {
         flush(M2);
     }
 }
@@ -952,9 +1020,14 @@ int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *i
     int32_t *no = (int32_t *)st.out(nsym, C * 4);
     float *dg = diag ? (float *)st.out(diag, C * 16) : nullptr;
     if (!x || !so || !sbo || !ho || !no) return st.finish();
-    if (M2 <= YLDS && smax <= (HALO + TILE_IN)) {   // fused: the 72 kHz samples never leave LDS
+    // fused: timing runs in the channel filter's workgroup on y in LDS (cf32: y never leaves LDS;
+    // SC16: y round-trips through a C x M2 scratch and is re-staged into the freed image/ring)
+    const bool fuse = fmt == TETRA_SC16 ? M2 + sm <= CF_LDS2 : (M2 <= YLDS && sm <= 2 * XIN4);
+    if (fuse) {
+        float2 *ys = nullptr;
+        if (fmt == TETRA_SC16 && !(ys = (float2 *)ws(ctx, S_W3, C * (size_t)M2 * 8))) return st.finish();
         const TimingOut to{P->gain, P->soft_scale, (float2 *)so, sbo, ho, no, (float4 *)dg, (int)smax};
-        rc = launch_chanfilt(ctx, P, x, fmt, C, N, M1, M2, nullptr, &to);
+        rc = launch_chanfilt(ctx, P, x, fmt, C, N, M1, M2, ys, &to);
         if (rc) return rc;
         return st.finish();
     }
