@@ -197,15 +197,22 @@ def test_sc16_ingest_matches_cf32(synth_small):
         assert np.array_equal(u, v)
 
 
-@pytest.mark.parametrize("N", [262144, 20000, 9001, 3000])
-def test_demod_lengths_vs_oracle(N):
+@pytest.mark.parametrize("fmt", ["cf32", "sc16"])
+@pytest.mark.parametrize("N", [262144, 131072, 20000, 9001, 3000])
+def test_demod_lengths_vs_oracle(N, fmt):
     """Chunk lengths around the kernel's structure: longer than the fused path's LDS output buffer
-    (component path), short, odd (trimmed to even like demod_batch does), and barely long enough."""
+    (component path), the 128 Ki design point (fused; SC16 re-stages y into the freed image and
+    stage-1 buffer), short, odd (trimmed to even like demod_batch does), and barely long enough --
+    for both input formats (SC16 against the oracle on its 1/32768-scaled samples)."""
     from tetraear.signal.etsi import synth, EtsiReceiver
     C = 3
     iq = synth(C, 262144, seed=9, snr_db=20.0)[0][:, :N]
+    inp = iq
+    if fmt == "sc16":
+        inp = np.stack([np.round(iq.real * 32768), np.round(iq.imag * 32768)], -1).clip(-32768, 32767).astype(np.int16)
+        iq = (inp[..., 0].astype(np.float32) / 32768 + 1j * (inp[..., 1].astype(np.float32) / 32768)).astype(np.complex64)
     rx = E.Receiver()
-    hard, soft, sym, ns = EtsiReceiver().demod_batch(iq)
+    hard, soft, sym, ns = EtsiReceiver().demod_batch(inp)
     Ne = N - N % 2
     for ch in range(C):
         so, sbo, ho, _ = rx.demod(iq[ch, :Ne])

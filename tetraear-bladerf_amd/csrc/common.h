@@ -41,7 +41,7 @@ struct tetra_ctx {
     std::string err;
     DevBuf slot[S_COUNT];
     char arch[64] = {0};
-    float coef_etsi[64 + 3 * 120];     // host image of the channel-filter tap tables
+    float coef_etsi[64 + 39 * 64];     // host image of the channel-filter tap tables (h1, stage-2 MFMA A)
 };
 
 extern thread_local std::string g_tetra_err;

@@ -6,11 +6,12 @@
 //
 //   k_chanfilt   stage 1: 48-tap decimate-by-10 FIR (2.4 MSps -> 240 kHz), stage 2: polyphase RRC
 //                (alpha 0.35, 321 taps at 720 kHz) resampler x3/10 -> 72 kHz = 4 samples/symbol.
-//                One workgroup streams one channel: 2560-sample input tiles (float4 loads, register
-//                prefetch two tiles deep), stage-1 outputs in a polyphase LDS ring, stage 2 every 8
-//                tiles as output triples (one per thread, wave-uniform taps from the scalar cache,
-//                packed fp32 FMA), outputs held in LDS and stored in one burst per channel.
-//                HBM-bound: 8 B read per input sample, 0.24 B written.
+//                One workgroup streams one channel: 2560-sample input tiles (float4 / SC16 uint2
+//                loads, register prefetch two tiles deep), stage 1 on packed fp32 FMA, stage-1
+//                outputs in a linear LDS buffer, stage 2 every 8 tiles on the matrix cores
+//                (v_mfma_f32_16x16x4_f32, exact f32: banded tap matrix x 16 columns of 5 output
+//                triples), y held in LDS (cf32) or round-tripped through L2 (SC16), then the timing
+//                stage on wave 0 (fused).  HBM-bound: 8 B read per input sample (cf32), 0.013 B written.
 //   k_timing     one wave per channel: Oerder-Meyr timing phase (wave reduction), block Gardner
 //                tracking (64 symbols per block = one per lane; error summed by xor-butterfly),
 //                cubic interpolation, differential decision, 4th-power CFO estimate, int8 soft bits.
@@ -36,10 +37,33 @@ __host__ __device__ constexpr KindP kind_params(int kind) {
 }
 
 // --------------------------------------------------------------------------- E2 timing
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v = v + __shfl_xor(v, off, 64);
+// 64-lane xor butterfly, levels 32, 16, .., LO: v_l + v_{l ^ off} at each level (the oracle's
+// tree; fp add is commutative, so operand order within a pair is free).  Cross-lane moves stay in
+// the VALU: permlane32/16 swaps for 32 and 16, DPP row rotations / quad permutes below (after the
+// xor-8 level a lane's value depends only on l mod 8, so rotating a row by 4 reads l ^ 4's value,
+// and by the same argument quad_perm covers 2 and 1) -- a ds_bpermute per level would put an LDS
+// round trip on the Gardner loop's critical path.
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+    // bound_ctrl: a lane without a source reads 0 (only wave_shr's lane 0, which is replaced);
+    // this form folds into the consuming v_add_f32_dpp
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+template <int LO>
+__device__ __forceinline__ float bfly(float v) {
+    const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(b[0]) + __uint_as_float(b[1]);
+    if constexpr (LO <= 8) v = v + dppf<0x128>(v);   // row_ror:8
+    if constexpr (LO <= 4) v = v + dppf<0x124>(v);   // row_ror:4
+    if constexpr (LO <= 2) v = v + dppf<0x4E>(v);    // quad_perm [2,3,0,1]
+    if constexpr (LO <= 1) v = v + dppf<0xB1>(v);    // quad_perm [1,0,3,2]
     return v;
+}
+__device__ __forceinline__ float wave_sum(float v) { return bfly<1>(v); }
+__device__ __forceinline__ float lane_f(float v, int l) {   // wave-uniform l
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
 __device__ __forceinline__ float pat2(float y, float x) {
@@ -106,9 +130,8 @@ __device__ __forceinline__ void timing_wave(const float2 *y, int M2, float gain,
         for (int u = 0; u < 8; ++u)
             if (n0 + 64 * u < M2) s += fmaf(v[u].x, v[u].x, v[u].y * v[u].y);
     }
-#pragma unroll
-    for (int off = 32; off >= 4; off >>= 1) s = s + __shfl_xor(s, off, 64);
-    const float A0 = __shfl(s, 0, 64), A1 = __shfl(s, 1, 64), A2 = __shfl(s, 2, 64), A3 = __shfl(s, 3, 64);
+    s = bfly<4>(s);
+    const float A0 = lane_f(s, 0), A1 = lane_f(s, 1), A2 = lane_f(s, 2), A3 = lane_f(s, 3);
     const float Xr = A0 - A2, Xi = A3 - A1;
     const float p = -0.63661977236758134f * pat2(Xi, Xr);
     float base = p < 0.0f ? p + 4.0f : p;
@@ -129,7 +152,7 @@ __device__ __forceinline__ void timing_wave(const float2 *y, int M2, float gain,
             on = interp(y, 0, t);
             mid = interp(y, 0, t - 2.0f);
         }
-        float2 pv = make_float2(__shfl_up(on.x, 1, 64), __shfl_up(on.y, 1, 64));
+        float2 pv = make_float2(dppf<0x138>(on.x), dppf<0x138>(on.y));   // wave_shr:1 (lane 0 replaced below)
         bool hp_ = true;
         if (lane == 0) { pv = prev; hp_ = have_prev; }
         float ev = 0.f, pw = 0.f;
@@ -148,7 +171,7 @@ __device__ __forceinline__ void timing_wave(const float2 *y, int M2, float gain,
             if (W > 0.0f) delta = delta - gain * (E / W);
             if (delta > 1.5f) delta = 1.5f;
             if (delta < -1.5f) delta = -1.5f;
-            prev = make_float2(__shfl(on.x, nv - 1, 64), __shfl(on.y, nv - 1, 64));
+            prev = make_float2(lane_f(on.x, nv - 1), lane_f(on.y, nv - 1));
             have_prev = true;
         }
         S += nv;
@@ -223,30 +246,38 @@ __global__ __launch_bounds__(64) void k_timing(const float2 *__restrict__ yall, 
 
 // --------------------------------------------------------------------------- E1 channel filter
 // The input tile is a linear float4 image (2 samples per entry, ds_write_b128 / ds_read_b128: a
-// 20-dword lane stride is conflict-free for b128's lane groups).  The stage-1 ring is polyphase:
-// x240[k] sits at [k % 10][k / 10], so stage 2's stride-10 reads are unit-stride across lanes.
-constexpr int RP = 231;         // row length of the stage-1 ring (10 x 231 = 2310 outputs kept; odd, so
-                                // the ten phase rows of one write fall in distinct LDS banks)
-constexpr int S2_EVERY = 8;     // stage 2 runs every 8 tiles: ~205 output triples, one per thread
+// 20-dword lane stride is conflict-free for b128's lane groups).  Stage-1 outputs x240[k] go to a
+// linear buffer lin[k - kbase]; after each stage-2 burst the still-needed tail is moved to its
+// front (kbase = 10 u_done), so stage 2's operand reads are base + immediate offset.
+constexpr int S2_EVERY = 8;     // stage 2 runs every 8 tiles: ~205 output triples
 constexpr int TPP = 107;        // RRC taps per polyphase branch (Lp = 321 = 3 x 107)
 constexpr int PFD = 2;          // input tiles in flight per workgroup (register prefetch depth, pa/pb;
                                 // 3 and 4 measured no faster)
 constexpr int YLDS = 4096;      // cf32: stage-2 outputs held in LDS before a flush (a 131072-sample
                                 // chunk has 3932)
-constexpr int XIN4 = (HALO + TILE_IN) / 2;        // float4 entries of the input image
-constexpr int CF_LDS4 = XIN4 + (10 * RP + 1) / 2; // image + ring, in float4 (39,344 B)
-constexpr int CF_LDS2 = 2 * CF_LDS4;              // the same in float2 (SC16 fused: y + timing scratch)
-constexpr int HQ = 120;         // row of the per-branch tap table, indexed by r = j + off_c
+// Stage 2 on the matrix cores (v_mfma_f32_16x16x4_f32: bit-for-bit a k-ordered fmaf chain).  One
+// MFMA tile: 16 columns = 8 segments x (re, im), each segment S2Q consecutive triples; row
+// i = 3q + c of a column is output 3(U + q) + c; A[i][s] = tap of x240[10U + s] for that output
+// (zero outside its 107: leading zeros keep the accumulator +0, trailing ones add +-0), so every
+// output is the oracle's ascending-j fma chain.
+constexpr int S2Q = 5;          // triples per column (rows 0..14; row 15 all-zero taps)
+constexpr int S2T = 8 * S2Q;    // triples per MFMA tile
+constexpr int S2K = 39;         // k-steps of 4: window 10 (S2Q - 1) + 114 = 154 -> 156 stage-1 outputs
+constexpr int LR = 2312;        // linear stage-1 buffer (float2)
+constexpr int XIN4 = (HALO + TILE_IN) / 2;   // float4 entries of the input image
+constexpr int CF_LDS4 = XIN4 + LR / 2;       // image + stage-1 buffer, in float4 (39,360 B)
+constexpr int CF_LDS2 = 2 * CF_LDS4;         // the same in float2 (SC16 fused: y + timing scratch)
+constexpr int CF_COEF = 64 + S2K * 64;       // device tap image: h1 (64) + A fragments [S2K][64 lanes]
 
 // Packed fp32 (v_pk_fma_f32): one real tap times a complex sample, each half a correctly rounded
 // fma -- the same per-component arithmetic as two fmaf calls.
 typedef float pf2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ pf2 pfma(float h, pf2 x, pf2 acc) { return __builtin_elementwise_fma(pf2{h, h}, x, acc); }
-__device__ __forceinline__ int rslot(int k) { return (k % 10) * RP + (k / 10) % RP; }
+typedef float f4 __attribute__((ext_vector_type(4)));
 
-// h1[48] stage-1 taps; hq[3][HQ]: branch c of stage 2, output m = 3u + c = sum_j hp[i0(c) - 3j] *
-// x240[10u + off_c + j] with i0 = {320, 318, 319}, off_c = {0, 4, 7}, stored at r = off_c + j
-// (zeros elsewhere).  Both tables are read with wave-uniform addresses (scalar loads).
+// h1[48] stage-1 taps (wave-uniform, scalar loads); stage 2: branch c, output m = 3u + c =
+// sum_j hp[i0(c) - 3j] * x240[10u + off_c + j] with i0 = {320, 318, 319}, off_c = {0, 4, 7}, held
+// as the MFMA A fragments (one VGPR per k-step per lane, loaded once).
 // Input pairs: one load = two complex samples -- float4 for cf32, uint2 (4 x int16) for SC16, the
 // BladeRF wire format (capture.py:241-269 scales by 1/32768, exact in fp32), so an SC16 capture is
 // filtered straight from its 4 B/sample form.
@@ -271,18 +302,20 @@ struct TimingOut {
 
 template <typename In, bool FUSE>
 __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, long N, int M1, int M2,
-                                                  const float *__restrict__ h1, const float *__restrict__ hq,
+                                                  const float *__restrict__ h1, const float *__restrict__ afrag,
                                                   float2 *__restrict__ y, TimingOut to) {
-    // cf32 keeps y in LDS (yb, 71 KB: two workgroups per CU, no y traffic); SC16 streams half the
+    // cf32 keeps y in LDS (yb, 72 KB: two workgroups per CU, no y traffic); SC16 streams half the
     // bytes per sample and is bound by the workgroup's own LDS/issue chain instead, so it keeps
-    // only the image and the ring (39 KB: four workgroups per CU) and sends y through HBM/L2
+    // only the image and the stage-1 buffer (39 KB: four workgroups per CU) and sends y through
+    // HBM/L2
     constexpr bool YL = std::is_same<In, float4>::value;
     __shared__ float4 lds[YL ? CF_LDS4 + YLDS / 2 : CF_LDS4];
     float4 *xin = lds;
-    float2 *ring = reinterpret_cast<float2 *>(lds + XIN4);
-    pf2 *yb = reinterpret_cast<pf2 *>(lds + CF_LDS4);   // YL only
+    float2 *lin = reinterpret_cast<float2 *>(lds + XIN4);
+    float *yb = reinterpret_cast<float *>(lds + CF_LDS4);   // YL only: y as (re, im) floats
     const int ch = blockIdx.x;
     const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6;
     const In *xp = iq + (size_t)ch * (N / 2);   // N even: 2 complex samples per load
     float2 *yp = y + (size_t)ch * M2;           // (YL && FUSE: unused)
     int ybase = 0;   // y index of yb[0]
@@ -291,10 +324,15 @@ __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, lon
     // batch at two workgroups per CU (HBM read/write turnarounds, and store acks inside the
     // prefetch's in-order vmcnt).
     auto flush = [&](int mend) {
-        for (int i = tid; i < mend - ybase; i += 256) yp[ybase + i] = make_float2(yb[i].x, yb[i].y);
+        for (int i = tid; i < mend - ybase; i += 256) yp[ybase + i] = make_float2(yb[2 * i], yb[2 * i + 1]);
         ybase = mend;
     };
-    for (int i = tid; i < 10 * RP; i += 256) ring[i] = make_float2(0.f, 0.f);   // finite x 0-tap
+    float at[S2K];   // this lane's A fragments
+#pragma unroll
+    for (int k = 0; k < S2K; ++k) at[k] = afrag[64 * k + lane];
+    // stage 2 reads whole windows, zero taps included: every entry must be finite
+    for (int i = tid; i < LR; i += 256) lin[i] = make_float2(0.f, 0.f);
+    int kbase = 0;   // x240 index of lin[0]
     // register prefetch PFD tiles deep (40 KiB in flight per workgroup): tile t's samples
     // [2560 t, 2560 t + 2560) land at image sample HALO + i
     // Loads are unconditional (index clamped) so the wait before a tile's LDS write can leave the
@@ -333,7 +371,7 @@ __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, lon
                 a = pfma(h1[2 * jj], pf2{v.x, v.y}, a);
                 a = pfma(h1[2 * jj + 1], pf2{v.z, v.w}, a);
             }
-            ring[rslot(k)] = make_float2(a.x, a.y);
+            lin[k - kbase] = make_float2(a.x, a.y);
         }
         __syncthreads();
         // halo for the next tile: image samples [0, 48) = this tile's [2560, 2608)
@@ -345,77 +383,57 @@ __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, lon
             const int num = 3 * kav + 2 - 320;   // largest m with floor((320 + 10m)/3) <= kav
             const int m_hi = num >= 0 ? min(num / 10, M2 - 1) : -1;
             const int u_hi = last ? (M2 - 1) / 3 : (m_hi >= 2 ? (m_hi - 2) / 3 : -1);
-            for (int u0 = u_done; u0 <= u_hi; u0 += 256) {
-                if (YL && min(3 * min(u0 + 256, u_hi + 1), M2) - ybase > YLDS) {   // chunk would not fit
-                    flush(3 * u0);
-                    __syncthreads();
+            const int nt = u_hi >= u_done ? (u_hi - u_done + S2T) / S2T : 0;   // MFMA tiles
+            const int mend = min(3 * (u_hi + 1), M2);
+            if (YL && nt > 0 && mend - ybase > YLDS) {   // this burst would not fit
+                flush(3 * u_done);
+                __syncthreads();
+            }
+            // columns: lane & 15 = 2 seg + comp; k-group lane >> 4.  Tile pairs (2p, 2p + 1) go to
+            // wave p % 4: two independent accumulators per wave cover the MFMA's latency.
+            const int kg = lane >> 4, seg = (lane & 15) >> 1, comp = lane & 1;
+            const float *lf = reinterpret_cast<const float *>(lin);
+            float *ys = YL ? yb : reinterpret_cast<float *>(xin + HALO / 2);   // !YL: staged, stored below
+            const int yo = YL ? ybase : 3 * u_done;
+            for (int p = wv; 2 * p < nt; p += 4) {
+                const int U0 = u_done + 2 * p * S2T + S2Q * seg, U1 = U0 + S2T;
+                // a column past u_hi reads the buffer's start instead (finite, never stored)
+                const int b0 = U0 <= u_hi ? 2 * (10 * U0 - kbase + kg) + comp : 2 * kg + comp;
+                const int b1 = U1 <= u_hi ? 2 * (10 * U1 - kbase + kg) + comp : 2 * kg + comp;
+                f4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int s2 = 0; s2 < S2K; ++s2) {
+                    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(at[s2], lf[b0 + 8 * s2], c0, 0, 0, 0);
+                    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(at[s2], lf[b1 + 8 * s2], c1, 0, 0, 0);
                 }
-                const int u = u0 + tid;
-                if (u <= u_hi) {
-                    // r-major over the 114 stage-1 inputs of the triple, rows loaded one block of
-                    // ten ahead of the FMAs (two register sets).  Taps outside a branch's 107 are
-                    // skipped where r is known at compile time (q = 0, q = 10 and the tail), so
-                    // each branch accumulates exactly its own taps in the oracle's order (kk
-                    // ascending); the zero entries left in the middle blocks do not exist.
-                    pf2 a0 = {0.f, 0.f}, a1 = {0.f, 0.f}, a2 = {0.f, 0.f};
-                    auto ld = [&](float2 (&v)[10], int q, int n) __attribute__((always_inline)) {
-                        const int row = (u + q) % RP;
+                // D: this lane holds rows i = 4 kg + r of its column; output m = 3 U + i
 #pragma unroll
-                        for (int p = 0; p < 10; ++p)
-                            if (p < n) v[p] = ring[p * RP + row];
-                    };
-                    // taps of block q; lo/hi: compile-time r window of each branch (r = 10q + p)
-                    auto blk = [&](const float2 (&v)[10], int q, int n, int lo1, int lo2, int hi0, int hi1)
-                        __attribute__((always_inline)) {
-#pragma unroll
-                        for (int p = 0; p < 10; ++p) {
-                            if (p >= n) continue;
-                            const pf2 x = {v[p].x, v[p].y};
-                            const int r = 10 * q + p;
-                            if (p <= hi0) a0 = pfma(hq[r], x, a0);
-                            if (p >= lo1 && p <= hi1) a1 = pfma(hq[HQ + r], x, a1);
-                            if (p >= lo2) a2 = pfma(hq[2 * HQ + r], x, a2);
-                        }
-                    };
-                    float2 v0[10], v1[10];
-                    ld(v0, 0, 10);
-                    ld(v1, 1, 10);
-                    blk(v0, 0, 10, 4, 7, 9, 9);   // branch 1 starts at r = 4, branch 2 at r = 7
-                    ld(v0, 2, 10);
-#pragma unroll 1
-                    for (int q = 1; q < 9; q += 2) {   // blocks 1..8
-                        blk(v1, q, 10, 0, 0, 9, 9);
-                        ld(v1, q + 2, 10);
-                        blk(v0, q + 1, 10, 0, 0, 9, 9);
-                        ld(v0, q + 3, 10);
-                    }
-                    blk(v1, 9, 10, 0, 0, 9, 9);
-                    ld(v1, 11, 4);
-                    blk(v0, 10, 10, 0, 0, 6, 9);   // branch 0 ends at r = 106
-                    blk(v1, 11, 4, 0, 0, -1, 0);   // r = 110..113: branch 1 ends at r = 110
-                    const int m = 3 * u;
-                    if constexpr (YL) {
-                        if (m < M2) yb[m - ybase] = a0;
-                        if (m + 1 < M2) yb[m + 1 - ybase] = a1;
-                        if (m + 2 < M2) yb[m + 2 - ybase] = a2;
-                    } else {
-                        // staged in the consumed part of the image (past the halo), stored below
-                        pf2 *xs = reinterpret_cast<pf2 *>(xin + HALO / 2) + 3 * tid;
-                        xs[0] = a0;
-                        xs[1] = a1;
-                        xs[2] = a2;
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 4 * kg + r, q = i / 3;
+                    if (i < 15) {
+                        const int m0 = 3 * U0 + i, m1 = 3 * U1 + i;
+                        if (U0 + q <= u_hi && m0 < M2) ys[2 * (m0 - yo) + comp] = c0[r];
+                        if (U1 + q <= u_hi && m1 < M2) ys[2 * (m1 - yo) + comp] = c1[r];
                     }
                 }
-                if constexpr (!YL) {
-                    // coalesced store of this chunk's outputs y[3 u0, 3 u0 + n)
+            }
+            if constexpr (!YL) {
+                if (nt > 0) {   // coalesced store of this burst's outputs y[3 u_done, mend)
                     __syncthreads();
-                    const int n = min(3 * min(u0 + 256, u_hi + 1), M2) - 3 * u0;
-                    const pf2 *xs = reinterpret_cast<const pf2 *>(xin + HALO / 2);
-                    for (int i = tid; i < n; i += 256) yp[3 * u0 + i] = make_float2(xs[i].x, xs[i].y);
-                    if (u0 + 256 <= u_hi) __syncthreads();
+                    const float2 *xs = reinterpret_cast<const float2 *>(ys);
+                    for (int i = tid; i < mend - yo; i += 256) yp[yo + i] = xs[i];
                 }
             }
             if (u_hi + 1 > u_done) u_done = u_hi + 1;
+            if (!last) {
+                // keep x240[10 u_done, kav] (the next triples' windows) at the buffer's front
+                const int from = 10 * u_done - kbase, cnt = kav + 1 - 10 * u_done;
+                __syncthreads();
+                const float2 v = tid < cnt ? lin[from + tid] : make_float2(0.f, 0.f);
+                __syncthreads();
+                if (tid < cnt) lin[tid] = v;
+                kbase = 10 * u_done;
+            }
         }
         __syncthreads();
     };
@@ -897,17 +915,20 @@ static int etsi_check(tetra_ctx *ctx, const tetra_etsi_plan *P) {
 // Stage-1 taps and the per-branch stage-2 tap table (k_chanfilt), then the launch.
 static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *x, int fmt, size_t C, size_t N,
                            int64_t M1, int64_t M2, float2 *y, const TimingOut *fused = nullptr) {
-    float *coef = (float *)ws(ctx, S_W6, (64 + 3 * HQ) * 4);
+    static_assert(sizeof(ctx->coef_etsi) == CF_COEF * sizeof(float), "tap image size");
+    float *coef = (float *)ws(ctx, S_W6, CF_COEF * 4);
     if (!coef) return TETRA_E_NOMEM;
     float *hc = ctx->coef_etsi;
     static const int i0[3] = {320, 318, 319}, off[3] = {0, 4, 7};
     for (int j = 0; j < 64; ++j) hc[j] = j < 48 ? P->h1[j] : 0.f;
-    for (int c = 0; c < 3; ++c)
-        for (int r = 0; r < HQ; ++r) {
-            const int j = r - off[c];
-            hc[64 + c * HQ + r] = j >= 0 && j < TPP ? P->hp[i0[c] - 3 * j] : 0.f;
+    // A fragment of k-step ks for lane l: A[i = l & 15][s = 4 ks + (l >> 4)], row i = 3q + c
+    for (int ks = 0; ks < S2K; ++ks)
+        for (int l = 0; l < 64; ++l) {
+            const int i = l & 15, sidx = 4 * ks + (l >> 4), q = i / 3, c = i % 3;
+            const int j = sidx - 10 * q - off[c];
+            hc[64 + 64 * ks + l] = i < 15 && j >= 0 && j < TPP ? P->hp[i0[c] - 3 * j] : 0.f;
         }
-    HIP_TRY(ctx, hipMemcpyAsync(coef, hc, (64 + 3 * HQ) * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(coef, hc, CF_COEF * 4, hipMemcpyHostToDevice, ctx->stream));
     PROF(ctx, fused ? "etsi_demod" : "etsi_chanfilt");
     const TimingOut to = fused ? *fused : TimingOut{};
     const dim3 g((unsigned)C), b(256);
