@@ -10,6 +10,9 @@ A step = one pass of the hot path over the rank's batch:
   --chain etsi   (default) channel filter + pi/4-DQPSK demod with Gardner timing + sync/slicing +
                  descramble + deinterleave + RCPC Viterbi + CRC  (the north-star chain)
   --chain compat reference-compatible process() + decode() lower MAC
+  --chain wideband  C3 (configs[2]): a 20 MSps capture of 800 carriers (--wb-samples per rank)
+                 -> polyphase filter bank + rocFFT -> per-carrier RRC resampler to 72 kHz ->
+                 timing/decision -> lower MAC, every carrier cut into 3932-sample timing chunks
 
 Launch: python bench.py --gpus 1 --steps 5 --warmup 2
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -40,7 +43,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--chain", choices=("etsi", "compat"), default=os.environ.get("TETRA_BENCH_CHAIN", "etsi"))
+    ap.add_argument("--chain", choices=("etsi", "compat", "wideband"),
+                    default=os.environ.get("TETRA_BENCH_CHAIN", "etsi"))
+    ap.add_argument("--wb-samples", type=int, default=10_000_000,
+                    help="wideband: 20 MSps samples per rank per step (C3: 0.5 s)")
     ap.add_argument("--channels", type=int, default=8192, help="channels per rank")
     ap.add_argument("--samples", type=int, default=131072, help="samples per channel chunk")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (rank 0)")
@@ -168,7 +174,11 @@ def main():
     c.check(c.lib.tetra_set_stream(c.handle, ctypes.c_void_p(stream.cuda_stream)), "set_stream")
 
     C, N = a.channels, a.samples
-    if a.chain == "etsi":
+    if a.chain == "wideband":
+        from tetraear.signal.wideband import BenchStep as WbStep
+        step = WbStep(c, a.wb_samples, seed=rank_seed(1000, rank), device=dev)
+        C, N = 1, a.wb_samples   # units: wideband samples
+    elif a.chain == "etsi":
         from tetraear.signal.etsi import BenchStep as EtsiStep
         step = EtsiStep(c, C, N, FS, seed=rank_seed(1000, rank), device=dev, iq_format=a.iq)
         pipe = "off" if a.no_pipeline else a.pipeline
@@ -207,7 +217,12 @@ def main():
     value = aggregate_msps(C * N, world, a.steps, elapsed)
 
     if rank == 0:
-        name, per_sample, ksym = step.dominant()
+        if hasattr(step, "stage_bytes"):   # several comparable stages: the slowest one is dominant
+            sb = step.stage_bytes()
+            name = max(sb, key=lambda k: prof.get(k, (0.0, 0))[0])
+            per_sample, ksym = sb[name]
+        else:
+            name, per_sample, ksym = step.dominant()
         kms, kcnt = prof.get(name, (0.0, 0))
         launch_ms = kms / max(1, kcnt)
         units_per_launch = C * N
@@ -226,18 +241,20 @@ def main():
             "vs_baseline": None,
             "dtype": step.dtype if hasattr(step, "dtype") else "f32/f64",
             "data": "synthetic (device-generated, seeded per rank)",
-            "config": {
+            "config": step.config(world) if hasattr(step, "config") else {
                 "workload": f"C5 shard: {C} channels x {N} {a.iq if a.chain == 'etsi' else 'cf32'} samples "
                             f"@2.4 MSps per GPU, chain={a.chain}",
                 "channels_per_gpu": C, "samples_per_channel": N, "sample_rate": FS,
                 "parallelism": f"channel-sharded x{world}",
                 "pipeline": bool(getattr(step, "pipelined", False)),
             },
-            "realtime_channels": int(value * 1e6 / FS),
+            "realtime_channels": int(step.realtime_channels(value) if hasattr(step, "realtime_channels")
+                                     else value * 1e6 / FS),
             "roofline": {
                 "bound": "hbm", "kernel": name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic_from_profiles(ksym, f"{C} channels x {N} {a.iq if a.chain == 'etsi' else 'cf32'}"),
+                "traffic": traffic_from_profiles(ksym, step.workload_key() if hasattr(step, "workload_key") else
+                                                 f"{C} channels x {N} {a.iq if a.chain == 'etsi' else 'cf32'}"),
                 "launch_ms": round(launch_ms, 4), "algorithmic_bytes_per_launch": per_sample * units_per_launch,
                 "kernel_symbol": ksym,
             },

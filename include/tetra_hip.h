@@ -241,6 +241,34 @@ int tetra_synth_bursts_per_channel(size_t N, double fs);
 int tetra_synth_etsi(tetra_ctx *ctx, size_t C, size_t N, double fs, uint64_t seed, float snr_db, float cfo_max,
                      void *iq, uint32_t *cell_init, int32_t *kinds, uint8_t *payload, double *t0);
 
+/* ---------------------------------------------------------------- wideband channeliser (C3)
+ * A fs = 20 MSps capture -> M carriers at fs/M spacing (polyphase filter bank, D = M/4, rocFFT)
+ * -> per-carrier RRC(0.35) resampler fs/D -> 72 kHz (up/down) = the ETSI timing stage's input
+ * (tetra_etsi_timing).  Replaces tuning the SDR to one carrier per capture (the reference's
+ * capture loop, /root/reference/tetraear/ui/modern.py:1886-1887 feeds one 2.4 MSps carrier
+ * into SignalProcessor.process); SURVEY.md §8d config C3.  Host pointers h, g. */
+typedef struct tetra_wb_plan {
+    int32_t M;           /* carriers = FFT length (800) */
+    int32_t D;           /* decimation, M / 4 (200): carrier rate fs / D */
+    int32_t P;           /* prototype taps per branch, 1..8 (L = M * P) */
+    int32_t up, down;    /* carrier resampler fs/D -> 72 kHz (18 / 25) */
+    int32_t Lg;          /* resampler taps, a multiple of up */
+    double fs;           /* wideband rate */
+    const float *h;      /* prototype lowpass [M * P] (unity DC gain) */
+    const float *g;      /* resampler RRC at up * fs / D [Lg] */
+} tetra_wb_plan;
+
+/* nblk filter-bank output blocks and n72 resampler outputs per carrier for Nw input samples. */
+int tetra_wb_lengths(const tetra_wb_plan *plan, size_t Nw, int64_t *nblk, int64_t *n72);
+/* x [Nw] cf32 -> y [M][n_keep] cf32 at 72 kHz (first n_keep <= n72 outputs of each carrier; a
+ * carrier's row is then n_keep / M2 timing chunks of M2 samples for tetra_etsi_timing). */
+int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *plan, const void *x, size_t Nw, void *y, size_t n_keep);
+/* Synthetic wideband capture: M carriers of tetra_synth_etsi bursts at fs/D, filter-bank
+ * synthesised to fs, plus AWGN at per-carrier Es/N0 = snr_db.  Outputs as tetra_synth_etsi with
+ * C = M and N = Nw / D + 1 (carrier k at +k fs / M, i.e. FFT bin k). */
+int tetra_synth_wideband(tetra_ctx *ctx, const tetra_wb_plan *plan, size_t Nw, uint64_t seed, float snr_db,
+                         float cfo_max, void *x, uint32_t *cell_init, int32_t *kinds, uint8_t *payload, double *t0);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,136 @@
+"""Wideband channeliser (C3): oracle self-consistency on the CPU, GPU parity.
+
+The reference has no channeliser, so oracle/wideband.py (float64) is the specification.  The GPU
+runs the filter bank in fp32 with a rocFFT transform: its 72 kHz output y is held to the oracle
+within a tolerance written below; from y on (timing, decision, lower MAC) the chain is the ETSI
+one and is compared bit-exactly / by round trip, as in test_gpu_etsi.py.
+"""
+import numpy as np
+import pytest
+
+import wideband as W
+
+# GPU y vs the float64 oracle: fp32 fold + 800-point fp32 FFT + 45-tap fp32 resampler
+Y_TOL = 2e-5   # of max |y| over the carriers compared
+
+
+def test_design_matches_oracle():
+    from tetraear.signal.wideband import wb_design
+    h, g = wb_design()
+    d = W.design()
+    assert np.array_equal(h, d["h"]) and np.array_equal(g, d["g"])
+
+
+def test_oracle_filter_bank_round_trip():
+    """synthesis -> analysis recovers a carrier's baseband tone at its own bin (unit gain, right
+    frequency sign), and far carriers see nothing."""
+    d = W.design()
+    M, D = d["M"], d["D"]
+    nbb = 300
+    s = np.zeros((M, nbb), complex)
+    f = 3000.0
+    s[5] = np.exp(2j * np.pi * f * np.arange(nbb) / (d["fs"] / D))
+    x = W.synthesize(s, d, nbb * D)
+    v = W.analysis(x, d)
+    seg = v[:, 40:60]
+    assert np.allclose(np.abs(seg[5]), 1.0, atol=2e-3)
+    assert np.allclose(np.angle(seg[5, 1:] / seg[5, :-1]), 2 * np.pi * f / (d["fs"] / D), atol=1e-6)
+    assert np.abs(seg[100]).max() < 1e-5 and np.abs(seg[405]).max() < 1e-5
+
+
+def test_lengths_match_oracle():
+    from tetraear.signal.wideband import wb_plan
+    p = wb_plan()
+    d = W.design()
+    for Nw in (1600, 1601, 20000, 1_100_000, 10_000_000):
+        assert p.lengths(Nw) == W.lengths(d, Nw), Nw
+
+
+@pytest.fixture(scope="module")
+def capture():
+    from tetraear.signal.wideband import synth_wideband
+    Nw = 1_120_000   # 56 ms: one 3932-sample timing chunk per carrier
+    return synth_wideband(Nw, seed=11, snr_db=30.0, cfo_max=300.0)
+
+
+@pytest.mark.gpu
+def test_synth_matches_oracle():
+    """The device generator is the oracle's synthesis of the same carrier baseband."""
+    from tetraear import _hip
+    from tetraear.signal.wideband import wb_plan
+    c = _hip.ctx()
+    p = wb_plan()
+    d = W.design()
+    Nw = 40_000
+    nbb = Nw // p.D + 1
+    x = np.empty(Nw, np.complex64)
+    cells = np.empty(p.M, np.uint32)
+    c.check(c.lib.tetra_synth_wideband(c.handle, p.c, Nw, 5, 1000.0, 300.0, _hip.ptr(x), _hip.ptr(cells), None, None,
+                                       None), "synth_wideband")
+    s = np.empty((p.M, nbb), np.complex64)
+    c.check(c.lib.tetra_synth_etsi(c.handle, p.M, nbb, p.fs / p.D, 5, 1000.0, 300.0, _hip.ptr(s), _hip.ptr(cells),
+                                   None, None, None), "synth_etsi")
+    want = W.synthesize(s, d, Nw)
+    assert np.abs(x - want).max() <= 1e-5 * np.abs(want).max()
+
+
+@pytest.mark.gpu
+def test_channelize_vs_oracle(capture):
+    from tetraear.signal.wideband import WidebandReceiver
+    x = capture[0]
+    d = W.design()
+    rx = WidebandReceiver()
+    y = rx.channelize(x)
+    _, n72 = W.lengths(d, len(x))
+    assert y.shape == (d["M"], n72)
+    want = W.channelize(x.astype(np.complex128), d)
+    err = np.abs(y - want).max()
+    assert err <= Y_TOL * np.abs(want).max(), err
+    # a partial row (n_keep < n72) is the same prefix
+    y2 = rx.channelize(x, 1000)
+    assert np.array_equal(y2, y[:, :1000])
+
+
+@pytest.mark.gpu
+def test_wideband_timing_bit_exact(capture):
+    """From y on the chain is the ETSI one: the GPU timing on the channeliser's own output equals
+    oracle/etsi.py on the same y, carrier by carrier."""
+    import etsi as E
+    from tetraear.signal.wideband import WidebandReceiver
+    x = capture[0]
+    rx = WidebandReceiver()
+    hard, soft, sym, ns = rx.demod(x)
+    nchunk = ns.shape[1]
+    y = rx.channelize(x, nchunk * rx.m2).reshape(rx.plan.M, nchunk, rx.m2)
+    ora = E.Receiver()
+    for k in (0, 1, 399, 400, 401, 799):
+        so, sbo, ho, _ = ora.timing(y[k, 0])
+        n = int(ns[k, 0])
+        assert n == len(so), k
+        assert np.array_equal(sym[k, 0, :n], so) and np.array_equal(hard[k, 0, :n - 1], ho)
+        assert np.array_equal(soft[k, 0, :2 * (n - 1)], sbo)
+
+
+@pytest.mark.gpu
+def test_wideband_round_trip(capture):
+    """800 carriers through channeliser + timing + lower MAC: every CRC-passing block is one the
+    carrier transmitted, and nearly all blocks pass."""
+    from tetraear.core.etsi import EtsiLowerMac
+    from tetraear.signal.wideband import WidebandReceiver
+    x, cells, kinds, payload, t0 = capture
+    rx = WidebandReceiver()
+    hard, soft, sym, ns = rx.demod(x)
+    M, nchunk = ns.shape
+    res = EtsiLowerMac().decode_batch(soft.reshape(M * nchunk, -1), hard.reshape(M * nchunk, -1), ns.reshape(-1),
+                                      np.repeat(cells, nchunk))
+    nblk = nok = 0
+    for i, frames in enumerate(res):
+        sent = {tuple(p) for bb in payload[i // nchunk] for p in bb}
+        for f in frames:
+            for b in f["blocks"]:
+                nblk += 1
+                if b["crc_ok"]:
+                    nok += 1
+                    assert tuple(np.pad(b["bits"], (0, 268 - len(b["bits"])))) in sent
+    assert nblk >= 2 * M
+    assert nok / nblk > 0.97, (nok, nblk)

@@ -22,6 +22,7 @@ enum Slot {
     S_IN0 = 0, S_IN1, S_IN2, S_IN3, S_IN4, S_IN5,          // staged host inputs
     S_OUT0, S_OUT1, S_OUT2, S_OUT3, S_OUT4, S_OUT5,        // staged host outputs
     S_W0, S_W1, S_W2, S_W3, S_W4, S_W5, S_W6, S_W7,        // kernel workspaces
+    S_W8, S_W9, S_W10,                                     // wideband channeliser
     S_COUNT
 };
 
@@ -42,6 +43,9 @@ struct tetra_ctx {
     DevBuf slot[S_COUNT];
     char arch[64] = {0};
     float coef_etsi[64 + 39 * 64];     // host image of the channel-filter tap tables (h1, stage-2 MFMA A)
+    std::vector<float> taps_wb;        // host image of the wideband prototype + resampler taps
+    void *fft = nullptr;               // rocFFT plan cache (wideband.hip), freed by fft_free
+    void (*fft_free)(void *) = nullptr;
 };
 
 extern thread_local std::string g_tetra_err;

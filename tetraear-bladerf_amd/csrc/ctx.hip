@@ -194,6 +194,7 @@ void tetra_destroy(tetra_ctx *ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (auto &r : ctx->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
+    if (ctx->fft && ctx->fft_free) ctx->fft_free(ctx->fft);
     for (auto &b : ctx->slot)
         if (b.p) (void)hipFree(b.p);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);

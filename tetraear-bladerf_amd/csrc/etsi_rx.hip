@@ -471,6 +471,8 @@ __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, lon
             scr = yl + M2;
         }
         if (tid < 64) {
+            // the timing pass is this workgroup's serial tail: let it win issue slots on its SIMD
+            __builtin_amdgcn_s_setprio(3);
             const size_t so = (size_t)ch * to.smax;
             timing_wave(ly, M2, to.gain, to.soft_scale, to.sym + so, scr, to.softbits + 2 * so, to.hard + so,
                         to.nsym + ch, to.diag ? to.diag + ch : nullptr, to.smax, tid);

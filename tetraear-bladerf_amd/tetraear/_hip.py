@@ -44,6 +44,15 @@ class EtsiPlan(ctypes.Structure):
     ]
 
 
+class WbPlan(ctypes.Structure):
+    """Mirror of struct tetra_wb_plan (include/tetra_hip.h); h and g point at arrays the owner keeps."""
+    _fields_ = [
+        ("M", ctypes.c_int32), ("D", ctypes.c_int32), ("P", ctypes.c_int32), ("up", ctypes.c_int32),
+        ("down", ctypes.c_int32), ("Lg", ctypes.c_int32), ("fs", ctypes.c_double),
+        ("h", ctypes.POINTER(ctypes.c_float)), ("g", ctypes.POINTER(ctypes.c_float)),
+    ]
+
+
 ETSI_MAXB, ETSI_MAXJ = 8, 16
 
 _lib = None
@@ -95,6 +104,10 @@ def _bind(L):
         "tetra_lmac_etsi": (_i32, [_vp, _vp, _vp, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp]),
         "tetra_etsi_decode_blocks": (_i32, [_vp, _vp, _sz, _i32, _vp, _vp, _vp]),
         "tetra_etsi_encode_blocks": (_i32, [_vp, _vp, _sz, _i32, _vp, _vp]),
+        "tetra_wb_lengths": (_i32, [ctypes.POINTER(WbPlan), _sz, _vp, _vp]),
+        "tetra_channelize": (_i32, [_vp, ctypes.POINTER(WbPlan), _vp, _sz, _vp, _sz]),
+        "tetra_synth_wideband": (_i32, [_vp, ctypes.POINTER(WbPlan), _sz, ctypes.c_uint64, ctypes.c_float,
+                                        ctypes.c_float, _vp, _vp, _vp, _vp, _vp]),
         "tetra_synth_bursts_per_channel": (_i32, [_sz, ctypes.c_double]),
         "tetra_synth_etsi": (_i32, [_vp, _sz, _sz, ctypes.c_double, ctypes.c_uint64, ctypes.c_float, ctypes.c_float,
                                     _vp, _vp, _vp, _vp, _vp]),

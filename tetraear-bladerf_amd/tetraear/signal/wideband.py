@@ -1,0 +1,237 @@
+"""Wideband channeliser on the GPU (BASELINE.json configs[2]).
+
+The reference receives one carrier per capture: the BladeRF is tuned to it and 2.4 MSps IQ goes
+to SignalProcessor.process (/root/reference/tetraear/ui/modern.py:1886-1887, 2029).  The north
+star's "polyphase FIR channeliser" instead takes a 20 MSps capture holding 800 carriers at 25 kHz
+spacing and splits it on the device: a polyphase filter bank (libtetra_hip.so k_pfb_fold +
+rocFFT, D = M/4), then per carrier an RRC(0.35) matched-filter resampler 100 kHz -> 72 kHz
+(k_pfb_resamp), which is exactly the sample stream the ETSI timing stage takes (4 samples per
+symbol, tetra_etsi_timing), followed by the ETSI lower MAC.  This module designs the filters and
+moves arrays; oracle/wideband.py is the float64 specification the tests hold it to.
+"""
+import ctypes
+import functools
+
+import numpy as np
+from scipy import signal as _design
+
+from tetraear import _hip
+from tetraear.signal.etsi import etsi_plan, rrc
+
+FS_WB = 20e6
+M_WB = 800
+P_WB = 2            # prototype taps per polyphase branch (L = 1600)
+UP, DOWN = 18, 25   # 100 kHz -> 72 kHz
+LG = 810            # resampler taps at 1.8 MHz (8.1 symbols of RRC)
+M2_CHUNK = 3932     # 72 kHz samples per timing chunk (as a 128 Ki chunk at 2.4 MSps)
+
+
+@functools.lru_cache(maxsize=4)
+def wb_design(fs=FS_WB, M=M_WB):
+    """Prototype lowpass h [M P] (unity DC gain, cut-off 2 carrier spacings: flat over +-12.5 kHz,
+    72 dB down from 87.5 kHz, the first band that aliases onto a carrier at fs/D) and the
+    resampler RRC g [LG] at up * fs / D."""
+    D = M // 4
+    if abs(fs / D * UP / DOWN - 72000.0) > 1e-6:
+        raise ValueError("the channeliser is built for fs / (M / 4) = 100 kHz carriers (20 MSps, 800 carriers)")
+    h = _design.firwin(M * P_WB, 2.0 * fs / M, fs=fs, window=("kaiser", 7.0)).astype(np.float32)
+    sps = fs / D * UP / 18000.0
+    g = rrc((np.arange(LG) - (LG - 1) / 2.0) / sps).astype(np.float32)
+    return h, g
+
+
+class WbPlan:
+    """tetra_wb_plan plus the tap arrays it points at."""
+
+    def __init__(self, fs=FS_WB, M=M_WB):
+        self.h, self.g = wb_design(fs, M)
+        p = _hip.WbPlan()
+        p.M, p.D, p.P, p.up, p.down, p.Lg, p.fs = M, M // 4, P_WB, UP, DOWN, LG, fs
+        p.h = self.h.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+        p.g = self.g.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+        self.c = p
+        self.M, self.D, self.fs = M, M // 4, fs
+
+    def lengths(self, Nw):
+        nb, n72 = ctypes.c_int64(), ctypes.c_int64()
+        _hip.lib().tetra_wb_lengths(self.c, Nw, ctypes.byref(nb), ctypes.byref(n72))
+        return nb.value, n72.value
+
+
+@functools.lru_cache(maxsize=4)
+def wb_plan(fs=FS_WB, M=M_WB):
+    return WbPlan(fs, M)
+
+
+def chunking(plan, Nw, m2=M2_CHUNK):
+    """(nchunk, M2): each carrier's 72 kHz row is cut into nchunk timing chunks of M2 samples."""
+    _, n72 = plan.lengths(Nw)
+    nchunk = n72 // m2
+    if nchunk < 1:
+        raise ValueError(f"{Nw} wideband samples give {n72} samples per carrier, less than one chunk of {m2}")
+    return nchunk, m2
+
+
+class WidebandReceiver:
+    """Channeliser + per-carrier ETSI demod (timing, decision) for host or device arrays."""
+
+    def __init__(self, fs=FS_WB, M=M_WB, m2=M2_CHUNK):
+        self.plan = wb_plan(fs, M)
+        self.etsi = etsi_plan(2.4e6)   # timing-loop constants (the channel-filter taps are not used)
+        self.m2 = m2
+
+    def channelize(self, x, n_keep=None):
+        """x [Nw] complex64 -> y [M][n_keep] complex64 at 72 kHz."""
+        c = _hip.ctx()
+        x = np.ascontiguousarray(x, np.complex64)
+        _, n72 = self.plan.lengths(len(x))
+        n_keep = n72 if n_keep is None else n_keep
+        y = np.empty((self.plan.M, n_keep), np.complex64)
+        c.check(c.lib.tetra_channelize(c.handle, self.plan.c, _hip.ptr(x), len(x), _hip.ptr(y), n_keep), "channelize")
+        return y
+
+    def demod(self, x):
+        """x [Nw] -> (hard, soft_bits, sym, nsym) per (carrier, chunk): [M, nchunk, smax] uint8,
+        [M, nchunk, 2 smax] int8, [M, nchunk, smax] complex64, [M, nchunk] int32."""
+        nchunk, m2 = chunking(self.plan, len(x), self.m2)
+        y = self.channelize(x, nchunk * m2)
+        c = _hip.ctx()
+        C = self.plan.M * nchunk
+        sm = m2 // 4 + 2
+        sym = np.empty((C, sm), np.complex64)
+        soft = np.empty((C, 2 * sm), np.int8)
+        hard = np.empty((C, sm), np.uint8)
+        ns = np.empty(C, np.int32)
+        c.check(c.lib.tetra_etsi_timing(c.handle, self.etsi, _hip.ptr(y), C, m2, _hip.ptr(sym), _hip.ptr(soft),
+                                        _hip.ptr(hard), _hip.ptr(ns), sm, None), "etsi_timing")
+        M = self.plan.M
+        return (hard.reshape(M, nchunk, sm), soft.reshape(M, nchunk, 2 * sm), sym.reshape(M, nchunk, sm),
+                ns.reshape(M, nchunk))
+
+
+def synth_wideband(Nw, seed=1, snr_db=30.0, cfo_max=300.0, fs=FS_WB, M=M_WB):
+    """Synthetic capture (device-generated, copied to the host): x [Nw] complex64, cells [M],
+    kinds [M][NB], payload [M][NB][2][268], t0 [M] (carrier k is FFT bin k, at +k fs/M)."""
+    plan = wb_plan(fs, M)
+    c = _hip.ctx()
+    nbb = Nw // plan.D + 1
+    nb = c.lib.tetra_synth_bursts_per_channel(nbb, fs / plan.D)
+    x = np.empty(Nw, np.complex64)
+    cells = np.empty(M, np.uint32)
+    kinds = np.empty((M, nb), np.int32)
+    payload = np.empty((M, nb, 2, 268), np.uint8)
+    t0 = np.empty(M, np.float64)
+    c.check(c.lib.tetra_synth_wideband(c.handle, plan.c, Nw, seed, snr_db, cfo_max, _hip.ptr(x), _hip.ptr(cells),
+                                       _hip.ptr(kinds), _hip.ptr(payload), _hip.ptr(t0)), "synth_wideband")
+    return x, cells, kinds, payload, t0
+
+
+class BenchStep:
+    """bench.py --chain wideband (C3): one step = channelise a device-resident 20 MSps capture,
+    timing + decision on every (carrier, chunk), lower MAC (sync, Viterbi, CRC) on all of them."""
+    dtype = "f32 (DSP, rocFFT), int8/int32 (Viterbi)"
+
+    def __init__(self, c, Nw, seed, device, snr_db=30.0, fs=FS_WB, M=M_WB):
+        import torch
+        self.c, self.Nw, self.fs = c, Nw, fs
+        self.plan = wb_plan(fs, M)
+        self.etsi = etsi_plan(2.4e6)
+        self.nchunk, self.m2 = chunking(self.plan, Nw)
+        self.C = M * self.nchunk
+        self.sm = self.m2 // 4 + 2
+        nbb = Nw // self.plan.D + 1
+        nb = c.lib.tetra_synth_bursts_per_channel(nbb, fs / self.plan.D)
+        self.x = torch.empty((Nw, 2), dtype=torch.float32, device=device)
+        cells = torch.empty(M, dtype=torch.int32, device=device)
+        self.kinds = torch.empty((M, nb), dtype=torch.int32, device=device)
+        self.payload = torch.empty((M, nb, 2, 268), dtype=torch.uint8, device=device)
+        c.check(c.lib.tetra_synth_wideband(c.handle, self.plan.c, Nw, seed, snr_db, 300.0, _hip.ptr(self.x),
+                                           _hip.ptr(cells), _hip.ptr(self.kinds), _hip.ptr(self.payload), None),
+                "synth_wideband")
+        # every chunk of carrier k uses carrier k's scrambling code
+        self.cells = cells.repeat_interleave(self.nchunk).contiguous()
+        c.check(c.lib.tetra_etsi_set_cells(c.handle, _hip.ptr(self.cells), self.C), "set_cells")
+        self.y = torch.empty((M, self.nchunk * self.m2, 2), dtype=torch.float32, device=device)
+        self.sym = torch.empty((self.C, self.sm, 2), dtype=torch.float32, device=device)
+        self.soft = torch.empty((self.C, 2 * self.sm), dtype=torch.int8, device=device)
+        self.hard = torch.empty((self.C, self.sm), dtype=torch.uint8, device=device)
+        self.nsym = torch.empty(self.C, dtype=torch.int32, device=device)
+        self.nburst = torch.empty(self.C, dtype=torch.int32, device=device)
+        self.bursts = torch.empty((self.C, _hip.ETSI_MAXB, 2), dtype=torch.int32, device=device)
+        self.nblock = torch.empty(self.C, dtype=torch.int32, device=device)
+        self.blocks = torch.empty((self.C, _hip.ETSI_MAXJ, 4), dtype=torch.int32, device=device)
+        self.type1 = torch.empty((self.C, _hip.ETSI_MAXJ, 268), dtype=torch.uint8, device=device)
+        self.pipelined = False
+
+    def contexts(self):
+        return [self.c]
+
+    def __call__(self):
+        c = self.c
+        c.check(c.lib.tetra_channelize(c.handle, self.plan.c, _hip.ptr(self.x), self.Nw, _hip.ptr(self.y),
+                                       self.nchunk * self.m2), "channelize")
+        c.check(c.lib.tetra_etsi_timing(c.handle, self.etsi, _hip.ptr(self.y), self.C, self.m2, _hip.ptr(self.sym),
+                                        _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.sm, None),
+                "etsi_timing")
+        c.check(c.lib.tetra_lmac_etsi(c.handle, _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.C,
+                                      self.sm, _hip.ptr(self.nburst), _hip.ptr(self.bursts), _hip.ptr(self.nblock),
+                                      _hip.ptr(self.blocks), _hip.ptr(self.type1)), "lmac_etsi")
+
+    def stage_bytes(self):
+        """Algorithmic bytes per wideband input sample of each timed stage (cf32 = 8 B):
+        fold reads x and writes Y (M per D samples), the FFT reads and writes Y, the resampler reads
+        Y and writes y (M carriers at 72 kHz), the timing stage reads y and writes per symbol an
+        8 B symbol, 2 soft bits and a hard dibit.  bench.py reports the slowest of them."""
+        M, D, fs = self.plan.M, self.plan.D, self.fs
+        yb = 8.0 * M * 72000.0 / fs
+        return {"wb_fold": (8.0 + 8.0 * M / D, "k_pfb_fold"), "wb_fft": (2 * 8.0 * M / D, None),
+                "wb_resamp": (8.0 * M / D + yb, "k_pfb_resamp"),
+                "etsi_timing": (yb + 11.0 * M * 18000.0 / fs, "k_timing")}
+
+    def config(self, world):
+        return {"workload": f"C3: {self.Nw} samples of a {self.fs / 1e6:g} MSps capture per GPU, "
+                            f"{self.plan.M} carriers x {self.nchunk} timing chunks of {self.m2}",
+                "wideband_samples_per_gpu": self.Nw, "sample_rate": self.fs, "carriers": self.plan.M,
+                "timing_chunks_per_carrier": self.nchunk, "parallelism": f"capture-sharded x{world}",
+                "pipeline": False}
+
+    def realtime_channels(self, value_msps):
+        return value_msps * 1e6 / self.fs * self.plan.M   # carriers served at real time
+
+    def workload_key(self):
+        return f"C3 {self.Nw} wideband"
+
+    def cpu_baseline(self, budget_s):
+        import os
+        import sys
+        import time
+        repo = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+        sys.path.insert(0, os.path.join(repo, "oracle"))
+        import etsi as E   # the CPU restatements (cpu_baseline leg only)
+        import wideband as W
+        d = W.design(self.fs, self.plan.M)
+        nw = (self.m2 * DOWN) // UP * self.plan.D + self.plan.M * P_WB + 64 * self.plan.D   # one chunk per carrier
+        x = self.x[:nw].cpu().numpy().view(np.complex64)[:, 0]
+        t0 = time.perf_counter()
+        y = W.channelize(x.astype(np.complex128), d, self.m2).astype(np.complex64)
+        t_ch = time.perf_counter() - t0
+        cells = self.cells[::self.nchunk].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+        rx = E.Receiver()
+        t1 = time.perf_counter()
+        k = 0
+        while k < self.plan.M and (k < 8 or time.perf_counter() - t0 < budget_s):
+            sym, soft, hard, _ = rx.timing(y[k])
+            rx.lower_mac(soft, hard, int(cells[k]))
+            k += 1
+        t_c = (time.perf_counter() - t1) / k
+        total = t_ch + self.plan.M * t_c
+        return dict(value=nw / total / 1e6, unit="Msamples/s", cores=1, kind="port",
+                    sample=f"{nw} samples @{self.fs / 1e6:g} MSps: numpy float64 channeliser ({t_ch:.2f} s) + C "
+                           f"oracle timing+lower MAC on {k} of {self.plan.M} carriers (x{self.plan.M / k:.1f} "
+                           f"extrapolated), 1 thread")
+
+    def quality(self):
+        nb = self.nblock.cpu().numpy()
+        blocks = self.blocks.cpu().numpy()
+        ok = sum(int(blocks[i, :nb[i], 1].sum()) for i in range(self.C))
+        return dict(blocks=int(nb.sum()), crc_ok=ok, bursts=int(self.nburst.sum().item()))
