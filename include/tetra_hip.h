@@ -269,6 +269,16 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *plan, const void *x, s
 int tetra_synth_wideband(tetra_ctx *ctx, const tetra_wb_plan *plan, size_t Nw, uint64_t seed, float snr_db,
                          float cfo_max, void *x, uint32_t *cell_init, int32_t *kinds, uint8_t *payload, double *t0);
 
+/* ---------------------------------------------------------------- waterfall spectrum (C3)
+ * Live spectrum / waterfall rows: frame f of channel c is x[c][f*hop .. f*hop + nfft), Hann
+ * window (numpy.hanning), forward FFT, fftshift, power = 20 log10(|X| / nfft + 1e-20) in dBFS --
+ * the display of /root/reference/tetraear/ui/modern.py:1928-1941 (one frame x[:2048] per chunk),
+ * batched over channels and frames.  iq [C][N] in TETRA_CF32 / TETRA_SC16 / TETRA_CF64; out
+ * [C][nframes][nfft] float32.  nfft = 2048 (the reference's fixed size); needs
+ * (nframes - 1) * hop + nfft <= N.  Single-pass fused kernel (window + LDS FFT + dB). */
+int tetra_waterfall(tetra_ctx *ctx, const void *iq, int iq_fmt, size_t C, size_t N, size_t nfft, size_t hop,
+                    size_t nframes, float *out);
+
 #ifdef __cplusplus
 }
 #endif

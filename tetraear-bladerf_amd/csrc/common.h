@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <type_traits>
 #include <cstdint>
@@ -23,6 +24,7 @@ enum Slot {
     S_OUT0, S_OUT1, S_OUT2, S_OUT3, S_OUT4, S_OUT5,        // staged host outputs
     S_W0, S_W1, S_W2, S_W3, S_W4, S_W5, S_W6, S_W7,        // kernel workspaces
     S_W8, S_W9, S_W10,                                     // wideband channeliser
+    S_W11,                                                 // waterfall window + twiddles
     S_COUNT
 };
 
@@ -46,6 +48,7 @@ struct tetra_ctx {
     std::vector<float> taps_wb;        // host image of the wideband prototype + resampler taps
     void *fft = nullptr;               // rocFFT plan cache (wideband.hip), freed by fft_free
     void (*fft_free)(void *) = nullptr;
+    bool wf_tables_ready = false;      // waterfall tables uploaded to slot S_W11
 };
 
 extern thread_local std::string g_tetra_err;

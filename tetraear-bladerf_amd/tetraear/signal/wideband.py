@@ -127,8 +127,9 @@ def synth_wideband(Nw, seed=1, snr_db=30.0, cfo_max=300.0, fs=FS_WB, M=M_WB):
 
 
 class BenchStep:
-    """bench.py --chain wideband (C3): one step = channelise a device-resident 20 MSps capture,
-    timing + decision on every (carrier, chunk), lower MAC (sync, Viterbi, CRC) on all of them."""
+    """bench.py --chain wideband (C3): one step = the capture's waterfall rows (2048-pt Hann, hop
+    2048), channelise the device-resident 20 MSps capture, timing + decision on every (carrier,
+    chunk), lower MAC (sync, Viterbi, CRC) on all of them."""
     dtype = "f32 (DSP, rocFFT), int8/int32 (Viterbi)"
 
     def __init__(self, c, Nw, seed, device, snr_db=30.0, fs=FS_WB, M=M_WB):
@@ -161,6 +162,8 @@ class BenchStep:
         self.nblock = torch.empty(self.C, dtype=torch.int32, device=device)
         self.blocks = torch.empty((self.C, _hip.ETSI_MAXJ, 4), dtype=torch.int32, device=device)
         self.type1 = torch.empty((self.C, _hip.ETSI_MAXJ, 268), dtype=torch.uint8, device=device)
+        self.nfr = Nw // 2048   # waterfall rows of the capture (2048-pt Hann frames, hop 2048)
+        self.wf = torch.empty((self.nfr, 2048), dtype=torch.float32, device=device)
         self.pipelined = False
 
     def contexts(self):
@@ -168,6 +171,8 @@ class BenchStep:
 
     def __call__(self):
         c = self.c
+        c.check(c.lib.tetra_waterfall(c.handle, _hip.ptr(self.x), _hip.TETRA_CF32, 1, self.Nw, 2048, 2048, self.nfr,
+                                      _hip.ptr(self.wf)), "waterfall")
         c.check(c.lib.tetra_channelize(c.handle, self.plan.c, _hip.ptr(self.x), self.Nw, _hip.ptr(self.y),
                                        self.nchunk * self.m2), "channelize")
         c.check(c.lib.tetra_etsi_timing(c.handle, self.etsi, _hip.ptr(self.y), self.C, self.m2, _hip.ptr(self.sym),
@@ -184,7 +189,8 @@ class BenchStep:
         8 B symbol, 2 soft bits and a hard dibit.  bench.py reports the slowest of them."""
         M, D, fs = self.plan.M, self.plan.D, self.fs
         yb = 8.0 * M * 72000.0 / fs
-        return {"wb_fold": (8.0 + 8.0 * M / D, "k_pfb_fold"), "wb_fft": (2 * 8.0 * M / D, None),
+        return {"waterfall": (12.0 * self.nfr * 2048 / self.Nw, "k_waterfall"),
+                "wb_fold": (8.0 + 8.0 * M / D, "k_pfb_fold"), "wb_fft": (2 * 8.0 * M / D, None),
                 "wb_resamp": (8.0 * M / D + yb, "k_pfb_resamp"),
                 "etsi_timing": (yb + 11.0 * M * 18000.0 / fs, "k_timing")}
 
