@@ -63,6 +63,10 @@ int tetra_device_arch(tetra_ctx *ctx, char *buf, size_t n);
  * context stream.  tetra_profile_read() synchronizes, then returns the accumulated milliseconds
  * and launch counts per stage since the previous read (names NUL-separated, in first-seen order). */
 int tetra_profile(tetra_ctx *ctx, int enable);
+/* Diagnostic: the channel filter's HBM read pattern without its arithmetic (rows workgroups, one
+ * row of row_bytes each, 16-B loads; lds_bytes of LDS per workgroup caps the residency like the
+ * real kernel's).  Device pointer x; timed under the "read_floor" profile stage. */
+int tetra_read_floor(tetra_ctx *ctx, const void *x, size_t rows, size_t row_bytes, size_t lds_bytes);
 int tetra_profile_read(tetra_ctx *ctx, char *names, size_t names_len, double *ms, int64_t *count,
                        int max_stages, int *n_stages);
 

@@ -25,6 +25,7 @@ enum Slot {
     S_W0, S_W1, S_W2, S_W3, S_W4, S_W5, S_W6, S_W7,        // kernel workspaces
     S_W8, S_W9, S_W10,                                     // wideband channeliser
     S_W11,                                                 // waterfall window + twiddles
+    S_W12,                                                 // ETSI channel-filter tap image (kept)
     S_COUNT
 };
 
@@ -45,6 +46,7 @@ struct tetra_ctx {
     DevBuf slot[S_COUNT];
     char arch[64] = {0};
     float coef_etsi[64 + 39 * 64];     // host image of the channel-filter tap tables (h1, stage-2 MFMA A)
+    const void *coef_etsi_dev = nullptr;   // workspace the tap image was last uploaded to
     std::vector<float> taps_wb;        // host image of the wideband prototype + resampler taps
     void *fft = nullptr;               // rocFFT plan cache (wideband.hip), freed by fft_free
     void (*fft_free)(void *) = nullptr;

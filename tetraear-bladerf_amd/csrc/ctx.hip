@@ -226,3 +226,35 @@ int tetra_device_arch(tetra_ctx *ctx, char *buf, size_t n) {
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------ HBM read floor (diagnostic)
+// The access pattern of the channel filter without its arithmetic: one workgroup streams one row
+// of `row_bytes` with 16-B loads, five per thread in flight per pass, and folds them into one word
+// (so nothing is dead-code eliminated).  `lds_bytes` of dynamic LDS caps the workgroups per CU the
+// way the real kernel's LDS does.  bench.py reports it as the measured floor beside the roofline.
+__global__ __launch_bounds__(256) void k_read_floor(const float4 *__restrict__ x, long row4, uint32_t *out) {
+    extern __shared__ float4 pad_lds[];
+    const float4 *p = x + (size_t)blockIdx.x * row4;
+    uint32_t acc = 0;
+    for (long q = threadIdx.x; q < row4; q += 5 * 256) {
+        float4 v[5];
+#pragma unroll
+        for (int r = 0; r < 5; ++r) v[r] = p[min(q + r * 256, row4 - 1)];
+#pragma unroll
+        for (int r = 0; r < 5; ++r)
+            acc ^= __float_as_uint(v[r].x) ^ __float_as_uint(v[r].y) ^ __float_as_uint(v[r].z) ^ __float_as_uint(v[r].w);
+    }
+    if (acc == 0x9E3779B9u) pad_lds[threadIdx.x] = make_float4(0.f, 0.f, 0.f, 0.f);   // keeps the LDS allocation
+    if (acc == 0x9E3779B9u) out[blockIdx.x] = acc;   // practically never: no store traffic
+}
+
+extern "C" int tetra_read_floor(tetra_ctx *ctx, const void *x, size_t rows, size_t row_bytes, size_t lds_bytes) {
+    if (!ctx || !x || rows == 0 || row_bytes % 16 || lds_bytes > 160 * 1024) return TETRA_E_INVALID;
+    uint32_t *o = (uint32_t *)ws(ctx, S_W7, rows * 4);
+    if (!o) return TETRA_E_NOMEM;
+    PROF(ctx, "read_floor");
+    hipLaunchKernelGGL(k_read_floor, dim3((unsigned)rows), dim3(256), lds_bytes, ctx->stream, (const float4 *)x,
+                       (long)(row_bytes / 16), o);
+    HIP_TRY(ctx, hipGetLastError());
+    return TETRA_OK;
+}

@@ -304,11 +304,11 @@ template <typename In, bool FUSE>
 __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, long N, int M1, int M2,
                                                   const float *__restrict__ h1, const float *__restrict__ afrag,
                                                   float2 *__restrict__ y, TimingOut to) {
+    constexpr bool YL = std::is_same<In, float4>::value;
     // cf32 keeps y in LDS (yb, 72 KB: two workgroups per CU, no y traffic); SC16 streams half the
     // bytes per sample and is bound by the workgroup's own LDS/issue chain instead, so it keeps
     // only the image and the stage-1 buffer (39 KB: four workgroups per CU) and sends y through
     // HBM/L2
-    constexpr bool YL = std::is_same<In, float4>::value;
     __shared__ float4 lds[YL ? CF_LDS4 + YLDS / 2 : CF_LDS4];
     float4 *xin = lds;
     float2 *lin = reinterpret_cast<float2 *>(lds + XIN4);
@@ -918,9 +918,9 @@ static int etsi_check(tetra_ctx *ctx, const tetra_etsi_plan *P) {
 static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *x, int fmt, size_t C, size_t N,
                            int64_t M1, int64_t M2, float2 *y, const TimingOut *fused = nullptr) {
     static_assert(sizeof(ctx->coef_etsi) == CF_COEF * sizeof(float), "tap image size");
-    float *coef = (float *)ws(ctx, S_W6, CF_COEF * 4);
+    float *coef = (float *)ws(ctx, S_W12, CF_COEF * 4);   // slot of its own: the image persists
     if (!coef) return TETRA_E_NOMEM;
-    float *hc = ctx->coef_etsi;
+    float hc[CF_COEF];
     static const int i0[3] = {320, 318, 319}, off[3] = {0, 4, 7};
     for (int j = 0; j < 64; ++j) hc[j] = j < 48 ? P->h1[j] : 0.f;
     // A fragment of k-step ks for lane l: A[i = l & 15][s = 4 ks + (l >> 4)], row i = 3q + c
@@ -930,7 +930,13 @@ static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void 
             const int j = sidx - 10 * q - off[c];
             hc[64 + 64 * ks + l] = i < 15 && j >= 0 && j < TPP ? P->hp[i0[c] - 3 * j] : 0.f;
         }
-    HIP_TRY(ctx, hipMemcpyAsync(coef, hc, CF_COEF * 4, hipMemcpyHostToDevice, ctx->stream));
+    // upload only when the taps or the workspace changed: a per-call pageable copy would sit on the
+    // stream in front of every launch
+    if (ctx->coef_etsi_dev != coef || memcmp(hc, ctx->coef_etsi, sizeof(hc)) != 0) {
+        memcpy(ctx->coef_etsi, hc, sizeof(hc));
+        HIP_TRY(ctx, hipMemcpyAsync(coef, ctx->coef_etsi, CF_COEF * 4, hipMemcpyHostToDevice, ctx->stream));
+        ctx->coef_etsi_dev = coef;
+    }
     PROF(ctx, fused ? "etsi_demod" : "etsi_chanfilt");
     const TimingOut to = fused ? *fused : TimingOut{};
     const dim3 g((unsigned)C), b(256);
@@ -1045,6 +1051,7 @@ int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *i
     if (!x || !so || !sbo || !ho || !no) return st.finish();
     // fused: timing runs in the channel filter's workgroup on y in LDS (cf32: y never leaves LDS;
     // SC16: y round-trips through a C x M2 scratch and is re-staged into the freed image/ring)
+    // (measured: cf32 with y through L2 at four workgroups per CU, as SC16 does, is 2.5 % slower)
     const bool fuse = fmt == TETRA_SC16 ? M2 + sm <= CF_LDS2 : (M2 <= YLDS && sm <= 2 * XIN4);
     if (fuse) {
         float2 *ys = nullptr;

@@ -149,9 +149,13 @@ class BenchStep:
 
     dtype = "f32 (DSP), int8/int32 (Viterbi)"
 
-    def __init__(self, c, C, N, fs, seed, device, snr_db=18.0, iq_format="cf32"):
+    def __init__(self, c, C, N, fs, seed, device, snr_db=18.0, iq_format="cf32", demod="fused"):
         import torch
         self.c, self.C, self.N, self.fs = c, C, N, fs
+        # "fused": k_chanfilt<.., true> (timing on the LDS-resident 72 kHz samples, wave 0 of the
+        # workgroup); "split": k_chanfilt<.., false> writes y (0.24 B per input sample) and k_timing
+        # runs as its own launch -- with the pipeline, beside the next batch's channel filter
+        self.demod_mode = demod
         self.fmt = {"cf32": _hip.TETRA_CF32, "sc16": _hip.TETRA_SC16}[iq_format]
         self.plan = etsi_plan(fs)
         _, self.M2, self.smax = lengths(self.plan, N)
@@ -175,7 +179,8 @@ class BenchStep:
         self.nblock = torch.empty(C, dtype=torch.int32, device=device)
         self.blocks = torch.empty((C, _hip.ETSI_MAXJ, 4), dtype=torch.int32, device=device)
         self.type1 = torch.empty((C, _hip.ETSI_MAXJ, 268), dtype=torch.uint8, device=device)
-
+        if demod == "split":
+            self.y = [torch.empty((C, self.M2, 2), dtype=torch.float32, device=device)]
         self.pipelined = False
 
     def pipeline(self):
@@ -194,6 +199,8 @@ class BenchStep:
         self.back.check(self.back.lib.tetra_etsi_set_cells(self.back.handle, _hip.ptr(self.cells), self.C), "set_cells")
         self.bufs = [(self.sym, self.soft, self.hard, self.nsym),
                      tuple(torch.empty_like(t) for t in (self.sym, self.soft, self.hard, self.nsym))]
+        if self.demod_mode == "split":   # y is what crosses the streams; the symbol buffers stay on the back one
+            self.y.append(torch.empty_like(self.y[0]))
         self.ev_front = [torch.cuda.Event() for _ in range(2)]
         self.ev_back = [torch.cuda.Event() for _ in range(2)]
         for e in self.ev_back:
@@ -215,12 +222,36 @@ class BenchStep:
                                       _hip.ptr(self.nburst), _hip.ptr(self.bursts), _hip.ptr(self.nblock),
                                       _hip.ptr(self.blocks), _hip.ptr(self.type1)), "lmac_etsi")
 
+    def _chanfilt(self, c, y):
+        c.check(c.lib.tetra_etsi_chanfilt_fmt(c.handle, self.plan, _hip.ptr(self.iq), self.fmt, self.C, self.N,
+                                              _hip.ptr(y)), "chanfilt")
+
+    def _timing(self, c, y):
+        c.check(c.lib.tetra_etsi_timing(c.handle, self.plan, _hip.ptr(y), self.C, self.M2, _hip.ptr(self.sym),
+                                        _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.smax,
+                                        None), "timing")
+
     def __call__(self):
+        split = self.demod_mode == "split"
         if not self.pipelined:
-            self._demod(self.c, self.sym, self.soft, self.hard, self.nsym)
+            if split:
+                self._chanfilt(self.c, self.y[0])
+                self._timing(self.c, self.y[0])
+            else:
+                self._demod(self.c, self.sym, self.soft, self.hard, self.nsym)
             self._lmac(self.c, self.soft, self.hard, self.nsym)
             return
         i = self.k & 1
+        if split:
+            self.k += 1
+            self.s_front.wait_event(self.ev_back[i])    # timing of batch k-2 has consumed y[i]
+            self._chanfilt(self.c, self.y[i])
+            self.ev_front[i].record(self.s_front)
+            self.s_back.wait_event(self.ev_front[i])
+            self._timing(self.back, self.y[i])
+            self._lmac(self.back, self.soft, self.hard, self.nsym)
+            self.ev_back[i].record(self.s_back)
+            return
         self.k += 1
         sym, soft, hard, nsym = self.bufs[i]
         self.s_front.wait_event(self.ev_back[i])        # lower MAC of batch k-2 has consumed buffer i
@@ -232,8 +263,19 @@ class BenchStep:
 
     def dominant(self):
         # fused k_chanfilt<.., true>: reads 8 B (cf32) or 4 B (SC16) per input sample; writes per
-        # symbol (0.0075 per input sample) 8 B cf32 symbol + 2 B soft bits + 1 B hard dibit
-        return ("etsi_demod", (4.0 if self.fmt == _hip.TETRA_SC16 else 8.0) + 11.0 * 18000.0 / self.fs, "k_chanfilt")
+        # symbol (0.0075 per input sample) 8 B cf32 symbol + 2 B soft bits + 1 B hard dibit.
+        # split k_chanfilt<.., false>: the same reads, writes y (8 B per 72 kHz sample = 0.24 B per
+        # input sample)
+        rd = 4.0 if self.fmt == _hip.TETRA_SC16 else 8.0
+        if self.demod_mode == "split":
+            return ("etsi_chanfilt", rd + 8.0 * self.M2 / self.N, "k_chanfilt")
+        return ("etsi_demod", rd + 11.0 * 18000.0 / self.fs, "k_chanfilt")
+
+    def floor_args(self):
+        """bench.py's read floor over this batch: one row per channel, the fused cf32 kernel's
+        72 KB of LDS (two workgroups per CU) or SC16's 39 KB (four)."""
+        row = self.N * (4 if self.fmt == _hip.TETRA_SC16 else 8)
+        return _hip.ptr(self.iq), self.C, row, (39 if self.fmt == _hip.TETRA_SC16 else 72) * 1024
 
     def quality(self):
         """Decoded-block statistics of the last step (device results, checked on the host)."""
