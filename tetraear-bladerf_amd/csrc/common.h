@@ -48,6 +48,8 @@ struct tetra_ctx {
     float coef_etsi[64 + 39 * 64];     // host image of the channel-filter tap tables (h1, stage-2 MFMA A)
     const void *coef_etsi_dev = nullptr;   // workspace the tap image was last uploaded to
     std::vector<float> taps_wb;        // host image of the wideband prototype + resampler taps
+    std::vector<float> taps_wb_up;     // ... as last uploaded to taps_wb_dev (slot S_W9)
+    const void *taps_wb_dev = nullptr;
     void *fft = nullptr;               // rocFFT plan cache (wideband.hip), freed by fft_free
     void (*fft_free)(void *) = nullptr;
     bool wf_tables_ready = false;      // waterfall tables uploaded to slot S_W11

@@ -64,6 +64,221 @@ __global__ __launch_bounds__(256) void k_pfb_fold(const float2 *__restrict__ x, 
     }
 }
 
+// ---------------------------------------------------------------- fused analysis: fold + FFT
+// Y_j[k] for M = 800 = 8 x 4 x 5 x 5 (mixed-radix Stockham, backward, unnormalised) fused with the
+// fold: a workgroup walks JB consecutive blocks; the wideband samples sit in an LDS ring (each
+// block brings D = 200 new samples, loaded AF blocks ahead into registers), stage 1 folds its
+// eight inputs u_j[i] = sum_p h[pM + i] x[n_j - pM - i] straight from the ring (thread b < 100
+// always owns i = b + 100 r, so its 8 P taps stay in registers), stages 2-3 run through a padded
+// LDS frame, stage 4 stores Y_j in natural order (5 coalesced 8-B stores per thread).  HBM: the D
+// new samples (8 B each, plus a 1600-sample halo per workgroup) in, the 800 outputs out -- against
+// fold-then-rocFFT's extra Y write + read + re-read of x from L2 per block.
+constexpr int AN_M = 800, AN_T = 256, AN_AF = 8;
+constexpr int AN_FR = AN_M + AN_M / 8;                  // padded frame
+constexpr int AN_TW2 = 0, AN_TW3 = 3 * 8, AN_TW4 = AN_TW3 + 4 * 32, AN_TWN = AN_TW4 + 4 * 160;   // r-major
+
+__device__ __forceinline__ int an_pad(int i) { return i + (i >> 3); }
+__device__ __forceinline__ float2 c_add(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 c_sub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 c_mul(float2 a, float2 b) {
+    return make_float2(fmaf(a.x, b.x, -(a.y * b.y)), fmaf(a.x, b.y, a.y * b.x));
+}
+__device__ __forceinline__ float2 c_pi(float2 a) { return make_float2(-a.y, a.x); }   // a * (+i)
+
+// backward DFTs (X_k = sum_n a_n e^{+2 pi i n k / R})
+__device__ __forceinline__ void bdft4(float2 &a0, float2 &a1, float2 &a2, float2 &a3) {
+    const float2 t0 = c_add(a0, a2), t1 = c_sub(a0, a2), t2 = c_add(a1, a3), t3 = c_pi(c_sub(a1, a3));
+    a0 = c_add(t0, t2);
+    a2 = c_sub(t0, t2);
+    a1 = c_add(t1, t3);
+    a3 = c_sub(t1, t3);
+}
+__device__ __forceinline__ void bdft8(float2 *v) {
+    float2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6], o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
+    bdft4(e0, e1, e2, e3);
+    bdft4(o0, o1, o2, o3);
+    const float s = 0.70710678118654752f;
+    o1 = make_float2((o1.x - o1.y) * s, (o1.x + o1.y) * s);      // * e^{+i pi/4}
+    o2 = c_pi(o2);
+    o3 = make_float2(-(o3.x + o3.y) * s, (o3.x - o3.y) * s);     // * e^{+3 i pi/4}
+    v[0] = c_add(e0, o0); v[4] = c_sub(e0, o0);
+    v[1] = c_add(e1, o1); v[5] = c_sub(e1, o1);
+    v[2] = c_add(e2, o2); v[6] = c_sub(e2, o2);
+    v[3] = c_add(e3, o3); v[7] = c_sub(e3, o3);
+}
+__device__ __forceinline__ void bdft5(float2 *a) {
+    const float c1 = 0.30901699437494742f, c2 = -0.80901699437494742f;   // cos(2 pi/5), cos(4 pi/5)
+    const float s1 = 0.95105651629515357f, s2 = 0.58778525229247313f;    // sin(2 pi/5), sin(4 pi/5)
+    const float2 t1 = c_add(a[1], a[4]), t2 = c_add(a[2], a[3]), t3 = c_sub(a[1], a[4]), t4 = c_sub(a[2], a[3]);
+    const float2 b1 = make_float2(a[0].x + c1 * t1.x + c2 * t2.x, a[0].y + c1 * t1.y + c2 * t2.y);
+    const float2 b2 = make_float2(a[0].x + c2 * t1.x + c1 * t2.x, a[0].y + c2 * t1.y + c1 * t2.y);
+    const float2 e1 = make_float2(s1 * t3.x + s2 * t4.x, s1 * t3.y + s2 * t4.y);   // X1 = b1 + i e1
+    const float2 e2 = make_float2(s2 * t3.x - s1 * t4.x, s2 * t3.y - s1 * t4.y);   // X2 = b2 + i e2
+    a[0] = c_add(a[0], c_add(t1, t2));
+    a[1] = c_add(b1, c_pi(e1));
+    a[4] = c_sub(b1, c_pi(e1));
+    a[2] = c_add(b2, c_pi(e2));
+    a[3] = c_sub(b2, c_pi(e2));
+}
+
+// Roles by wave: waves 0-2 fold + transform + store, wave 3 only loads (the new samples of block
+// j + 1 + AF while block j is transformed, written into the ring during block j's stage 1).  A
+// wave's vmcnt counts its loads and stores in one queue: were one wave to do both, waiting for a
+// prefetched load would also wait for every store issued since.  Two frames alternate per block,
+// so a block costs three barriers (after stages 1, 2, 3).
+template <int P>
+__global__ __launch_bounds__(AN_T) void k_pfb_analysis(const float4 *__restrict__ x2, int nblk, int JB,
+                                                       const float *__restrict__ h, const float2 *__restrict__ twg,
+                                                       float2 *__restrict__ Y) {
+    constexpr int M = AN_M, D = M / 4, L = P * M;
+    constexpr int RING = L + D <= 2048 ? 2048 : (L + D <= 4096 ? 4096 : 8192);   // samples, power of 2
+    __shared__ float4 ring4[RING / 2];
+    __shared__ float2 frb[2][AN_FR];
+    __shared__ float2 tw[AN_TWN];
+    const float2 *ring = reinterpret_cast<const float2 *>(ring4);
+    const int t = threadIdx.x;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int j0 = blockIdx.x * JB, j1 = min(nblk, j0 + JB);
+    for (int i = t; i < AN_TWN; i += AN_T) tw[i] = twg[i];
+    // the first block's window x[j0 D, j0 D + L) (pairs: j0 D is even)
+    for (int q = t; q < L / 2; q += AN_T) {
+        const long pr = (long)j0 * (D / 2) + q;
+        ring4[(int)(pr & (RING / 2 - 1))] = x2[pr];
+    }
+    if (wv == 3) {
+        // loader: lane l carries pairs l and l + 64 (< D / 2 = 100) of the new samples of block j,
+        // x[L + (j - 1) D, + D); loads are unconditional (lane and block clamped) so no branch joins
+        // wait for them
+        const int l = t - 192;
+        const int q0 = l, q1 = min(l + 64, D / 2 - 1);
+        auto base = [&](int j) -> long { return (long)(L + (long)(min(j, j1 - 1) - 1) * D) / 2; };
+        // four register slots, one per block of the unrolled loop (plain variables and a macro, so
+        // they stay in VGPRs), each waited for with the count of the loads issued after it
+        static_assert(AN_AF == 8, "loader unroll");
+        float4 s0a = x2[base(j0 + 1) + q0], s0b = x2[base(j0 + 1) + q1];
+        float4 s1a = x2[base(j0 + 2) + q0], s1b = x2[base(j0 + 2) + q1];
+        float4 s2a = x2[base(j0 + 3) + q0], s2b = x2[base(j0 + 3) + q1];
+        float4 s3a = x2[base(j0 + 4) + q0], s3b = x2[base(j0 + 4) + q1];
+        float4 s4a = x2[base(j0 + 5) + q0], s4b = x2[base(j0 + 5) + q1];
+        float4 s5a = x2[base(j0 + 6) + q0], s5b = x2[base(j0 + 6) + q1];
+        float4 s6a = x2[base(j0 + 7) + q0], s6b = x2[base(j0 + 7) + q1];
+        float4 s7a = x2[base(j0 + 8) + q0], s7b = x2[base(j0 + 8) + q1];
+        __syncthreads();
+#define AN_LOAD_BLOCK(J, A, B)                                                                  \
+        {                                                                                       \
+            const int jj = (J);                                                                 \
+            if (jj + 1 < j1) {   /* block jj + 1's samples (fetched AF blocks ago) to the ring */ \
+                const long bb = (long)(L + (long)jj * D) / 2;                                   \
+                ring4[(int)((bb + q0) & (RING / 2 - 1))] = A;                                   \
+                if (l + 64 < D / 2) ring4[(int)((bb + l + 64) & (RING / 2 - 1))] = B;           \
+            }                                                                                   \
+            A = x2[base(jj + 1 + AN_AF) + q0];   /* block jj + 1 + AF's */                      \
+            B = x2[base(jj + 1 + AN_AF) + q1];                                                  \
+            __syncthreads(); /* after stage 1 */                                                \
+            __syncthreads(); /* after stage 2 */                                                \
+            __syncthreads(); /* after stage 3 */                                                \
+        }
+        int j = j0;
+        for (; j + 8 <= j1; j += 8) {
+            AN_LOAD_BLOCK(j, s0a, s0b)
+            AN_LOAD_BLOCK(j + 1, s1a, s1b)
+            AN_LOAD_BLOCK(j + 2, s2a, s2b)
+            AN_LOAD_BLOCK(j + 3, s3a, s3b)
+            AN_LOAD_BLOCK(j + 4, s4a, s4b)
+            AN_LOAD_BLOCK(j + 5, s5a, s5b)
+            AN_LOAD_BLOCK(j + 6, s6a, s6b)
+            AN_LOAD_BLOCK(j + 7, s7a, s7b)
+        }
+        if (j < j1) AN_LOAD_BLOCK(j, s0a, s0b)
+        if (j + 1 < j1) AN_LOAD_BLOCK(j + 1, s1a, s1b)
+        if (j + 2 < j1) AN_LOAD_BLOCK(j + 2, s2a, s2b)
+        if (j + 3 < j1) AN_LOAD_BLOCK(j + 3, s3a, s3b)
+        if (j + 4 < j1) AN_LOAD_BLOCK(j + 4, s4a, s4b)
+        if (j + 5 < j1) AN_LOAD_BLOCK(j + 5, s5a, s5b)
+        if (j + 6 < j1) AN_LOAD_BLOCK(j + 6, s6a, s6b)
+#undef AN_LOAD_BLOCK
+        return;
+    }
+    float hr[8][P];
+    if (t < 100) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+#pragma unroll
+            for (int p = 0; p < P; ++p) hr[r][p] = h[p * M + t + 100 * r];
+    }
+    __syncthreads();
+    for (int j = j0; j < j1; ++j) {
+        float2 *fa = frb[(j - j0) & 1], *fb = frb[((j - j0) & 1) ^ 1];
+        const long nj = (long)L - 1 + (long)j * D;
+        // stage 1 (R = 8, Ns = 1): butterfly t < 100 on u[t + 100 r], folded from the ring
+        if (t < 100) {
+            float2 v[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int i = t + 100 * r;
+                float ar = 0.f, ai = 0.f;
+#pragma unroll
+                for (int p = 0; p < P; ++p) {
+                    const float2 xv = ring[(int)((nj - p * M - i) & (RING - 1))];
+                    ar = fmaf(hr[r][p], xv.x, ar);
+                    ai = fmaf(hr[r][p], xv.y, ai);
+                }
+                v[r] = make_float2(ar, ai);
+            }
+            bdft8(v);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) fa[an_pad(8 * t + r)] = v[r];
+        }
+        __syncthreads();
+        // stage 2 (R = 4, Ns = 8): 200 butterflies on 192 threads, fa -> fb
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+            const int b = t + 192 * h2;
+            if (b < 200) {
+                float2 v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = fa[an_pad(b + 200 * r)];
+                const int m = b & 7;
+#pragma unroll
+                for (int r = 1; r < 4; ++r) v[r] = c_mul(v[r], tw[AN_TW2 + (r - 1) * 8 + m]);
+                bdft4(v[0], v[1], v[2], v[3]);
+                const int base = (b >> 3) * 32 + m;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) fb[an_pad(base + 8 * r)] = v[r];
+            }
+        }
+        __syncthreads();
+        // stage 3 (R = 5, Ns = 32): 160 butterflies, fb -> fa
+        if (t < 160) {
+            float2 v[5];
+#pragma unroll
+            for (int r = 0; r < 5; ++r) v[r] = fb[an_pad(t + 160 * r)];
+            const int m = t & 31;
+#pragma unroll
+            for (int r = 1; r < 5; ++r) v[r] = c_mul(v[r], tw[AN_TW3 + (r - 1) * 32 + m]);
+            bdft5(v);
+            const int base = (t >> 5) * 160 + m;
+#pragma unroll
+            for (int r = 0; r < 5; ++r) fa[an_pad(base + 32 * r)] = v[r];
+        }
+        __syncthreads();
+        // stage 4 (R = 5, Ns = 160): outputs k = t + 160 r, natural order, to HBM
+        if (t < 160) {
+            float2 v[5];
+#pragma unroll
+            for (int r = 0; r < 5; ++r) v[r] = fa[an_pad(t + 160 * r)];
+#pragma unroll
+            for (int r = 1; r < 5; ++r) v[r] = c_mul(v[r], tw[AN_TW4 + (r - 1) * 160 + t]);
+            bdft5(v);
+            float2 *yo = Y + (size_t)j * M;
+#pragma unroll
+            for (int r = 0; r < 5; ++r) yo[t + 160 * r] = v[r];
+        }
+        // block j + 1's stage 1 writes the other frame; its stage 2 (after the next barrier) is the
+        // first to touch this one again
+    }
+}
+
 // y[k][n] for 64 channels x RS_T outputs: v rows staged (rotated) in LDS, one lane per channel,
 // so an output's taps are wave-uniform: the phase-major table gT[rho][q] comes in by scalar loads
 // and the Q-tap loop is unrolled; the tile is transposed through LDS for row-contiguous stores.
@@ -131,6 +346,69 @@ __global__ __launch_bounds__(256) void k_pfb_resamp(const float2 *__restrict__ Y
     for (int e = tid; e < RS_C * RS_T; e += 256) {
         const int c = e / RS_T, o = e - c * RS_T, k = k0 + c, n = n0 + o;
         if (k < M && n < n1) y[(size_t)k * n_keep + n] = vt[c * (RS_T + 1) + o];
+    }
+}
+
+// The same resampler with the rate pair fixed at compile time (UP / DOWN = 72 kHz / carrier rate):
+// output n = UP m + o uses rows DOWN m + lo(o) .. + Q - 1 with lo(o) = floor(DOWN o / UP) and taps
+// g[rho(o) + UP q], rho(o) = DOWN o mod UP -- all compile-time for o < UP.  A lane owns one carrier
+// and one group of UP outputs: it streams the group's DOWN (UP-1)/UP + Q rows once (row loads are
+// 64 consecutive carriers = 512 contiguous bytes per wave), and every row feeds the outputs whose
+// window holds it, with the tap a wave-uniform scalar operand.  Each tap of g is used exactly once
+// per group, so a group is Lg FMAs per component with no LDS on the input side; LDS only transposes
+// the [carrier][output] tile for row-contiguous stores.
+template <int UP, int DOWN, int Q>
+__global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict__ Y, int M, int nblk,
+                                                        const float *__restrict__ g, float2 *__restrict__ y,
+                                                        int n_keep) {
+    constexpr int ROWS = (DOWN * (UP - 1)) / UP + Q;   // rows of one output group
+    constexpr int OT = 4 * UP;                          // outputs per workgroup (4 waves x one group)
+    __shared__ float2 tile[RS_C * (OT + 1)];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int k = min(blockIdx.x * RS_C + lane, M - 1);
+    const int m = blockIdx.y * 4 + wv;                  // output group: outputs UP m .. UP m + UP - 1
+    const long r0 = (long)DOWN * m;
+    float ar[UP], ai[UP];
+#pragma unroll
+    for (int o = 0; o < UP; ++o) ar[o] = ai[o] = 0.f;
+    constexpr int RB = 17;   // rows in flight per batch
+#pragma unroll
+    for (int i0 = 0; i0 < ROWS; i0 += RB) {
+        float2 v[RB];
+#pragma unroll
+        for (int b = 0; b < RB; ++b) {
+            if (i0 + b < ROWS) {
+                const long row = min(r0 + i0 + b, (long)nblk - 1);   // clamped rows feed only n >= n_keep
+                v[b] = Y[(size_t)row * M + k];
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < RB; ++b) {
+            const int i = i0 + b;
+            if (i < ROWS) {
+                // v_k[row] = (-i)^{(k row) mod 4} Y_row[k]
+                const int q = (int)(((long)k * (r0 + i)) & 3);
+                const float a = (q & 1) ? v[b].y : v[b].x, bb = (q & 1) ? -v[b].x : v[b].y;
+                const float vr = (q & 2) ? -a : a, vi = (q & 2) ? -bb : bb;
+#pragma unroll
+                for (int o = 0; o < UP; ++o) {
+                    const int lo = (DOWN * o) / UP, rho = (DOWN * o) % UP;
+                    if (i >= lo && i <= lo + Q - 1) {
+                        const float w = g[rho + UP * (lo + Q - 1 - i)];
+                        ar[o] = fmaf(w, vr, ar[o]);
+                        ai[o] = fmaf(w, vi, ai[o]);
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 0; o < UP; ++o) tile[lane * (OT + 1) + wv * UP + o] = make_float2(ar[o], ai[o]);
+    __syncthreads();
+    const int k0 = blockIdx.x * RS_C, n0 = blockIdx.y * OT;
+    for (int e = tid; e < RS_C * OT; e += 256) {
+        const int c = e / OT, o = e - c * OT, kk = k0 + c, n = n0 + o;
+        if (kk < M && n < n_keep) y[(size_t)kk * n_keep + n] = tile[c * (OT + 1) + o];
     }
 }
 
@@ -283,16 +561,50 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
     float2 *yd = (float2 *)st.out(y, (size_t)M * n_keep * 8);
     float2 *u = (float2 *)ws(ctx, S_W8, (size_t)nblk * M * 8);
     if (Q != 45 || P->up > 32) return tetra_fail(ctx, TETRA_E_INVALID, "resampler built for Lg / up = 45 taps");
-    float *taps = (float *)ws(ctx, S_W9, (size_t)(L + P->up * RS_QP) * 4);
+    const bool fixed = P->up == 18 && P->down == 25;   // 100 kHz -> 72 kHz (the 20 MSps / 800 plan)
+    float *taps = (float *)ws(ctx, S_W9, (size_t)(L + P->up * RS_QP + P->Lg + 2 + 2 * AN_TWN) * 4);
     if (!xd || !yd || !u || !taps) return st.finish();
-    // h, then g phase-major: gT[rho][q] = g[rho + up q] (zero-padded to RS_QP)
+    // h, then g phase-major: gT[rho][q] = g[rho + up q] (zero-padded to RS_QP), then g as given
     ctx->taps_wb.assign(P->h, P->h + L);
     ctx->taps_wb.resize((size_t)L + P->up * RS_QP, 0.f);
     for (int rho = 0; rho < P->up; ++rho)
         for (int q = 0; q < Q; ++q) ctx->taps_wb[L + rho * RS_QP + q] = P->g[rho + P->up * q];
-    HIP_TRY(ctx, hipMemcpyAsync(taps, ctx->taps_wb.data(), ctx->taps_wb.size() * 4, hipMemcpyHostToDevice,
-                                ctx->stream));
-    {
+    ctx->taps_wb.insert(ctx->taps_wb.end(), P->g, P->g + P->Lg);
+    const bool fused = M == AN_M && P->P <= 4;   // fold + FFT in one pass (k_pfb_analysis)
+    const size_t tw_off = ctx->taps_wb.size() + (ctx->taps_wb.size() & 1);   // float2-aligned
+    if (fused) {   // backward twiddles e^{+2 pi i m r / (Ns R)}, r-major per stage
+        ctx->taps_wb.resize(tw_off + 2 * AN_TWN, 0.f);
+        auto put = [&](int off, int ns, int R) {
+            for (int r = 1; r < R; ++r)
+                for (int m = 0; m < ns; ++m) {
+                    const double a = 2.0 * 3.14159265358979323846 * m * r / (ns * R);
+                    ctx->taps_wb[tw_off + 2 * (off + (r - 1) * ns + m)] = (float)cos(a);
+                    ctx->taps_wb[tw_off + 2 * (off + (r - 1) * ns + m) + 1] = (float)sin(a);
+                }
+        };
+        put(AN_TW2, 8, 4);
+        put(AN_TW3, 32, 5);
+        put(AN_TW4, 160, 5);
+    }
+    if (ctx->taps_wb_dev != taps || ctx->taps_wb_up != ctx->taps_wb) {   // upload only on change
+        ctx->taps_wb_up = ctx->taps_wb;
+        HIP_TRY(ctx, hipMemcpyAsync(taps, ctx->taps_wb_up.data(), ctx->taps_wb_up.size() * 4, hipMemcpyHostToDevice,
+                                    ctx->stream));
+        ctx->taps_wb_dev = taps;
+    }
+    if (fused) {
+        PROF(ctx, "wb_analysis");
+        // one round of workgroups (four per CU at <= 53 KB LDS) when the capture allows, >= 16
+        // blocks each (the L-sample window each workgroup loads first is its overhead)
+        const int jb = std::max<int>(16, (int)((nblk + 4 * 256 - 1) / (4 * 256)));
+        const unsigned grid = (unsigned)((nblk + jb - 1) / jb);
+        switch (P->P) {
+#define AN(PP) case PP: hipLaunchKernelGGL(k_pfb_analysis<PP>, dim3(grid), dim3(AN_T), 0, ctx->stream, (const float4 *)xd, (int)nblk, jb, taps, (const float2 *)(taps + tw_off), u); break;
+            AN(1) AN(2) AN(3) AN(4)
+#undef AN
+        }
+        HIP_TRY(ctx, hipGetLastError());
+    } else {
         PROF(ctx, "wb_fold");
         constexpr int JB = 16;
         const dim3 gr((unsigned)((M + 255) / 256), (unsigned)((nblk + JB - 1) / JB));
@@ -303,12 +615,18 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
         }
         HIP_TRY(ctx, hipGetLastError());
     }
-    {
+    if (!fused) {
         PROF(ctx, "wb_fft");
         rc = fft_backward(ctx, M, nblk, 1, M, 1, M, u, u);
         if (rc) return rc;
     }
-    {
+    if (fixed) {
+        PROF(ctx, "wb_resamp");
+        const dim3 gr((unsigned)((M + RS_C - 1) / RS_C), (unsigned)((n_keep + 4 * 18 - 1) / (4 * 18)));
+        hipLaunchKernelGGL((k_pfb_resamp_fix<18, 25, 45>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk,
+                           taps + L + P->up * RS_QP, yd, (int)n_keep);
+        HIP_TRY(ctx, hipGetLastError());
+    } else {
         PROF(ctx, "wb_resamp");
         const int rows = (int)(((long)P->down * (RS_T - 1)) / P->up) + Q + 1;
         const size_t lds = (size_t)std::max(rows * RS_C, RS_C * (RS_T + 1)) * 8;
@@ -341,6 +659,7 @@ int tetra_synth_wideband(tetra_ctx *ctx, const tetra_wb_plan *P, size_t Nw, uint
     if (!xd || !W || !taps) return st.finish();
     ctx->taps_wb.assign(P->h, P->h + L);
     HIP_TRY(ctx, hipMemcpyAsync(taps, ctx->taps_wb.data(), (size_t)L * 4, hipMemcpyHostToDevice, ctx->stream));
+    ctx->taps_wb_dev = nullptr;   // slot S_W9 now holds only h
     // W[j][r] = sum_k s[k][j] e^{+i 2 pi k r / M}: input stride nbb between carriers, 1 between j
     rc = fft_backward(ctx, M, nbb, nbb, 1, 1, M, s, W);
     if (rc) return rc;

@@ -184,12 +184,13 @@ class BenchStep:
 
     def stage_bytes(self):
         """Algorithmic bytes per wideband input sample of each timed stage (cf32 = 8 B):
-        fold reads x and writes Y (M per D samples), the FFT reads and writes Y, the resampler reads
+        the fused analysis (M = 800) and the fold read x and write Y (M per D samples), the FFT reads and writes Y, the resampler reads
         Y and writes y (M carriers at 72 kHz), the timing stage reads y and writes per symbol an
         8 B symbol, 2 soft bits and a hard dibit.  bench.py reports the slowest of them."""
         M, D, fs = self.plan.M, self.plan.D, self.fs
         yb = 8.0 * M * 72000.0 / fs
         return {"waterfall": (12.0 * self.nfr * 2048 / self.Nw, "k_waterfall"),
+                "wb_analysis": (8.0 + 8.0 * M / D, "k_pfb_analysis"),   # fused fold + FFT: x in, Y out
                 "wb_fold": (8.0 + 8.0 * M / D, "k_pfb_fold"), "wb_fft": (2 * 8.0 * M / D, None),
                 "wb_resamp": (8.0 * M / D + yb, "k_pfb_resamp"),
                 "etsi_timing": (yb + 11.0 * M * 18000.0 / fs, "k_timing")}
