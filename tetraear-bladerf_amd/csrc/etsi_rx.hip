@@ -660,8 +660,8 @@ __global__ __launch_bounds__(64 * SYNC_WAVES) void k_etsi_sync(const uint8_t *__
 // New state n = 4q + m has predecessors p = n>>1 = 2q + (m>>1), in lane q>>1 at local index
 // 2(q&1) + (m>>1), and p|8, in lane 2 + (q>>1) at the same index: each step a lane reads the four
 // metrics of both source lanes with quad-permute DPP and keeps the pair it needs.  The quad gathers
-// (descramble + deinterleave) into one shared LDS row; each lane stores its 4 decision bits as one
-// byte of the step's 32-bit survivor word ([step][job], coalesced); all four lanes trace back (same
+// (descramble + deinterleave) into one shared LDS row; each lane packs its 4 decision bits of 8
+// steps into one survivor dword ([group][job][lane], coalesced); all four lanes trace back (same
 // path) and lane 0 writes the block with the CRC accumulated on the fly.  16 blocks per 64-lane
 // workgroup keep LDS at 7 KB, so Viterbi workgroups fit beside the demod's on a CU.
 constexpr int VROW = 436;   // LDS row per block: 432 type-3 values, padded to 109 dwords (bank spread)
@@ -671,40 +671,47 @@ __device__ __forceinline__ int32_t quad_perm(int32_t v) {
     return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
 }
 
-template <int PAIRS>
-__device__ __forceinline__ void acs_pairs4(int32_t (&pm)[4], int q, const int8_t *row, uint8_t *sv, size_t sstride) {
+// Survivors: a lane packs its 4 decision bits of 8 consecutive steps into one dword (bit
+// 4 (t & 7) + m for state 4q + m at step t) and stores it once per 8 steps, [group][job][lane]:
+// one coalesced 256-B store per wave per 8 steps instead of eight byte stores.
+template <int GROUPS>
+__device__ __forceinline__ void acs_groups4(int32_t (&pm)[4], int q, const int8_t *row, uint32_t *sv, size_t gstride) {
     // rate-2/3 puncturing: step 2g sees mother outputs (g1, g2) = type-3 (3g, 3g+1); step 2g+1 sees
     // g1 = type-3 3g+2; the other mother outputs are erased.
     const bool odd = q & 1;
     const bool flip = ((q ^ (q >> 1)) & 1) != 0;   // d1 ^ d2 of this lane's states
-    for (int g = 0; g < PAIRS; ++g) {
-        const int32_t a = row[3 * g], b = row[3 * g + 1], c = row[3 * g + 2];
-        const int32_t be = flip ? -b : b;
+    for (int gi = 0; gi < GROUPS; ++gi) {
+        uint32_t word = 0;
 #pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            int32_t A[4], B[4];
+        for (int g4 = 0; g4 < 4; ++g4) {
+            const int g = 4 * gi + g4;
+            const int32_t a = row[3 * g], b = row[3 * g + 1], c = row[3 * g + 2];
+            const int32_t be = flip ? -b : b;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                A[i] = quad_perm<0x50 /* [0,0,1,1] */>(pm[i]);   // lane q>>1
-                B[i] = quad_perm<0xFA /* [2,2,3,3] */>(pm[i]);   // lane 2 + (q>>1)
+            for (int half = 0; half < 2; ++half) {
+                int32_t A[4], B[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    A[i] = quad_perm<0x50 /* [0,0,1,1] */>(pm[i]);   // lane q>>1
+                    B[i] = quad_perm<0xFA /* [2,2,3,3] */>(pm[i]);   // lane 2 + (q>>1)
+                }
+                const int32_t X0 = odd ? A[2] : A[0], X1 = odd ? A[3] : A[1];
+                const int32_t Y0 = odd ? B[2] : B[0], Y1 = odd ? B[3] : B[1];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const int bb = m & 1, d0 = (m >> 1) & 1;
+                    // branch metric for d3 = 0; d3 = 1 flips every generator output (negates it)
+                    int32_t v;
+                    if (half == 0) v = ((bb ^ d0) ? -a : a) + (bb ? -be : be);
+                    else v = (bb ^ d0) ? -c : c;
+                    const int32_t m0 = ((m >> 1) ? X1 : X0) + v, m1 = ((m >> 1) ? Y1 : Y0) - v;
+                    const bool t1 = m1 > m0;
+                    pm[m] = t1 ? m1 : m0;
+                    word |= (uint32_t)t1 << (4 * (2 * g4 + half) + m);
+                }
             }
-            const int32_t X0 = odd ? A[2] : A[0], X1 = odd ? A[3] : A[1];
-            const int32_t Y0 = odd ? B[2] : B[0], Y1 = odd ? B[3] : B[1];
-            uint32_t bits = 0;
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const int bb = m & 1, d0 = (m >> 1) & 1;
-                // branch metric for d3 = 0; d3 = 1 flips every generator output (negates it)
-                int32_t v;
-                if (half == 0) v = ((bb ^ d0) ? -a : a) + (bb ? -be : be);
-                else v = (bb ^ d0) ? -c : c;
-                const int32_t m0 = ((m >> 1) ? X1 : X0) + v, m1 = ((m >> 1) ? Y1 : Y0) - v;
-                const bool t1 = m1 > m0;
-                pm[m] = t1 ? m1 : m0;
-                bits |= (uint32_t)t1 << m;
-            }
-            sv[(size_t)(2 * g + half) * sstride] = (uint8_t)bits;
         }
+        sv[(size_t)gi * gstride] = word;
     }
 }
 
@@ -750,27 +757,41 @@ __device__ __forceinline__ void viterbi_wave(int8_t *rows, const Job *__restrict
     int32_t pm[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) pm[m] = (q == 0 && m == 0) ? 0 : -(1 << 28);
-    uint32_t *sv = surv + j;
+    const size_t gstride = 4 * ss;   // dwords between survivor groups
+    uint32_t *sv = surv + 4 * j + q;
     if (act) {
-        acs_pairs4<P.n2 / 2>(pm, q, row, reinterpret_cast<uint8_t *>(sv) + q, 4 * ss);
-        __threadfence_block();   // the other lanes' survivor bytes are read below
-        // traceback from state 0 (tail bits), CRC over type-1 + CRC bits on the fly
+        constexpr int NG = P.n2 / 8;   // n2 is a multiple of 8
+        acs_groups4<NG>(pm, q, row, sv, gstride);
+        __threadfence_block();   // the quad's survivor words are read back below (same wave)
+        // traceback from state 0 (tail bits), CRC over type-1 + CRC bits on the fly.  The words do
+        // not depend on the state: each lane loads its own for 8 groups (64 steps) at a time, the
+        // quad broadcasts them (DPP), and a step only selects lane s2 >> 2's word.
         constexpr int L = P.n1 + 16;
         uint32_t c = CRC_TAB.init[L];
         int s2 = 0;
         uint8_t *op = type1 + ((size_t)jb.ch * ETSI_MAXJ + jb.slot) * 268;
-        for (int t0 = P.n2 - 1; t0 >= 0; t0 -= 8) {   // n2 is a multiple of 8
+        for (int g0 = NG - 1; g0 >= 0; g0 -= 8) {
             uint32_t w[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) w[u] = sv[(size_t)(t0 - u) * ss];   // independent of the state
+            for (int u = 0; u < 8; ++u) w[u] = g0 - u >= 0 ? sv[(size_t)(g0 - u) * gstride] : 0u;
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                const int t = t0 - u;
-                const int bit = s2 & 1;
-                if (q == 0 && t < P.n1) op[t] = (uint8_t)bit;
-                if (bit && t < L) c ^= CRC_TAB.t[L - 1 - t];
-                // state s2's decision: byte s2 >> 2 (lane), bit s2 & 3
-                s2 = (s2 >> 1) | ((int)((w[u] >> (8 * (s2 >> 2) + (s2 & 3))) & 1u) << 3);
+                const int gi = g0 - u;
+                if (gi < 0) break;
+                const int32_t wi = (int32_t)w[u];
+                const uint32_t w0 = (uint32_t)quad_perm<0x00>(wi), w1 = (uint32_t)quad_perm<0x55>(wi),
+                               w2 = (uint32_t)quad_perm<0xAA>(wi), w3 = (uint32_t)quad_perm<0xFF>(wi);
+#pragma unroll
+                for (int st = 7; st >= 0; --st) {
+                    const int t = 8 * gi + st;
+                    const int bit = s2 & 1;
+                    if (q == 0 && t < P.n1) op[t] = (uint8_t)bit;
+                    if (bit && t < L) c ^= CRC_TAB.t[L - 1 - t];
+                    // state s2's decision: lane s2 >> 2, bit 4 st + (s2 & 3)
+                    const int ln = s2 >> 2;
+                    const uint32_t ww = ln & 2 ? (ln & 1 ? w3 : w2) : (ln & 1 ? w1 : w0);
+                    s2 = (s2 >> 1) | ((int)((ww >> (4 * st + (s2 & 3))) & 1u) << 3);
+                }
             }
         }
         if (q == 0) {
@@ -1132,7 +1153,8 @@ int tetra_lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard,
     int32_t *ko = (int32_t *)st.out(blocks, C * ETSI_MAXJ * 4 * 4);
     uint8_t *to = (uint8_t *)st.out(type1, C * ETSI_MAXJ * 268);
     const size_t jtot = 32 * C;   // the three job regions (job_base / job_cap)
-    // workspace: [job counters per kind (16 B)] [jobs] [survivors: 288 steps x jtot x 32 bits]
+    // workspace: [job counters per kind (16 B)] [jobs] [survivors: 36 groups x jtot x 4 lanes x 32 bits
+    // (SCH/F: 288 steps / 8; allocated as 288 x jtot dwords)]
     char *w = (char *)ws(ctx, S_W7, 16 + jtot * sizeof(Job) + 288 * jtot * 4);
     if (!sb || !hd || !ns || !nbo || !bo || !nko || !ko || !to || !w) return st.finish();
     unsigned long long *jcount = (unsigned long long *)w;
