@@ -192,7 +192,7 @@ class BenchStep:
         return {"waterfall": (12.0 * self.nfr * 2048 / self.Nw, "k_waterfall"),
                 "wb_analysis": (8.0 + 8.0 * M / D, "k_pfb_analysis"),   # fused fold + FFT: x in, Y out
                 "wb_fold": (8.0 + 8.0 * M / D, "k_pfb_fold"), "wb_fft": (2 * 8.0 * M / D, None),
-                "wb_resamp": (8.0 * M / D + yb, "k_pfb_resamp"),
+                "wb_resamp": (8.0 * M / D + yb, "k_pfb_resamp_fix"),
                 "etsi_timing": (yb + 11.0 * M * 18000.0 / fs, "k_timing")}
 
     def config(self, world):
@@ -206,7 +206,7 @@ class BenchStep:
         return value_msps * 1e6 / self.fs * self.plan.M   # carriers served at real time
 
     def workload_key(self):
-        return f"C3 {self.Nw} wideband"
+        return f"C3: {self.Nw} samples"   # a substring of config()["workload"]
 
     def cpu_baseline(self, budget_s):
         import os
