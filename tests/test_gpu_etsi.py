@@ -220,3 +220,55 @@ def test_demod_lengths_vs_oracle(N, fmt):
         assert n == len(so), (N, ch)
         assert np.array_equal(sym[ch, :n], so) and np.array_equal(hard[ch, :max(n - 1, 0)], ho)
         assert np.array_equal(soft[ch, :2 * max(n - 1, 0)], sbo)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [0, 1, 2, 47, 48, 400, 3300, 3301, 3500])
+def test_process_edge_lengths(N):
+    """process() on empty, one-sample, sub-filter and barely-demodulable chunks: the same symbols
+    as the oracle (empty where the oracle has none), never an exception -- the reference's
+    process() returns an empty uint8 array for an empty chunk (processor.py:239-241)."""
+    from tetraear.signal import SignalProcessor
+    x = (0.2 * np.random.default_rng(N).standard_normal(N) + 0j).astype(np.complex64)
+    p = SignalProcessor(2.4e6, mode="etsi")
+    hard = p.process(x)
+    assert hard.dtype == np.uint8
+    so, sbo, ho, _ = E.Receiver().demod(x[:N - N % 2])
+    if len(so) < 2:
+        assert len(hard) == 0
+    else:
+        assert np.array_equal(np.asarray(hard), ho) and np.array_equal(p.symbols, so)
+        assert np.array_equal(hard.soft_bits, sbo)
+
+
+@pytest.mark.gpu
+def test_lower_mac_empty_and_low_snr():
+    """The lower MAC beside channels with no symbols (0 and 1): those give no bursts; two channels
+    demodulated at 6 dB Es/N0 (marginal: bursts found, CRCs failing) match the oracle block
+    for block."""
+    from tetraear.core.etsi import EtsiLowerMac
+    from tetraear.signal.etsi import synth, EtsiReceiver
+    iq, cells2, _, _, _ = synth(2, 131072, seed=21, snr_db=6.0)
+    h2, s2, _, n2 = EtsiReceiver().demod_batch(iq)
+    sm = h2.shape[1]
+    hard = np.concatenate([np.zeros((2, sm), np.uint8), h2])
+    soft = np.concatenate([np.zeros((2, 2 * sm), np.int8), s2])
+    ns = np.concatenate([np.array([0, 1], np.int32), n2])
+    cells = np.concatenate([np.array([3, 7], np.uint32), cells2])
+    res = EtsiLowerMac().decode_batch(soft, hard, ns, cells)
+    assert res[0] == [] and res[1] == []
+    rx = E.Receiver()
+    nfail = nblk = 0
+    for ch in (2, 3):
+        n = int(ns[ch])
+        want = rx.lower_mac(soft[ch, :2 * (n - 1)], hard[ch, :n - 1], int(cells[ch]))
+        got = res[ch]
+        assert len(got) == len(want)
+        for f, (start, bk, blocks) in zip(got, want):
+            assert f["position"] == start and f["burst_kind"] == bk
+            assert [b["crc_ok"] for b in f["blocks"]] == [bool(ok) for _, _, ok in blocks]
+            for b, (_, t1, _) in zip(f["blocks"], blocks):
+                assert np.array_equal(b["bits"], t1)
+                nblk += 1
+                nfail += not b["crc_ok"]
+    assert nblk > 0
