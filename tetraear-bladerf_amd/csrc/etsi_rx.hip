@@ -656,10 +656,7 @@ __global__ __launch_bounds__(64 * SYNC_WAVES) void k_etsi_sync(const uint8_t *__
 }
 
 // --------------------------------------------------------------------------- E4 Viterbi
-// Four LANES per coded block (one DPP quad): lane q holds the path metrics of states 4q..4q+3.
-// New state n = 4q + m has predecessors p = n>>1 = 2q + (m>>1), in lane q>>1 at local index
-// 2(q&1) + (m>>1), and p|8, in lane 2 + (q>>1) at the same index: each step a lane reads the four
-// metrics of both source lanes with quad-permute DPP and keeps the pair it needs.  The quad gathers
+// Four LANES per coded block (one DPP quad) holding the 16 path metrics (layout below).  The quad gathers
 // (descramble + deinterleave) into one shared LDS row; each lane packs its 4 decision bits of 8
 // steps into one survivor dword ([group][job][lane], coalesced); all four lanes trace back (same
 // path) and lane 0 writes the block with the CRC accumulated on the fly.  16 blocks per 64-lane
@@ -671,43 +668,49 @@ __device__ __forceinline__ int32_t quad_perm(int32_t v) {
     return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
 }
 
+// Strided state layout: lane l of the quad holds states n = 4 i + l in pm[i].  New state n has
+// predecessors p0 = n >> 1 = 2 i + (l >> 1) (register i >> 1 of lane (2 i + (l >> 1)) & 3) and
+// p1 = p0 | 8 (register (i >> 1) + 2, same lane): for a given i both sit in one register of a lane
+// that one quad_perm pattern names, so each new metric takes two DPP moves and no selects.  The
+// branch-metric signs depend on n & 3 = l (lane constants) and on n >> 2 = i (compile time).
 // Survivors: a lane packs its 4 decision bits of 8 consecutive steps into one dword (bit
-// 4 (t & 7) + m for state 4q + m at step t) and stores it once per 8 steps, [group][job][lane]:
-// one coalesced 256-B store per wave per 8 steps instead of eight byte stores.
+// 4 (t & 7) + i for state 4 i + l at step t) and stores it once per 8 steps, [group][job][lane]:
+// one coalesced 256-B store per wave per 8 steps.
 template <int GROUPS>
 __device__ __forceinline__ void acs_groups4(int32_t (&pm)[4], int q, const int8_t *row, uint32_t *sv, size_t gstride) {
     // rate-2/3 puncturing: step 2g sees mother outputs (g1, g2) = type-3 (3g, 3g+1); step 2g+1 sees
     // g1 = type-3 3g+2; the other mother outputs are erased.
-    const bool odd = q & 1;
-    const bool flip = ((q ^ (q >> 1)) & 1) != 0;   // d1 ^ d2 of this lane's states
+    const bool bb = q & 1, d0 = (q >> 1) & 1;   // bits 0 and 1 of this lane's states
     for (int gi = 0; gi < GROUPS; ++gi) {
         uint32_t word = 0;
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
             const int g = 4 * gi + g4;
             const int32_t a = row[3 * g], b = row[3 * g + 1], c = row[3 * g + 2];
-            const int32_t be = flip ? -b : b;
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
-                int32_t A[4], B[4];
+                // branch metric for d3 = 0 (d3 = 1 negates every generator output):
+                // step 2g: +-a +-b (b's sign also flips with (n >> 2) ^ (n >> 3)); step 2g+1: +-c
+                int32_t v0, v1;
+                if (half == 0) {
+                    const int32_t sa = (bb ^ d0) ? -a : a, sb = bb ? -b : b;
+                    v0 = sa + sb;   // i with flip 0 (i = 0, 3)
+                    v1 = sa - sb;   // flip 1 (i = 1, 2)
+                } else {
+                    v0 = v1 = (bb ^ d0) ? -c : c;
+                }
+                const int32_t X0 = quad_perm<0x50>(pm[0]), Y0 = quad_perm<0x50>(pm[2]);
+                const int32_t X1 = quad_perm<0xFA>(pm[0]), Y1 = quad_perm<0xFA>(pm[2]);
+                const int32_t X2 = quad_perm<0x50>(pm[1]), Y2 = quad_perm<0x50>(pm[3]);
+                const int32_t X3 = quad_perm<0xFA>(pm[1]), Y3 = quad_perm<0xFA>(pm[3]);
+                const int32_t X[4] = {X0, X1, X2, X3}, Y[4] = {Y0, Y1, Y2, Y3};
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    A[i] = quad_perm<0x50 /* [0,0,1,1] */>(pm[i]);   // lane q>>1
-                    B[i] = quad_perm<0xFA /* [2,2,3,3] */>(pm[i]);   // lane 2 + (q>>1)
-                }
-                const int32_t X0 = odd ? A[2] : A[0], X1 = odd ? A[3] : A[1];
-                const int32_t Y0 = odd ? B[2] : B[0], Y1 = odd ? B[3] : B[1];
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const int bb = m & 1, d0 = (m >> 1) & 1;
-                    // branch metric for d3 = 0; d3 = 1 flips every generator output (negates it)
-                    int32_t v;
-                    if (half == 0) v = ((bb ^ d0) ? -a : a) + (bb ? -be : be);
-                    else v = (bb ^ d0) ? -c : c;
-                    const int32_t m0 = ((m >> 1) ? X1 : X0) + v, m1 = ((m >> 1) ? Y1 : Y0) - v;
+                    const int32_t v = ((i ^ (i >> 1)) & 1) ? v1 : v0;
+                    const int32_t m0 = X[i] + v, m1 = Y[i] - v;
                     const bool t1 = m1 > m0;
-                    pm[m] = t1 ? m1 : m0;
-                    word |= (uint32_t)t1 << (4 * (2 * g4 + half) + m);
+                    pm[i] = t1 ? m1 : m0;
+                    word |= (uint32_t)t1 << (4 * (2 * g4 + half) + i);
                 }
             }
         }
@@ -787,10 +790,10 @@ __device__ __forceinline__ void viterbi_wave(int8_t *rows, const Job *__restrict
                     const int bit = s2 & 1;
                     if (q == 0 && t < P.n1) op[t] = (uint8_t)bit;
                     if (bit && t < L) c ^= CRC_TAB.t[L - 1 - t];
-                    // state s2's decision: lane s2 >> 2, bit 4 st + (s2 & 3)
-                    const int ln = s2 >> 2;
+                    // state s2's decision: lane s2 & 3, bit 4 st + (s2 >> 2)
+                    const int ln = s2 & 3;
                     const uint32_t ww = ln & 2 ? (ln & 1 ? w3 : w2) : (ln & 1 ? w1 : w0);
-                    s2 = (s2 >> 1) | ((int)((ww >> (4 * st + (s2 & 3))) & 1u) << 3);
+                    s2 = (s2 >> 1) | ((int)((ww >> (4 * st + (s2 >> 2))) & 1u) << 3);
                 }
             }
         }
