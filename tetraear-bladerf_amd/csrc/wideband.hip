@@ -271,8 +271,13 @@ __global__ __launch_bounds__(AN_T) void k_pfb_analysis(const float4 *__restrict_
             for (int r = 1; r < 5; ++r) v[r] = c_mul(v[r], tw[AN_TW4 + (r - 1) * 160 + t]);
             bdft5(v);
             float2 *yo = Y + (size_t)j * M;
+            // the mixer term here, once per output: v_k[j] = (-i)^{(k j) mod 4} Y_j[k]
 #pragma unroll
-            for (int r = 0; r < 5; ++r) yo[t + 160 * r] = v[r];
+            for (int r = 0; r < 5; ++r) {
+                const int k = t + 160 * r, q = (k * (j & 3)) & 3;
+                const float a = (q & 1) ? v[r].y : v[r].x, bb = (q & 1) ? -v[r].x : v[r].y;
+                yo[k] = (q & 2) ? make_float2(-a, -bb) : make_float2(a, bb);
+            }
         }
         // block j + 1's stage 1 writes the other frame; its stage 2 (after the next barrier) is the
         // first to touch this one again
@@ -282,7 +287,7 @@ __global__ __launch_bounds__(AN_T) void k_pfb_analysis(const float4 *__restrict_
 // y[k][n] for 64 channels x RS_T outputs: v rows staged (rotated) in LDS, one lane per channel,
 // so an output's taps are wave-uniform: the phase-major table gT[rho][q] comes in by scalar loads
 // and the Q-tap loop is unrolled; the tile is transposed through LDS for row-contiguous stores.
-template <int Q>
+template <int Q, bool ROT>
 __global__ __launch_bounds__(256) void k_pfb_resamp(const float2 *__restrict__ Y, int M, int nblk, int up, int down,
                                                     const float *__restrict__ gT, float2 *__restrict__ y,
                                                     int n_keep) {
@@ -310,7 +315,7 @@ __global__ __launch_bounds__(256) void k_pfb_resamp(const float2 *__restrict__ Y
                 const int rr = r0 + 4 * b;
                 if (rr < rows) {
                     // z * (-i)^q, q = k i mod 4, branch-free: odd q swaps (re, im) -> (im, -re)
-                    const int q = (int)(((long)k * (ilo + rr)) & 3);
+                    const int q = ROT ? (int)(((long)k * (ilo + rr)) & 3) : 0;   // !ROT: rotated upstream
                     const float a = (q & 1) ? z[b].y : z[b].x, bb = (q & 1) ? -z[b].x : z[b].y;
                     vt[rr * RS_C + lane] = (q & 2) ? make_float2(-a, -bb) : make_float2(a, bb);
                 }
@@ -357,20 +362,47 @@ __global__ __launch_bounds__(256) void k_pfb_resamp(const float2 *__restrict__ Y
 // window holds it, with the tap a wave-uniform scalar operand.  Each tap of g is used exactly once
 // per group, so a group is Lg FMAs per component with no LDS on the input side; LDS only transposes
 // the [carrier][output] tile for row-contiguous stores.
+// Position of tap (row i, output o) in the use-ordered tap table gU (rows ascending, outputs
+// ascending within a row): the n-th FMA of a group reads tap n.  The table sits in LDS (810
+// floats): as scalar loads the compiler hoisted hundreds of taps and spilled SGPRs to VGPR lanes.
 template <int UP, int DOWN, int Q>
+struct ResampUse {
+    static constexpr int ROWS = (DOWN * (UP - 1)) / UP + Q;
+    int idx[ROWS][UP];
+    int n = 0;
+    constexpr ResampUse() : idx{} {
+        for (int i = 0; i < ROWS; ++i)
+            for (int o = 0; o < UP; ++o) {
+                const int lo = (DOWN * o) / UP;
+                idx[i][o] = (i >= lo && i <= lo + Q - 1) ? n++ : -1;
+            }
+    }
+};
+
+template <int UP, int DOWN, int Q, bool ROT>
 __global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict__ Y, int M, int nblk,
-                                                        const float *__restrict__ g, float2 *__restrict__ y,
+                                                        const float *__restrict__ gU, float2 *__restrict__ y,
                                                         int n_keep) {
-    constexpr int ROWS = (DOWN * (UP - 1)) / UP + Q;   // rows of one output group
+    using U = ResampUse<UP, DOWN, Q>;
+    constexpr U use{};
+    constexpr int ROWS = U::ROWS;                       // rows of one output group
     constexpr int OT = 4 * UP;                          // outputs per workgroup (4 waves x one group)
     __shared__ float2 tile[RS_C * (OT + 1)];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    __shared__ float tapL[use.n];   // taps in use order: each read is a same-address LDS broadcast
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int e = tid; e < use.n; e += 256) tapL[e] = gU[e];
     const int k = min(blockIdx.x * RS_C + lane, M - 1);
     const int m = blockIdx.y * 4 + wv;                  // output group: outputs UP m .. UP m + UP - 1
-    const long r0 = (long)DOWN * m;
-    float ar[UP], ai[UP];
+    const int r0 = DOWN * m;                            // wave-uniform: row offsets are scalar
+    // rows r0 .. r0 + ROWS - 1; a group reaching past nblk (the last ones) clamps its row index --
+    // clamped rows only feed outputs n >= n_keep, which are not stored
+    const float2 *base = Y + k;
+    __syncthreads();
+    typedef float pf2 __attribute__((ext_vector_type(2)));   // (re, im): one v_pk_fma_f32 per tap
+    pf2 acc[UP];
 #pragma unroll
-    for (int o = 0; o < UP; ++o) ar[o] = ai[o] = 0.f;
+    for (int o = 0; o < UP; ++o) acc[o] = pf2{0.f, 0.f};
     constexpr int RB = 17;   // rows in flight per batch
 #pragma unroll
     for (int i0 = 0; i0 < ROWS; i0 += RB) {
@@ -378,32 +410,33 @@ __global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict
 #pragma unroll
         for (int b = 0; b < RB; ++b) {
             if (i0 + b < ROWS) {
-                const long row = min(r0 + i0 + b, (long)nblk - 1);   // clamped rows feed only n >= n_keep
-                v[b] = Y[(size_t)row * M + k];
+                const int row = min(r0 + i0 + b, nblk - 1);
+                v[b] = base[(size_t)row * M];
             }
         }
 #pragma unroll
         for (int b = 0; b < RB; ++b) {
             const int i = i0 + b;
             if (i < ROWS) {
-                // v_k[row] = (-i)^{(k row) mod 4} Y_row[k]
-                const int q = (int)(((long)k * (r0 + i)) & 3);
-                const float a = (q & 1) ? v[b].y : v[b].x, bb = (q & 1) ? -v[b].x : v[b].y;
-                const float vr = (q & 2) ? -a : a, vi = (q & 2) ? -bb : bb;
+                // v_k[row] = (-i)^{(k row) mod 4} Y_row[k] (ROT: here; else k_pfb_analysis applied it)
+                pf2 vv = pf2{v[b].x, v[b].y};
+                if constexpr (ROT) {
+                    const int q = (k * ((r0 + i) & 3)) & 3;
+                    const float a = (q & 1) ? v[b].y : v[b].x, bb = (q & 1) ? -v[b].x : v[b].y;
+                    vv = (q & 2) ? pf2{-a, -bb} : pf2{a, bb};
+                }
 #pragma unroll
                 for (int o = 0; o < UP; ++o) {
-                    const int lo = (DOWN * o) / UP, rho = (DOWN * o) % UP;
-                    if (i >= lo && i <= lo + Q - 1) {
-                        const float w = g[rho + UP * (lo + Q - 1 - i)];
-                        ar[o] = fmaf(w, vr, ar[o]);
-                        ai[o] = fmaf(w, vi, ai[o]);
+                    if (use.idx[i][o] >= 0) {
+                        const float w = tapL[use.idx[i][o]];
+                        acc[o] = __builtin_elementwise_fma(pf2{w, w}, vv, acc[o]);   // = fmaf per component
                     }
                 }
             }
         }
     }
 #pragma unroll
-    for (int o = 0; o < UP; ++o) tile[lane * (OT + 1) + wv * UP + o] = make_float2(ar[o], ai[o]);
+    for (int o = 0; o < UP; ++o) tile[lane * (OT + 1) + wv * UP + o] = make_float2(acc[o].x, acc[o].y);
     __syncthreads();
     const int k0 = blockIdx.x * RS_C, n0 = blockIdx.y * OT;
     for (int e = tid; e < RS_C * OT; e += 256) {
@@ -569,7 +602,19 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
     ctx->taps_wb.resize((size_t)L + P->up * RS_QP, 0.f);
     for (int rho = 0; rho < P->up; ++rho)
         for (int q = 0; q < Q; ++q) ctx->taps_wb[L + rho * RS_QP + q] = P->g[rho + P->up * q];
-    ctx->taps_wb.insert(ctx->taps_wb.end(), P->g, P->g + P->Lg);
+    if (fixed) {   // k_pfb_resamp_fix's use-ordered table gU (see ResampUse)
+        constexpr ResampUse<18, 25, 45> use{};
+        std::vector<float> gU((size_t)use.n);
+        for (int i = 0; i < ResampUse<18, 25, 45>::ROWS; ++i)
+            for (int o = 0; o < 18; ++o)
+                if (use.idx[i][o] >= 0) {
+                    const int lo = (25 * o) / 18, rho = (25 * o) % 18;
+                    gU[use.idx[i][o]] = P->g[rho + 18 * (lo + 45 - 1 - i)];
+                }
+        ctx->taps_wb.insert(ctx->taps_wb.end(), gU.begin(), gU.end());
+    } else {
+        ctx->taps_wb.insert(ctx->taps_wb.end(), P->g, P->g + P->Lg);
+    }
     const bool fused = M == AN_M && P->P <= 4;   // fold + FFT in one pass (k_pfb_analysis)
     const size_t tw_off = ctx->taps_wb.size() + (ctx->taps_wb.size() & 1);   // float2-aligned
     if (fused) {   // backward twiddles e^{+2 pi i m r / (Ns R)}, r-major per stage
@@ -623,8 +668,12 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
     if (fixed) {
         PROF(ctx, "wb_resamp");
         const dim3 gr((unsigned)((M + RS_C - 1) / RS_C), (unsigned)((n_keep + 4 * 18 - 1) / (4 * 18)));
-        hipLaunchKernelGGL((k_pfb_resamp_fix<18, 25, 45>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk,
-                           taps + L + P->up * RS_QP, yd, (int)n_keep);
+        if (fused)   // Y already carries the mixer rotation
+            hipLaunchKernelGGL((k_pfb_resamp_fix<18, 25, 45, false>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk,
+                               taps + L + P->up * RS_QP, yd, (int)n_keep);
+        else
+            hipLaunchKernelGGL((k_pfb_resamp_fix<18, 25, 45, true>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk,
+                               taps + L + P->up * RS_QP, yd, (int)n_keep);
         HIP_TRY(ctx, hipGetLastError());
     } else {
         PROF(ctx, "wb_resamp");
@@ -632,7 +681,11 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
         const size_t lds = (size_t)std::max(rows * RS_C, RS_C * (RS_T + 1)) * 8;
         if (lds > 160 * 1024) return tetra_fail(ctx, TETRA_E_INVALID, "resampler tile does not fit LDS");
         const dim3 gr((unsigned)((M + RS_C - 1) / RS_C), (unsigned)((n_keep + RS_T - 1) / RS_T));
-        hipLaunchKernelGGL(k_pfb_resamp<45>, gr, dim3(256), lds, ctx->stream, u, M, (int)nblk, P->up, P->down,
+        if (fused)
+            hipLaunchKernelGGL((k_pfb_resamp<45, false>), gr, dim3(256), lds, ctx->stream, u, M, (int)nblk, P->up, P->down,
+                           taps + L, yd, (int)n_keep);
+        else
+            hipLaunchKernelGGL((k_pfb_resamp<45, true>), gr, dim3(256), lds, ctx->stream, u, M, (int)nblk, P->up, P->down,
                            taps + L, yd, (int)n_keep);
         HIP_TRY(ctx, hipGetLastError());
     }
