@@ -283,6 +283,13 @@ int tetra_synth_wideband(tetra_ctx *ctx, const tetra_wb_plan *plan, size_t Nw, u
 int tetra_waterfall(tetra_ctx *ctx, const void *iq, int iq_fmt, size_t C, size_t N, size_t nfft, size_t hop,
                     size_t nframes, float *out);
 
+/* ---------------------------------------------------------------- FFT resampler
+ * SignalProcessor.resample (/root/reference/tetraear/signal/processor.py:35-49 =
+ * scipy.signal.resample(x, num)): x [C][Nx] complex (TETRA_CF32 or TETRA_CF64) -> y [C][num] in the
+ * same precision; forward rocFFT, spectrum truncation / zero-padding with scipy's Nyquist
+ * split/join, inverse rocFFT, scale num/Nx folded in. */
+int tetra_resample(tetra_ctx *ctx, const void *x, int fmt, size_t C, size_t Nx, size_t num, void *y);
+
 #ifdef __cplusplus
 }
 #endif

@@ -99,6 +99,11 @@ struct ProfScope {
 #define PROF_CAT(a, b) PROF_CAT2(a, b)
 #define PROF(ctx, name) ProfScope PROF_CAT(prof_scope_, __LINE__)((ctx), (name))
 
+// Batched complex-to-complex rocFFT on the context stream (fft.hip): `inverse` = e^{+i}, unnormalised
+// both ways; `dbl` = double precision; plans cached per context.
+int fft_c2c(tetra_ctx *ctx, bool inverse, bool dbl, size_t len, size_t batch, size_t istride, size_t idist,
+            size_t ostride, size_t odist, void *in, void *out);
+
 static inline unsigned grid_for(size_t threads, unsigned block) {
     return (unsigned)((threads + block - 1) / block);
 }

@@ -21,9 +21,6 @@
 // stage dominates), and the resampler writes 8 B per 72 kHz output.
 #include "common.h"
 
-#include <rocfft/rocfft.h>
-
-#include <mutex>
 
 namespace {
 
@@ -484,80 +481,6 @@ __global__ __launch_bounds__(256) void k_pfb_synth(const float2 *__restrict__ W,
     x[n] = make_float2(ar, ai);
 }
 
-// ------------------------------------------------------------------------------------ rocFFT
-struct FftPlan {
-    size_t M, batch, istride, idist, ostride, odist;
-    bool inplace;
-    rocfft_plan plan;
-    rocfft_execution_info info;
-    size_t work;
-};
-struct FftCache {
-    std::vector<FftPlan> plans;
-    DevBuf work;
-};
-
-void fft_free(void *p) {
-    auto *c = static_cast<FftCache *>(p);
-    for (auto &f : c->plans) {
-        rocfft_execution_info_destroy(f.info);
-        rocfft_plan_destroy(f.plan);
-    }
-    if (c->work.p) (void)hipFree(c->work.p);
-    delete c;
-}
-
-std::once_flag g_fft_once;
-
-// Batched length-M backward (e^{+i}) single-precision complex transform, unnormalised.
-int fft_backward(tetra_ctx *ctx, size_t M, size_t batch, size_t istride, size_t idist, size_t ostride, size_t odist,
-                 void *in, void *out) {
-    std::call_once(g_fft_once, [] { rocfft_setup(); });
-    if (!ctx->fft) {
-        ctx->fft = new FftCache();
-        ctx->fft_free = fft_free;
-    }
-    auto *cache = static_cast<FftCache *>(ctx->fft);
-    const bool inplace = in == out;
-    FftPlan *fp = nullptr;
-    for (auto &f : cache->plans)
-        if (f.M == M && f.batch == batch && f.istride == istride && f.idist == idist && f.ostride == ostride &&
-            f.odist == odist && f.inplace == inplace)
-            fp = &f;
-    if (!fp) {
-        FftPlan f{M, batch, istride, idist, ostride, odist, inplace, nullptr, nullptr, 0};
-        rocfft_plan_description desc = nullptr;
-        if (rocfft_plan_description_create(&desc) != rocfft_status_success)
-            return tetra_fail(ctx, TETRA_E_HIP, "rocfft_plan_description_create failed");
-        const size_t is[1] = {istride}, os[1] = {ostride};
-        rocfft_status s = rocfft_plan_description_set_data_layout(
-            desc, rocfft_array_type_complex_interleaved, rocfft_array_type_complex_interleaved, nullptr, nullptr, 1, is,
-            idist, 1, os, odist);
-        const size_t len[1] = {M};
-        if (s == rocfft_status_success)
-            s = rocfft_plan_create(&f.plan, inplace ? rocfft_placement_inplace : rocfft_placement_notinplace,
-                                   rocfft_transform_type_complex_inverse, rocfft_precision_single, 1, len, batch, desc);
-        rocfft_plan_description_destroy(desc);
-        if (s != rocfft_status_success) return tetra_fail(ctx, TETRA_E_HIP, "rocfft_plan_create failed (%d)", (int)s);
-        rocfft_plan_get_work_buffer_size(f.plan, &f.work);
-        rocfft_execution_info_create(&f.info);
-        cache->plans.push_back(f);
-        fp = &cache->plans.back();
-    }
-    if (fp->work > cache->work.bytes) {
-        if (cache->work.p) HIP_TRY(ctx, hipFree(cache->work.p));
-        cache->work = DevBuf{};
-        HIP_TRY(ctx, hipMalloc(&cache->work.p, fp->work));
-        cache->work.bytes = fp->work;
-    }
-    if (fp->work) rocfft_execution_info_set_work_buffer(fp->info, cache->work.p, fp->work);
-    rocfft_execution_info_set_stream(fp->info, ctx->stream);
-    void *ib[1] = {in}, *ob[1] = {out};
-    if (rocfft_execute(fp->plan, ib, inplace ? nullptr : ob, fp->info) != rocfft_status_success)
-        return tetra_fail(ctx, TETRA_E_HIP, "rocfft_execute failed");
-    return TETRA_OK;
-}
-
 int wb_check(tetra_ctx *ctx, const tetra_wb_plan *P) {
     if (!P || !P->h || !P->g) return tetra_fail(ctx, TETRA_E_INVALID, "null wideband plan");
     if (P->M <= 0 || P->D <= 0 || P->M != 4 * P->D || P->P < 1 || P->P > 8)
@@ -662,7 +585,7 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
     }
     if (!fused) {
         PROF(ctx, "wb_fft");
-        rc = fft_backward(ctx, M, nblk, 1, M, 1, M, u, u);
+        rc = fft_c2c(ctx, true, false, M, nblk, 1, M, 1, M, u, u);
         if (rc) return rc;
     }
     if (fixed) {
@@ -714,7 +637,7 @@ int tetra_synth_wideband(tetra_ctx *ctx, const tetra_wb_plan *P, size_t Nw, uint
     HIP_TRY(ctx, hipMemcpyAsync(taps, ctx->taps_wb.data(), (size_t)L * 4, hipMemcpyHostToDevice, ctx->stream));
     ctx->taps_wb_dev = nullptr;   // slot S_W9 now holds only h
     // W[j][r] = sum_k s[k][j] e^{+i 2 pi k r / M}: input stride nbb between carriers, 1 between j
-    rc = fft_backward(ctx, M, nbb, nbb, 1, 1, M, s, W);
+    rc = fft_c2c(ctx, true, false, M, nbb, nbb, 1, 1, M, s, W);
     if (rc) return rc;
     // per-carrier Es/N0 as tetra_synth_etsi defines it (amplitude 0.5, fs/18000 samples per symbol)
     const float amp = 0.5f;

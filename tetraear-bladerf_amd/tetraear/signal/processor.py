@@ -125,10 +125,25 @@ class SignalProcessor:
 
     # --------------------------------------------------------------- component methods
     def resample(self, samples, target_rate):
-        """FFT resampling (processor.py:35-49) -- outside the hot path; delegates to scipy as the
-        reference does."""
-        new_n = int(len(samples) * target_rate / self.sample_rate)
-        return _design.resample(samples, new_n)
+        """FFT resampling (processor.py:35-49: scipy.signal.resample to int(len * target / fs)
+        samples) on the GPU: tetra_resample (rocFFT forward, scipy's spectrum truncation/padding
+        and Nyquist split/join, rocFFT inverse).  complex64 stays complex64, complex128 stays
+        complex128; real input runs the complex transform and returns the real part, which is
+        scipy's rfft path up to rounding."""
+        x = np.asarray(samples)
+        new_n = int(len(x) * target_rate / self.sample_rate)
+        if new_n <= 0 or len(x) == 0:
+            raise ValueError(f"resample: cannot resample {len(x)} samples to {new_n}")   # scipy errors too
+        real = not np.iscomplexobj(x)
+        if x.dtype in (np.complex64, np.float32, np.float16):
+            fmt, dt = _hip.TETRA_CF32, np.complex64
+        else:
+            fmt, dt = _hip.TETRA_CF64, np.complex128
+        xc = np.ascontiguousarray(x, dt)
+        y = np.empty(new_n, dt)
+        c = _hip.ctx()
+        c.check(c.lib.tetra_resample(c.handle, _hip.ptr(xc), fmt, 1, len(xc), new_n, _hip.ptr(y)), "tetra_resample")
+        return y.real.copy() if real else y
 
     def filter_signal(self, samples, bandwidth=25000, sample_rate=None):
         """Butterworth-4 filtfilt low-pass (processor.py:51-83), on the GPU."""
