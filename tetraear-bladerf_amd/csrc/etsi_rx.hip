@@ -249,7 +249,13 @@ __global__ __launch_bounds__(64) void k_timing(const float2 *__restrict__ yall, 
 // 20-dword lane stride is conflict-free for b128's lane groups).  Stage-1 outputs x240[k] go to a
 // linear buffer lin[k - kbase]; after each stage-2 burst the still-needed tail is moved to its
 // front (kbase = 10 u_done), so stage 2's operand reads are base + immediate offset.
-constexpr int S2_EVERY = 8;     // stage 2 runs every 8 tiles: ~205 output triples
+// Stage 2 runs every S2_EVERY tiles (cf32: 12 = ~307 output triples = 7.7 MFMA tiles for the 8
+// wave-pair slots; SC16: 8, whose 39 KB LDS budget for four workgroups per CU caps the stage-1
+// buffer).  Measured (same box, serial demod): cf32 every 12 tiles 1.486 ms against 1.514 ms every
+// 8, 1.515 every 10, 1.58 every 6, 1.67 every 4.
+template <typename In> struct CfCfg;
+template <> struct CfCfg<float4> { static constexpr int s2_every = 12, lr = 3336; };
+template <> struct CfCfg<uint2> { static constexpr int s2_every = 8, lr = 2312; };
 constexpr int TPP = 107;        // RRC taps per polyphase branch (Lp = 321 = 3 x 107)
 constexpr int PFD = 2;          // input tiles in flight per workgroup (register prefetch depth, pa/pb;
                                 // 3 and 4 measured no faster)
@@ -263,10 +269,13 @@ constexpr int YLDS = 4096;      // cf32: stage-2 outputs held in LDS before a fl
 constexpr int S2Q = 5;          // triples per column (rows 0..14; row 15 all-zero taps)
 constexpr int S2T = 8 * S2Q;    // triples per MFMA tile
 constexpr int S2K = 39;         // k-steps of 4: window 10 (S2Q - 1) + 114 = 154 -> 156 stage-1 outputs
-constexpr int LR = 2312;        // linear stage-1 buffer (float2)
+// linear stage-1 buffer (float2): S2_EVERY tiles of 256 outputs + the next triples' windows
+template <typename In> constexpr int cf_lr() { return CfCfg<In>::lr; }
 constexpr int XIN4 = (HALO + TILE_IN) / 2;   // float4 entries of the input image
-constexpr int CF_LDS4 = XIN4 + LR / 2;       // image + stage-1 buffer, in float4 (39,360 B)
-constexpr int CF_LDS2 = 2 * CF_LDS4;         // the same in float2 (SC16 fused: y + timing scratch)
+template <typename In> constexpr int cf_lds4() { return XIN4 + cf_lr<In>() / 2; }   // image + stage-1 buffer (float4)
+constexpr int CF_LDS2_SC16 = 2 * (XIN4 + CfCfg<uint2>::lr / 2);   // SC16 fused: y + timing scratch (float2)
+static_assert(XIN4 + CfCfg<uint2>::lr / 2 == 2460, "SC16 LDS: 39,360 B, four workgroups per CU");
+static_assert((XIN4 + CfCfg<float4>::lr / 2) * 16 + 4096 * 8 <= 80 * 1024, "cf32 LDS: two workgroups per CU");
 constexpr int CF_COEF = 64 + S2K * 64;       // device tap image: h1 (64) + A fragments [S2K][64 lanes]
 
 // Packed fp32 (v_pk_fma_f32): one real tap times a complex sample, each half a correctly rounded
@@ -309,6 +318,7 @@ __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, lon
     // bytes per sample and is bound by the workgroup's own LDS/issue chain instead, so it keeps
     // only the image and the stage-1 buffer (39 KB: four workgroups per CU) and sends y through
     // HBM/L2
+    constexpr int CF_LDS4 = cf_lds4<In>(), LR = cf_lr<In>(), S2_EVERY = CfCfg<In>::s2_every;
     __shared__ float4 lds[YL ? CF_LDS4 + YLDS / 2 : CF_LDS4];
     float4 *xin = lds;
     float2 *lin = reinterpret_cast<float2 *>(lds + XIN4);
@@ -453,7 +463,7 @@ __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, lon
         float2 *scr = reinterpret_cast<float2 *>(xin);
         if constexpr (!YL) {
             // y (this workgroup's stores) back into LDS, the timing scratch after it (the launch
-            // guarantees M2 + smax <= CF_LDS2).  Workgroup-scope fence: the stores and the loads
+            // guarantees M2 + smax <= CF_LDS2_SC16).  Workgroup-scope fence: the stores and the loads
             // share this CU's L1 (a device-scope fence would write back the whole L2 per channel).
             __threadfence_block();
             __syncthreads();
@@ -1076,7 +1086,7 @@ int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *i
     // fused: timing runs in the channel filter's workgroup on y in LDS (cf32: y never leaves LDS;
     // SC16: y round-trips through a C x M2 scratch and is re-staged into the freed image/ring)
     // (measured: cf32 with y through L2 at four workgroups per CU, as SC16 does, is 2.5 % slower)
-    const bool fuse = fmt == TETRA_SC16 ? M2 + sm <= CF_LDS2 : (M2 <= YLDS && sm <= 2 * XIN4);
+    const bool fuse = fmt == TETRA_SC16 ? M2 + sm <= CF_LDS2_SC16 : (M2 <= YLDS && sm <= 2 * XIN4);
     if (fuse) {
         float2 *ys = nullptr;
         if (fmt == TETRA_SC16 && !(ys = (float2 *)ws(ctx, S_W3, C * (size_t)M2 * 8))) return st.finish();
