@@ -577,9 +577,22 @@ __global__ __launch_bounds__(64 * SYNC_WAVES) void k_etsi_sync(const uint8_t *__
     const uint8_t *hp = hard + (size_t)ch * smax;
     // pack hard bits with ballots: 64 dibit symbols per step -> 2 words (bit 2i = b1, 2i+1 = b2)
     const int nsy = nbits / 2;
-    for (int s0 = 0; s0 < nsy + 64; s0 += 64) {
+    // symbols loaded 8 steps (512 symbols) at a time, all before the first ballot: a load per step
+    // in the dependent loop cost one memory latency per 64 symbols
+    constexpr int PK = 8;
+    for (int s00 = 0; s00 < nsy + 64; s00 += 64 * PK) {
+    uint32_t hb[PK];
+#pragma unroll
+    for (int u = 0; u < PK; ++u) {
+        const int s = s00 + 64 * u + lane;
+        hb[u] = hp[min(s, smax - 1)];   // unconditional (in the row): no branch join waits per load
+    }
+#pragma unroll
+    for (int u = 0; u < PK; ++u) {
+        const int s0 = s00 + 64 * u;
+        if (s0 >= nsy + 64) break;   // uniform
         const int s = s0 + lane;
-        const uint32_t h = s < nsy ? hp[s] : 0u;
+        const uint32_t h = s < nsy ? hb[u] : 0u;
         const uint64_t m1 = __ballot((h >> 1) & 1u), m2 = __ballot(h & 1u);
         auto spread = [](uint64_t x) {   // bit i -> bit 2i (32 -> 64)
             x &= 0xFFFFFFFFull;
@@ -594,6 +607,7 @@ __global__ __launch_bounds__(64 * SYNC_WAVES) void k_etsi_sync(const uint8_t *__
             words[s0 / 32] = spread(m1) | (spread(m2) << 1);
             words[s0 / 32 + 1] = spread(m1 >> 32) | (spread(m2 >> 32) << 1);
         }
+    }
     }
     __syncthreads();
     int nb = 0;
