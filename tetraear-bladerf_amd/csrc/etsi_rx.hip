@@ -249,12 +249,13 @@ __global__ __launch_bounds__(64) void k_timing(const float2 *__restrict__ yall, 
 // 20-dword lane stride is conflict-free for b128's lane groups).  Stage-1 outputs x240[k] go to a
 // linear buffer lin[k - kbase]; after each stage-2 burst the still-needed tail is moved to its
 // front (kbase = 10 u_done), so stage 2's operand reads are base + immediate offset.
-// Stage 2 runs every S2_EVERY tiles (cf32: 12 = ~307 output triples = 7.7 MFMA tiles for the 8
-// wave-pair slots; SC16: 8, whose 39 KB LDS budget for four workgroups per CU caps the stage-1
-// buffer).  Measured (same box, serial demod): cf32 every 12 tiles 1.486 ms against 1.514 ms every
-// 8, 1.515 every 10, 1.58 every 6, 1.67 every 4.
+// Stage 2 runs every S2_EVERY tiles (~205 output triples at 8).  Measured for cf32 (same box):
+// serial demod every 12 tiles (LR 3336, 79.6 KB) 0.8 % faster than every 8 (1.569 vs 1.581 ms;
+// 10 and 8 equal, 6 and 4 slower), but the pipelined step 0.7 % slower (1.694 vs 1.683 ms): at
+// 2 x 79.6 KB the CU has no LDS left for the lower MAC's 7 KB workgroups, which then wait for a
+// demod workgroup to retire.  The bench's pipelined step decides: 8 (16 KB free per CU).
 template <typename In> struct CfCfg;
-template <> struct CfCfg<float4> { static constexpr int s2_every = 12, lr = 3336; };
+template <> struct CfCfg<float4> { static constexpr int s2_every = 8, lr = 2312; };
 template <> struct CfCfg<uint2> { static constexpr int s2_every = 8, lr = 2312; };
 constexpr int TPP = 107;        // RRC taps per polyphase branch (Lp = 321 = 3 x 107)
 constexpr int PFD = 2;          // input tiles in flight per workgroup (register prefetch depth, pa/pb;
@@ -275,7 +276,7 @@ constexpr int XIN4 = (HALO + TILE_IN) / 2;   // float4 entries of the input imag
 template <typename In> constexpr int cf_lds4() { return XIN4 + cf_lr<In>() / 2; }   // image + stage-1 buffer (float4)
 constexpr int CF_LDS2_SC16 = 2 * (XIN4 + CfCfg<uint2>::lr / 2);   // SC16 fused: y + timing scratch (float2)
 static_assert(XIN4 + CfCfg<uint2>::lr / 2 == 2460, "SC16 LDS: 39,360 B, four workgroups per CU");
-static_assert((XIN4 + CfCfg<float4>::lr / 2) * 16 + 4096 * 8 <= 80 * 1024, "cf32 LDS: two workgroups per CU");
+static_assert((XIN4 + CfCfg<float4>::lr / 2) * 16 + 4096 * 8 <= 72 * 1024, "cf32 LDS: two workgroups per CU + 16 KB");
 constexpr int CF_COEF = 64 + S2K * 64;       // device tap image: h1 (64) + A fragments [S2K][64 lanes]
 
 // Packed fp32 (v_pk_fma_f32): one real tap times a complex sample, each half a correctly rounded

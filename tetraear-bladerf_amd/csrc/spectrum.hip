@@ -16,6 +16,8 @@
 // frame's LDS stages), stage 4 writes the shifted dB row to HBM with 4-byte coalesced stores.
 #include "common.h"
 
+#include <mutex>
+
 #pragma clang fp contract(fast)   // the spectrum is a tolerance product (oracle/spectrum.py), not a bit-exact one
 
 namespace {
@@ -192,15 +194,11 @@ int tetra_waterfall(tetra_ctx *ctx, const void *iq, int iq_fmt, size_t C, size_t
     float *od = (float *)st.out(out, (size_t)total * WF_N * 4);
     WfTables *tab = (WfTables *)ws(ctx, S_W11, sizeof(WfTables));
     if (!xd || !od || !tab) return st.finish();
-    if (!ctx->wf_tables_ready) {
+    if (!ctx->wf_tables_ready) {   // window + twiddles, built once per process (contexts may live on several threads)
         static WfTables host;
-        static bool built = false;
-        if (!built) {
-            wf_tables(host);
-            built = true;
-        }
+        static std::once_flag once;
+        std::call_once(once, [] { wf_tables(host); });
         HIP_TRY(ctx, hipMemcpyAsync(tab, &host, sizeof(WfTables), hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));   // `host` is static, but keep the copy ordered
         ctx->wf_tables_ready = true;
     }
     {

@@ -1,11 +1,12 @@
 #!/bin/bash
-# Same-box A/B of library variants: tools/ab_demod.sh lib1.so lib2.so ... (serial bench, 3 rounds)
+# Same-box A/B of library variants: tools/ab_demod.sh lib1.so lib2.so ... (3 rounds; bench args from
+# AB_ARGS, default the serial bench: --pipeline off)
 set -e
 O=gpurun_out/ab; mkdir -p $O
 for i in 1 2 3; do
   for L in "$@"; do
     n=$(basename $L .so)
-    TETRA_HIP_LIB=$PWD/$L timeout -k 10 200 python -u bench.py --no-cpu --pipeline off --steps 30 > $O/$n.$i.log 2>&1
+    TETRA_HIP_LIB=$PWD/$L timeout -k 10 200 python -u bench.py --no-cpu --steps 30 ${AB_ARGS:---pipeline off} > $O/$n.$i.log 2>&1
     python -c "import json; d=[json.loads(l) for l in open('$O/$n.$i.log') if l.startswith('{')][-1]; print('$n', d['ms_per_step'], d['stages_ms_per_step'], d['roofline'].get('measured_read_floor_GBs'))"
   done
 done
