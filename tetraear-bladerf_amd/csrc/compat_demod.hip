@@ -100,12 +100,12 @@ template <typename V> __device__ __forceinline__ auto velt(const V &v, int i) { 
 // consecutive outputs are one vector store.  Input rows are complex [C][N]; a vector load holds
 // CPV consecutive complex samples of both components (CPV = 2 for complex64 rows of even length).
 template <typename T, int CPV>
-__global__ __launch_bounds__(64) void k_sos_fwd(const T *__restrict__ x, int C, long N, int pad,
+__global__ __launch_bounds__(256) void k_sos_fwd(const T *__restrict__ x, int C, long N, int pad,
                                                 const T *__restrict__ sos, const T *__restrict__ zi,
                                                 T *__restrict__ scr, long Lp, T *__restrict__ sink) {
     using V = typename Vec16<T>::type;
     constexpr int VW = Vec16<T>::n;           // outputs per vector store
-    const int gid = blockIdx.x * 64 + threadIdx.x;
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
     const int g = gid >> 2, sec = gid & 3;
     const int ch = min(g >> 1, C - 1), comp = g & 1;   // tail lanes shadow the last stream, store to sink
     const bool own = (g >> 1) < C;
@@ -183,12 +183,12 @@ __global__ __launch_bounds__(64) void k_sos_fwd(const T *__restrict__ x, int C, 
 // Reverse pass (sosfiltfilt's second sosfilt over the time-reversed forward output), keeping
 // decimate's y[::q]: output t (= ext index t + pad) when t % q == 0.
 template <typename T>
-__global__ __launch_bounds__(64) void k_sos_bwd(const T *__restrict__ scr, long Lp, int C, long N, int pad, int q,
+__global__ __launch_bounds__(256) void k_sos_bwd(const T *__restrict__ scr, long Lp, int C, long N, int pad, int q,
                                                 const T *__restrict__ sos, const T *__restrict__ zi,
                                                 T *__restrict__ out, Lay lo) {
     using V = typename Vec16<T>::type;
     constexpr int VW = Vec16<T>::n;
-    const int gid = blockIdx.x * 64 + threadIdx.x;
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
     const int g = gid >> 2, sec = gid & 3;
     const int ch = min(g >> 1, C - 1), comp = g & 1;
     const bool own = (g >> 1) < C;
@@ -646,7 +646,9 @@ int run_decimate(tetra_ctx *ctx, const tetra_compat_plan *P, const T *x, Lay lx,
     for (int i = 0; i < 24; ++i) hc[i] = std::is_same<T, float>::value ? (T)P->sos_f32[i] : (T)P->sos_f64[i];
     for (int i = 0; i < 8; ++i) hc[24 + i] = std::is_same<T, float>::value ? (T)P->zi_f32[i] : (T)P->zi_f64[i];
     HIP_TRY(ctx, hipMemcpyAsync(coef, hc, sizeof hc, hipMemcpyHostToDevice, ctx->stream));
-    const unsigned blk = 64;
+    // four waves per workgroup: one per SIMD of a CU.  The 8 C lanes make one wave per SIMD over the
+    // chip, and 64-lane workgroups left the placement to the dispatcher
+    const unsigned blk = 256;
     const dim3 grid(grid_for((size_t)8 * C, blk));
     {
         PROF(ctx, "compat_sos_fwd");
