@@ -182,7 +182,7 @@ __global__ __launch_bounds__(256) void k_sos_fwd(const T *__restrict__ x, int C,
 
 // Reverse pass (sosfiltfilt's second sosfilt over the time-reversed forward output), keeping
 // decimate's y[::q]: output t (= ext index t + pad) when t % q == 0.
-template <typename T>
+template <typename T, int QT>
 __global__ __launch_bounds__(256) void k_sos_bwd(const T *__restrict__ scr, long Lp, int C, long N, int pad, int q,
                                                 const T *__restrict__ sos, const T *__restrict__ zi,
                                                 T *__restrict__ out, Lay lo) {
@@ -209,53 +209,106 @@ __global__ __launch_bounds__(256) void k_sos_bwd(const T *__restrict__ scr, long
             if (st && t >= 0 && t < N && t % q == 0) op[(size_t)(t / q) * so] = y;
         }
     };
-    // body batches start where the first vector load is aligned: (L - tau) % VW == 0, tau >= 3
-    long tau0 = 3;
-    while ((L - tau0) % VW) ++tau0;
     long tau = 0;
-    for (; tau < tau0; ++tau) tick(tau, sp[L - 1 - tau]);
-    constexpr int NL = SKB / VW;
-    V xa[NL], xb[NL];
-    auto ld = [&](V (&v)[NL], long t0) __attribute__((always_inline)) {
-        // ticks t0 .. t0+SKB-1 read j = L-1-t0 down to L-t0-SKB; vector k covers
-        // [L - t0 - (k+1) VW, L - t0 - k VW)
-#pragma unroll
-        for (int k = 0; k < NL; ++k) v[k] = *reinterpret_cast<const V *>(sp + (L - t0 - (k + 1) * VW));
-    };
-    // The output lanes' index t = L-1-(tau-3)-pad falls by one per tick and is the same for every
-    // stream (equal lengths), so t / q and t % q are wave-uniform scalars: the decimating store is
-    // a scalar branch, not per-lane arithmetic.
-    int tc = 0, tq = 0, tr = 0;
-    auto run = [&](V (&v)[NL], long t0) __attribute__((always_inline)) {
-#pragma unroll
-        for (int u = 0; u < SKB; ++u) {
-            const T xin = velt(v[u / VW], VW - 1 - (u % VW));
-            const T left = from_left(y);
-            y = bq.step(sec == 0 ? xin : left);
-            if (tr == 0 && tc >= 0 && tc < N) {
-                if (st) op[(size_t)tq * so] = y;
+    if constexpr (QT == 0) {
+        // body batches start where the first vector load is aligned: (L - tau) % VW == 0, tau >= 3
+        long tau0 = 3;
+        while ((L - tau0) % VW) ++tau0;
+        for (; tau < tau0; ++tau) tick(tau, sp[L - 1 - tau]);
+        constexpr int NL = SKB / VW;
+        V xa[NL], xb[NL];
+        auto ld = [&](V (&v)[NL], long t0) __attribute__((always_inline)) {
+            // ticks t0 .. t0+SKB-1 read j = L-1-t0 down to L-t0-SKB; vector k covers
+            // [L - t0 - (k+1) VW, L - t0 - k VW)
+    #pragma unroll
+            for (int k = 0; k < NL; ++k) v[k] = *reinterpret_cast<const V *>(sp + (L - t0 - (k + 1) * VW));
+        };
+        // The output lanes' index t = L-1-(tau-3)-pad falls by one per tick and is the same for every
+        // stream (equal lengths), so t / q and t % q are wave-uniform scalars: the decimating store is
+        // a scalar branch, not per-lane arithmetic.
+        int tc = 0, tq = 0, tr = 0;
+        auto run = [&](V (&v)[NL], long t0) __attribute__((always_inline)) {
+    #pragma unroll
+            for (int u = 0; u < SKB; ++u) {
+                const T xin = velt(v[u / VW], VW - 1 - (u % VW));
+                const T left = from_left(y);
+                y = bq.step(sec == 0 ? xin : left);
+                if (tr == 0 && tc >= 0 && tc < N) {
+                    if (st) op[(size_t)tq * so] = y;
+                }
+                --tc;
+                if (--tr < 0) { tr = q - 1; --tq; }
             }
-            --tc;
-            if (--tr < 0) { tr = q - 1; --tq; }
-        }
-    };
-    if (L - tau >= 2 * SKB) {
-        tc = __builtin_amdgcn_readfirstlane((int)(L - 1 - (tau - 3) - pad));   // >= 0 here
-        tq = __builtin_amdgcn_readfirstlane(tc / q);
-        tr = __builtin_amdgcn_readfirstlane(tc % q);
-        ld(xa, tau);
-        ld(xb, tau + SKB);
-        for (; tau + 4 * SKB <= L; tau += 2 * SKB) {
+        };
+        if (L - tau >= 2 * SKB) {
+            tc = __builtin_amdgcn_readfirstlane((int)(L - 1 - (tau - 3) - pad));   // >= 0 here
+            tq = __builtin_amdgcn_readfirstlane(tc / q);
+            tr = __builtin_amdgcn_readfirstlane(tc % q);
+            ld(xa, tau);
+            ld(xb, tau + SKB);
+            for (; tau + 4 * SKB <= L; tau += 2 * SKB) {
+                run(xa, tau);
+                __builtin_amdgcn_sched_barrier(0);
+                ld(xa, tau + 2 * SKB);
+                run(xb, tau + SKB);
+                __builtin_amdgcn_sched_barrier(0);
+                ld(xb, tau + 3 * SKB);
+            }
             run(xa, tau);
-            __builtin_amdgcn_sched_barrier(0);
-            ld(xa, tau + 2 * SKB);
             run(xb, tau + SKB);
-            __builtin_amdgcn_sched_barrier(0);
-            ld(xb, tau + 3 * SKB);
+            tau += 2 * SKB;
         }
-        run(xa, tau);
-        run(xb, tau + SKB);
-        tau += 2 * SKB;
+    } else {
+        // q = QT known at compile time: batches of SB ticks (a multiple of QT and of VW) that start
+        // where the vector load is aligned, inside the span where every output index lies in [0, N).
+        // The output phase ph (the first tick u of a batch with t % QT == 0) is then the same for
+        // every batch (it cannot always be 0: with the odd pad the aligned starts have odd t), so
+        // the section output of each tick goes to a register yr[u] and the batch ends with SB / QT
+        // stores of yr[ph + k QT] -- no per-tick counters or branches.
+        constexpr int SB = (2 * QT) % VW == 0 ? 2 * QT : 4 * QT;
+        constexpr int NL = SB / VW;
+        auto tcur = [&](long tt) { return L - 1 - (tt - 3) - pad; };   // output index t of section 3 at tick tt
+        long tau0 = pad + 3;   // first tick whose t < N
+        while ((L - tau0) % VW) ++tau0;
+        const int ph = __builtin_amdgcn_readfirstlane((int)(tcur(tau0) % QT));   // t % QT == 0 at u = ph
+        for (; tau < tau0; ++tau) tick(tau, sp[L - 1 - tau]);
+        V xa[NL], xb[NL];
+        auto ld = [&](V (&v)[NL], long t0) __attribute__((always_inline)) {
+#pragma unroll
+            for (int k = 0; k < NL; ++k) v[k] = *reinterpret_cast<const V *>(sp + (L - t0 - (k + 1) * VW));
+        };
+        T *dst0 = op;
+        auto run = [&](V (&v)[NL], long t0) __attribute__((always_inline)) {
+            const long tq0 = (tcur(t0) - ph) / QT;   // wave-uniform: output index of tick ph
+            T yr[SB];
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const T xin = velt(v[u / VW], VW - 1 - (u % VW));
+                const T left = from_left(y);
+                y = bq.step(sec == 0 ? xin : left);
+                yr[u] = y;
+            }
+            if (st) {
+#pragma unroll
+                for (int k = 0; k < SB / QT; ++k) dst0[(size_t)(tq0 - k) * so] = yr[ph + k * QT];
+            }
+        };
+        // batches while the last tick of the next two batches still has t >= 0 (t = tcur(tau + 2 SB - 1))
+        if (tcur(tau + 2 * SB - 1) >= 0 && L - tau >= 2 * SB) {
+            ld(xa, tau);
+            ld(xb, tau + SB);
+            for (; tcur(tau + 4 * SB - 1) >= 0 && tau + 4 * SB <= L; tau += 2 * SB) {
+                run(xa, tau);
+                __builtin_amdgcn_sched_barrier(0);
+                ld(xa, tau + 2 * SB);
+                run(xb, tau + SB);
+                __builtin_amdgcn_sched_barrier(0);
+                ld(xb, tau + 3 * SB);
+            }
+            run(xa, tau);
+            run(xb, tau + SB);
+            tau += 2 * SB;
+        }
     }
     for (; tau < L + 3; ++tau) tick(tau, tau < L ? sp[L - 1 - tau] : T(0));
 }
@@ -666,8 +719,16 @@ int run_decimate(tetra_ctx *ctx, const tetra_compat_plan *P, const T *x, Lay lx,
     }
     {
         PROF(ctx, "compat_sos_bwd");
-        hipLaunchKernelGGL(k_sos_bwd<T>, grid, dim3(blk), 0, ctx->stream, scr, Lp, C, N, pad, P->q, coef, coef + 24,
-                           out, lo);
+        // the decimation factors of 2.4 and 1.8 MSps captures (q = 10, 7) compiled in; others generic
+        if (P->q == 10)
+            hipLaunchKernelGGL((k_sos_bwd<T, 10>), grid, dim3(blk), 0, ctx->stream, scr, Lp, C, N, pad, P->q, coef,
+                               coef + 24, out, lo);
+        else if (P->q == 7)
+            hipLaunchKernelGGL((k_sos_bwd<T, 7>), grid, dim3(blk), 0, ctx->stream, scr, Lp, C, N, pad, P->q, coef,
+                               coef + 24, out, lo);
+        else
+            hipLaunchKernelGGL((k_sos_bwd<T, 0>), grid, dim3(blk), 0, ctx->stream, scr, Lp, C, N, pad, P->q, coef,
+                               coef + 24, out, lo);
     }
     return TETRA_OK;
 }
