@@ -102,12 +102,12 @@ template <typename V> __device__ __forceinline__ auto velt(const V &v, int i) { 
 template <typename T, int CPV>
 __global__ __launch_bounds__(256) void k_sos_fwd(const T *__restrict__ x, int C, long N, int pad,
                                                 const T *__restrict__ sos, const T *__restrict__ zi,
-                                                T *__restrict__ scr, long Lp, T *__restrict__ sink) {
+                                                T *__restrict__ scr, long Lp) {
     using V = typename Vec16<T>::type;
     constexpr int VW = Vec16<T>::n;           // outputs per vector store
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
     const int g = gid >> 2, sec = gid & 3;
-    const int ch = min(g >> 1, C - 1), comp = g & 1;   // tail lanes shadow the last stream, store to sink
+    const int ch = min(g >> 1, C - 1), comp = g & 1;   // tail lanes shadow the last stream, store nothing
     const bool own = (g >> 1) < C;
     const bool st = own && sec == 3;
     const T *xr = x + (size_t)ch * N * 2;      // complex row
@@ -121,7 +121,6 @@ __global__ __launch_bounds__(256) void k_sos_fwd(const T *__restrict__ x, int C,
     };
     Biquad<T> bq = load_section(sos, zi, sec, ext(0));
     T *sp = scr + (size_t)(2 * ch + comp) * Lp;
-    V *vsink = reinterpret_cast<V *>(sink) + gid;
     T y = 0;
     auto tick = [&](long tau, T xin) __attribute__((always_inline)) {
         const T left = from_left(y);
@@ -157,8 +156,7 @@ __global__ __launch_bounds__(256) void k_sos_fwd(const T *__restrict__ x, int C,
                 V w;
                 if constexpr (VW == 4) w = V{o[0], o[1], o[2], o[3]};
                 else w = V{o[0], o[1]};
-                V *dst = st ? reinterpret_cast<V *>(sp + (t0 + u - 3 - (VW - 1))) : vsink;
-                *dst = w;
+                if (st) *reinterpret_cast<V *>(sp + (t0 + u - 3 - (VW - 1))) = w;   // section-3 lanes only
             }
         }
     };
@@ -693,8 +691,7 @@ int run_decimate(tetra_ctx *ctx, const tetra_compat_plan *P, const T *x, Lay lx,
     const long Lp = (L + 3) & ~3L;   // stream-major scratch rows, 16-byte aligned
     T *scr = (T *)ws(ctx, S_W0, (size_t)2 * C * Lp * sizeof(T));
     T *coef = (T *)ws(ctx, S_W7, 32 * sizeof(T));
-    T *sink = (T *)ws(ctx, S_W4, (size_t)8 * C * 16 + 1024);
-    if (!scr || !coef || !sink) return TETRA_E_NOMEM;
+    if (!scr || !coef) return TETRA_E_NOMEM;
     T hc[32];
     for (int i = 0; i < 24; ++i) hc[i] = std::is_same<T, float>::value ? (T)P->sos_f32[i] : (T)P->sos_f64[i];
     for (int i = 0; i < 8; ++i) hc[24 + i] = std::is_same<T, float>::value ? (T)P->zi_f32[i] : (T)P->zi_f64[i];
@@ -710,12 +707,12 @@ int run_decimate(tetra_ctx *ctx, const tetra_compat_plan *P, const T *x, Lay lx,
             if (N % 2 == 0) {   // complex64 rows 16-byte aligned: 2 samples per load
                 two = true;
                 hipLaunchKernelGGL((k_sos_fwd<T, 2>), grid, dim3(blk), 0, ctx->stream, x, C, N, pad, coef, coef + 24,
-                                   scr, Lp, sink);
+                                   scr, Lp);
             }
         }
         if (!two)
             hipLaunchKernelGGL((k_sos_fwd<T, 1>), grid, dim3(blk), 0, ctx->stream, x, C, N, pad, coef, coef + 24, scr,
-                               Lp, sink);
+                               Lp);
     }
     {
         PROF(ctx, "compat_sos_bwd");
