@@ -58,6 +58,9 @@ def parse():
                          "(auto: cf32 on; sc16 off -- its demod fills every CU's LDS, so the back-end "
                          "kernels cannot co-reside and only slow it down)")
     ap.add_argument("--no-pipeline", action="store_true", help="same as --pipeline off")
+    ap.add_argument("--host-input", action="store_true",
+                    help="etsi: PCIe-inclusive mode -- each batch is copied from pinned host memory (double-buffered "
+                         "copy stream); value is then the host-fed rate, never the HBM-resident headline")
     ap.add_argument("--demod", choices=("fused", "split"), default="fused",
                     help="etsi: fused channel filter + timing in one launch, or split (y through HBM, timing "
                          "launched separately -- beside the next batch's channel filter when pipelined)")
@@ -200,6 +203,8 @@ def main():
         pipe = "off" if a.no_pipeline else a.pipeline
         if pipe == "on" or (pipe == "auto" and a.iq == "cf32"):
             step.pipeline()
+        if a.host_input:
+            step.host_feed()
     else:
         g = torch.Generator(device=dev)
         g.manual_seed(rank_seed(1000, rank))
@@ -264,6 +269,8 @@ def main():
                 "channels_per_gpu": C, "samples_per_channel": N, "sample_rate": FS,
                 "parallelism": f"channel-sharded x{world}",
                 "pipeline": bool(getattr(step, "pipelined", False)),
+                **({"input": "host-fed over PCIe (pinned, double-buffered copy stream)"}
+                   if getattr(step, "hostfed", False) else {}),
                 **({"demod": step.demod_mode} if hasattr(step, "demod_mode") else {}),
             },
             "realtime_channels": int(step.realtime_channels(value) if hasattr(step, "realtime_channels")

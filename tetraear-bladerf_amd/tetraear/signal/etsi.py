@@ -212,10 +212,48 @@ class BenchStep:
     def contexts(self):
         return [self.c] + ([self.back] if self.pipelined else [])
 
+    def host_feed(self):
+        """PCIe-inclusive mode (bench.py --host-input): every step's batch starts in pinned host
+        memory and is copied host -> device on a copy stream, double-buffered, so batch k+1's copy
+        overlaps batch k's demod -- the rate a host-fed receiver (SDR capture buffers) would see.
+        Never the headline `value` (that is measured with the input resident in HBM)."""
+        import torch
+        dev = self.iq.device
+        self.host = self.iq.cpu().pin_memory()
+        self.dbuf = [self.iq, torch.empty_like(self.iq)]
+        self.s_copy = torch.cuda.Stream(device=dev)
+        self.ev_copied = [torch.cuda.Event() for _ in range(2)]
+        self.ev_used = [torch.cuda.Event() for _ in range(2)]
+        for e in self.ev_used:
+            e.record(torch.cuda.current_stream(dev))
+        self.kin = 0
+        self.hostfed = True
+        return self
+
+    def _input(self):
+        """Device input of this step: the resident batch, or (host-fed) the freshly copied buffer."""
+        if not getattr(self, "hostfed", False):
+            return self.iq
+        import torch
+        i = self.kin & 1
+        self.kin += 1
+        with torch.cuda.stream(self.s_copy):
+            self.s_copy.wait_event(self.ev_used[i])            # the demod two steps back is done with it
+            self.dbuf[i].copy_(self.host, non_blocking=True)
+            self.ev_copied[i].record(self.s_copy)
+        front = self.s_front if self.pipelined else torch.cuda.current_stream(self.iq.device)
+        front.wait_event(self.ev_copied[i])
+        self._used = (self.ev_used[i], front)
+        return self.dbuf[i]
+
     def _demod(self, c, sym, soft, hard, nsym):
-        c.check(c.lib.tetra_demod_etsi_fmt(c.handle, self.plan, _hip.ptr(self.iq), self.fmt, self.C, self.N,
+        x = self._input()
+        c.check(c.lib.tetra_demod_etsi_fmt(c.handle, self.plan, _hip.ptr(x), self.fmt, self.C, self.N,
                                            _hip.ptr(sym), _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(nsym), self.smax,
                                            None), "demod_etsi")
+        if getattr(self, "hostfed", False):
+            ev, st = self._used
+            ev.record(st)
 
     def _lmac(self, c, soft, hard, nsym):
         c.check(c.lib.tetra_lmac_etsi(c.handle, _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(nsym), self.C, self.smax,
@@ -223,8 +261,12 @@ class BenchStep:
                                       _hip.ptr(self.blocks), _hip.ptr(self.type1)), "lmac_etsi")
 
     def _chanfilt(self, c, y):
-        c.check(c.lib.tetra_etsi_chanfilt_fmt(c.handle, self.plan, _hip.ptr(self.iq), self.fmt, self.C, self.N,
+        x = self._input()
+        c.check(c.lib.tetra_etsi_chanfilt_fmt(c.handle, self.plan, _hip.ptr(x), self.fmt, self.C, self.N,
                                               _hip.ptr(y)), "chanfilt")
+        if getattr(self, "hostfed", False):
+            ev, st = self._used
+            ev.record(st)
 
     def _timing(self, c, y):
         c.check(c.lib.tetra_etsi_timing(c.handle, self.plan, _hip.ptr(y), self.C, self.M2, _hip.ptr(self.sym),
