@@ -98,6 +98,30 @@ __device__ __forceinline__ float2 interp(const float2 *w, int w0, float t) {
     return make_float2(r, q);
 }
 
+// interp(w, w0, t) and interp(w, w0, t - 2) together: t - 2 is exact here (t < 2^22), so both share
+// the fraction f and the four Lagrange weights -- computed once, the same bits either way.
+__device__ __forceinline__ void interp_pair(const float2 *w, int w0, float t, float2 &on, float2 &mid) {
+    const float K6 = 1.0f / 6.0f;
+    const float fi = floorf(t);
+    const int i = (int)fi;
+    const float f = t - fi;
+    const float fm1 = f - 1.0f, fm2 = f - 2.0f, fp1 = f + 1.0f;
+    const float cm = -(f * fm1 * fm2) * K6;
+    const float c0 = (fp1 * fm1 * fm2) * 0.5f;
+    const float c1 = -(fp1 * f * fm2) * 0.5f;
+    const float c2 = (fp1 * f * fm1) * K6;
+    auto one = [&](int j) -> float2 {
+        const float2 a = w[j - 1 - w0], b = w[j - w0], c = w[j + 1 - w0], d = w[j + 2 - w0];
+        float r = cm * a.x, q = cm * a.y;
+        r = fmaf(c0, b.x, r); q = fmaf(c0, b.y, q);
+        r = fmaf(c1, c.x, r); q = fmaf(c1, c.y, q);
+        r = fmaf(c2, d.x, r); q = fmaf(c2, d.y, q);
+        return make_float2(r, q);
+    };
+    on = one(i);
+    mid = one(i - 2);
+}
+
 __device__ __forceinline__ float2 csqrt_p(float x, float y) {
     const float r = sqrtf(fmaf(x, x, y * y));
     if (r == 0.0f) return make_float2(0.f, 0.f);
@@ -148,10 +172,7 @@ __device__ __forceinline__ void timing_wave(const float2 *y, int M2, float gain,
         const unsigned long long bal = __ballot(!valid);
         const int nv = bal ? (__ffsll((long long)bal) - 1) : 64;
         float2 on = make_float2(0.f, 0.f), mid = make_float2(0.f, 0.f);
-        if (lane < nv) {
-            on = interp(y, 0, t);
-            mid = interp(y, 0, t - 2.0f);
-        }
+        if (lane < nv) interp_pair(y, 0, t, on, mid);
         float2 pv = make_float2(dppf<0x138>(on.x), dppf<0x138>(on.y));   // wave_shr:1 (lane 0 replaced below)
         bool hp_ = true;
         if (lane == 0) { pv = prev; hp_ = have_prev; }
