@@ -155,8 +155,9 @@ def test_full_size_round_trip():
 
 
 def test_bench_pipeline_matches_serial():
-    """bench.py's two-stream pipeline (front: chanfilt, back: timing + lower MAC, double-buffered
-    72 kHz intermediate) gives the same per-step results as the single-stream chain."""
+    """bench.py's step variants give the same per-step results as the single-stream fused chain:
+    the two-stream pipeline (front: fused demod, back: lower MAC, double-buffered symbol outputs),
+    the split demod (chanfilt -> y in HBM -> timing) pipelined, and the host-fed (PCIe) mode."""
     import torch
     from tetraear import _hip
     from tetraear.signal.etsi import BenchStep
@@ -164,18 +165,28 @@ def test_bench_pipeline_matches_serial():
     c = _hip.ctx()
     c.check(c.lib.tetra_set_stream(c.handle, None), "set_stream")
     outs = []
-    for pipe in (False, True):
-        st = BenchStep(c, 64, 131072, 2.4e6, seed=11, device=dev)
+    for pipe, demod, host in ((False, "fused", False), (True, "fused", False), (True, "split", False),
+                              (True, "fused", True), (False, "split", True)):
+        st = BenchStep(c, 64, 131072, 2.4e6, seed=11, device=dev, demod=demod)
         if pipe:
             st.pipeline()
+        if host:
+            st.host_feed()
         for _ in range(3):
             st()
         torch.cuda.synchronize(dev)
-        outs.append([t.cpu().clone() for t in (st.soft, st.hard, st.nsym, st.nburst, st.bursts, st.nblock,
-                                               st.blocks, st.type1)])
+        soft, hard, ns = st.soft.cpu(), st.hard.cpu(), st.nsym.cpu()
+        nb, bursts, nk, blocks, t1 = st.nburst.cpu(), st.bursts.cpu(), st.nblock.cpu(), st.blocks.cpu(), st.type1.cpu()
+        # the written parts only (the buffers are torch.empty: padding differs between instances)
+        n1 = {0: 268, 1: 124, 2: 60}   # type-1 bits per block kind (the rest of a type1 row is padding)
+        outs.append([ns, nb, nk] + [x for ch in range(64) for x in (
+            soft[ch, :2 * max(int(ns[ch]) - 1, 0)], hard[ch, :max(int(ns[ch]) - 1, 0)], bursts[ch, :int(nb[ch])],
+            blocks[ch, :int(nk[ch])])] + [t1[ch, j, :n1[int(blocks[ch, j, 0])]] for ch in range(64)
+                                          for j in range(int(nk[ch]))])
         assert st.quality()["crc_ok"] > 64
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
 
 
 def test_sc16_ingest_matches_cf32(synth_small):
