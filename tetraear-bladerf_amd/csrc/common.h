@@ -26,6 +26,7 @@ enum Slot {
     S_W8, S_W9, S_W10,                                     // wideband channeliser
     S_W11,                                                 // waterfall window + twiddles
     S_W12,                                                 // ETSI channel-filter tap image (kept)
+    S_W13,                                                 // diagnostics (tetra_read_floor sink)
     S_COUNT
 };
 

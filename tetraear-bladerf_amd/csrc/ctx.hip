@@ -250,7 +250,7 @@ __global__ __launch_bounds__(256) void k_read_floor(const float4 *__restrict__ x
 
 extern "C" int tetra_read_floor(tetra_ctx *ctx, const void *x, size_t rows, size_t row_bytes, size_t lds_bytes) {
     if (!ctx || !x || rows == 0 || row_bytes % 16 || lds_bytes > 160 * 1024) return TETRA_E_INVALID;
-    uint32_t *o = (uint32_t *)ws(ctx, S_W7, rows * 4);
+    uint32_t *o = (uint32_t *)ws(ctx, S_W13, rows * 4);
     if (!o) return TETRA_E_NOMEM;
     PROF(ctx, "read_floor");
     hipLaunchKernelGGL(k_read_floor, dim3((unsigned)rows), dim3(256), lds_bytes, ctx->stream, (const float4 *)x,
