@@ -311,6 +311,229 @@ __global__ __launch_bounds__(256) void k_sos_bwd(const T *__restrict__ scr, long
     for (; tau < L + 3; ++tau) tick(tau, tau < L ? sp[L - 1 - tau] : T(0));
 }
 
+// ------------------------------------------------------------------ fp32 decimator, banked lanes
+// The kernels above are bound by the texture data path (TD ~95 % busy, r01 PMC): the four
+// section lanes of a stream, and for the forward pass both components of a channel, load the same
+// 16 bytes, so every load instruction returns 1 KiB for 128-256 useful bytes.  Here the section
+// is the DPP bank instead of the low lane bits:
+//   lane = 16 row + 4 sec + s,   stream g = 16 wave + 4 row + s   (g = 2 ch + comp)
+// The section chain moves one bank right per tick (row_shr:4), and the 4 lanes of a stream load 4
+// DIFFERENT 16-byte chunks of its input window; section 0 (bank 0) takes the tick's sample from
+// the lane of bank j with row_shl:4j under bank_mask 1 -- the same DPP move that replaces the
+// section-0 select, so a tick is 2 DPP moves + the 9-operation biquad.  Arithmetic per section and
+// sample is unchanged (bit-identical to the kernels above and to scipy's _sosfilt).
+template <int CTRL, int BANKS, bool BC>
+__device__ __forceinline__ float dppf(float old, float src) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old),
+                                                                 __builtin_bit_cast(int, src), CTRL, 0xf, BANKS, BC));
+}
+// section 0 takes src of bank j (compile time); the other banks keep `left`
+template <int J>
+__device__ __forceinline__ float bank0_from(float left, float src) {
+    if constexpr (J == 0) return dppf<0xE4, 0x1, false>(left, src);   // quad_perm identity
+    else return dppf<0x100 + 4 * J, 0x1, false>(left, src);            // row_shl:4J
+}
+__device__ __forceinline__ float from_left_bank(float y) { return dppf<0x114, 0xf, true>(0.f, y); }   // row_shr:4
+
+// 4-byte aligned 16-byte load (the imaginary stream's window starts one float into a complex pair)
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+
+struct BankLane {
+    int sec, g, ch, comp;
+    bool own, st;
+    __device__ BankLane(int C) {
+        const int lane = threadIdx.x & 63, w = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+        sec = (lane >> 2) & 3;
+        g = 16 * w + 4 * (lane >> 4) + (lane & 3);
+        ch = min(g >> 1, C - 1);   // tail lanes shadow the last stream and store nothing
+        comp = g & 1;
+        own = (g >> 1) < C;
+        st = own && sec == 3;
+    }
+};
+
+// Forward pass (k_sos_fwd's contract) for complex64 rows of even length.  Window of 8 samples:
+// lane (sec = j) loads floats [2 n0 + 4 j + comp, +4): elements 0 and 2 are component `comp` of
+// samples n0 + 2j and n0 + 2j + 1.
+__global__ __launch_bounds__(256) void k_sos_fwd_bank(const float *__restrict__ x, int C, long N, int pad,
+                                                     const float *__restrict__ sos, const float *__restrict__ zi,
+                                                     float *__restrict__ scr, long Lp) {
+    const BankLane bl(C);
+    const int sec = bl.sec, comp = bl.comp;
+    const bool st = bl.st;
+    const float *xr = x + (size_t)bl.ch * N * 2;
+    const long L = N + 2 * pad;
+    auto xat = [&](long n) { return xr[2 * n + comp]; };
+    const float two = 2, x0 = xat(0), xl = xat(N - 1);
+    auto ext = [&](long j) -> float {   // scipy _arraytools.odd_ext
+        if (j < pad) return two * x0 - xat(pad - j);
+        if (j < pad + N) return xat(j - pad);
+        return two * xl - xat(N - 2 - (j - pad - N));
+    };
+    Biquad<float> bq = load_section(sos, zi, sec, ext(0));
+    float *sp = scr + (size_t)(2 * bl.ch + comp) * Lp;
+    float y = 0;
+    auto tick = [&](long tau, float xin) __attribute__((always_inline)) {
+        const float left = from_left_bank(y);
+        const long j = tau - sec;
+        if (j >= 0 && j < L) {
+            y = bq.step(sec == 0 ? xin : left);
+            if (st) sp[j] = y;
+        }
+    };
+    long tau = 0;
+    for (; tau < pad; ++tau) tick(tau, ext(tau));
+    constexpr int NW = SKB / 8;   // 8-sample windows per batch
+    f4u xa[NW], xb[NW];
+    const float *xw = xr + 4 * sec + comp;
+    auto ld = [&](f4u (&v)[NW], long t0) __attribute__((always_inline)) {
+        const float *src = xw + 2 * (t0 - pad);
+#pragma unroll
+        for (int k = 0; k < NW; ++k) v[k] = *reinterpret_cast<const f4u *>(src + 16 * k);
+    };
+    // Output: section 3 emits j = tau - 3.  Every 16 ticks the four lanes of a stream each store 4
+    // of section 3's last 16 outputs (bank j takes o[4j .. 4j+3] from bank 3 with row_shl:4(3-j)):
+    // one 64-lane store of 64 contiguous bytes per stream instead of four 16-lane stores of 16.
+    const bool own = bl.own;
+    auto run = [&](f4u (&v)[NW], long t0) __attribute__((always_inline)) {
+        float o[16];
+#pragma unroll
+        for (int u = 0; u < SKB; ++u) {
+            const f4u &pv = v[u >> 3];
+            const float e = (u & 1) ? pv.z : pv.x;
+            const float left = from_left_bank(y);
+            float xin;
+            switch ((u >> 1) & 3) {
+                case 0: xin = bank0_from<0>(left, e); break;
+                case 1: xin = bank0_from<1>(left, e); break;
+                case 2: xin = bank0_from<2>(left, e); break;
+                default: xin = bank0_from<3>(left, e); break;
+            }
+            y = bq.step(xin);   // every section active: pad >= 3
+            o[u & 15] = y;
+            if ((u & 15) == 15) {
+                float w[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    w[i] = o[12 + i];
+                    w[i] = dppf<0x10C, 0x1, false>(w[i], o[i]);       // bank 0 <- bank 3 (row_shl:12)
+                    w[i] = dppf<0x108, 0x2, false>(w[i], o[4 + i]);   // bank 1 <- bank 3 (row_shl:8)
+                    w[i] = dppf<0x104, 0x4, false>(w[i], o[8 + i]);   // bank 2 <- bank 3 (row_shl:4)
+                }
+                if (own) *reinterpret_cast<float4 *>(sp + (t0 + u - 18 + 4 * sec)) = float4{w[0], w[1], w[2], w[3]};
+            }
+        }
+        // elements 1 and 3 are never read: keep the whole vector live to here, or the allocator
+        // reuses them as temporaries while the next window's load into them is in flight (a
+        // write-after-write wait on every outstanding load)
+#pragma unroll
+        for (int k = 0; k < NW; ++k) asm volatile("" ::"v"(v[k]));
+    };
+    // the imaginary lanes of the last chunk read one float past their window: the batches stop
+    // one sample short of the row end, so that float is inside the row
+    if (N >= 2 * SKB + 1) {
+        ld(xa, tau);
+        ld(xb, tau + SKB);
+        for (; tau + 4 * SKB < pad + N; tau += 2 * SKB) {
+            run(xa, tau);
+            __builtin_amdgcn_sched_barrier(0);
+            ld(xa, tau + 2 * SKB);
+            run(xb, tau + SKB);
+            __builtin_amdgcn_sched_barrier(0);
+            ld(xb, tau + 3 * SKB);
+        }
+        run(xa, tau);
+        run(xb, tau + SKB);
+        tau += 2 * SKB;
+    }
+    for (; tau < L + 3; ++tau) tick(tau, tau < L ? ext(tau) : 0.f);
+}
+
+// Reverse pass with decimation q = QT (k_sos_bwd<float, QT>'s contract).  The scratch row is the
+// stream's own, so the 4 lanes of a stream load the 4 chunks of a 16-tick window with no
+// duplication: lane (sec = j) loads floats [L - t0 - 16 k - 4 j - 4, +4), tick u of the window reads
+// element 3 - (u & 3) of chunk (u >> 2) & 3.  The batch start is chosen so that the first output
+// tick of every batch is the compile-time phase PH, so outputs are stored as they are produced.
+template <int QT>
+__global__ __launch_bounds__(256) void k_sos_bwd_bank(const float *__restrict__ scr, long Lp, int C, long N, int pad,
+                                                     int q, const float *__restrict__ sos,
+                                                     const float *__restrict__ zi, float *__restrict__ out, Lay lo) {
+    const BankLane bl(C);
+    const int sec = bl.sec;
+    const bool st = bl.st;
+    const float *sp = scr + (size_t)(2 * bl.ch + bl.comp) * Lp;
+    const long L = N + 2 * pad;
+    Biquad<float> bq = load_section(sos, zi, sec, sp[L - 1]);
+    float *op = out + lo.off(bl.ch, 0) + bl.comp;
+    const size_t so = lo.s_n;
+    float y = 0;
+    auto tick = [&](long tau, float xin) __attribute__((always_inline)) {
+        const float left = from_left_bank(y);
+        const long k = tau - sec;
+        if (k >= 0 && k < L) {
+            y = bq.step(sec == 0 ? xin : left);
+            const int t = (int)(L - 1 - k - pad);
+            if (st && t >= 0 && t < N && t % q == 0) op[(size_t)(t / q) * so] = y;
+        }
+    };
+    constexpr int SB = QT * 16 / (QT % 16 == 0 ? 16 : QT % 8 == 0 ? 8 : QT % 4 == 0 ? 4 : QT % 2 == 0 ? 2 : 1);
+    static_assert(SB % 16 == 0 && SB % QT == 0, "batch = lcm(16, QT)");
+    constexpr int NL = SB / 16;
+    // output index of section 3 at tick tt; t % QT == 0 at tick u of a batch iff u % QT == PH
+    auto tcur = [&](long tt) { return L - 1 - (tt - 3) - pad; };
+    // PH must match the parity that the aligned starts allow (tcur(tau0) = L - tau0 + 2 - pad with
+    // L - tau0 a multiple of 4): odd for even QT and the default odd pad
+    constexpr int PH = QT % 2 ? 0 : 5 % QT;
+    long tau0 = pad + 3;
+    while (((L - tau0) % 4 || tcur(tau0) % QT != PH) && tau0 < pad + 3 + 4 * QT) ++tau0;
+    const bool phased = (L - tau0) % 4 == 0 && tcur(tau0) % QT == PH;
+    long tau = 0;
+    if (phased) {
+        for (; tau < tau0; ++tau) tick(tau, sp[L - 1 - tau]);
+        float4 xa[NL], xb[NL];
+        const float *sw = sp + L - 4 - 4 * sec;
+        auto ld = [&](float4 (&v)[NL], long t0) __attribute__((always_inline)) {
+#pragma unroll
+            for (int k = 0; k < NL; ++k) v[k] = *reinterpret_cast<const float4 *>(sw - t0 - 16 * k);
+        };
+        auto run = [&](float4 (&v)[NL], long t0) __attribute__((always_inline)) {
+            const long tq0 = tcur(t0 + PH) / QT;   // wave-uniform: output index of tick PH
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const float4 &pv = v[u >> 4];
+                const int el = 3 - (u & 3);
+                const float e = el == 3 ? pv.w : el == 2 ? pv.z : el == 1 ? pv.y : pv.x;
+                const float left = from_left_bank(y);
+                float xin;
+                switch ((u >> 2) & 3) {
+                    case 0: xin = bank0_from<0>(left, e); break;
+                    case 1: xin = bank0_from<1>(left, e); break;
+                    case 2: xin = bank0_from<2>(left, e); break;
+                    default: xin = bank0_from<3>(left, e); break;
+                }
+                y = bq.step(xin);
+                if (u % QT == PH && st) op[(size_t)(tq0 - u / QT) * so] = y;
+            }
+        };
+        if (tcur(tau + 2 * SB - 1) >= 0 && L - tau >= 2 * SB) {
+            ld(xa, tau);
+            ld(xb, tau + SB);
+            for (; tcur(tau + 4 * SB - 1) >= 0 && tau + 4 * SB <= L; tau += 2 * SB) {
+                run(xa, tau);
+                __builtin_amdgcn_sched_barrier(0);
+                ld(xa, tau + 2 * SB);
+                run(xb, tau + SB);
+                __builtin_amdgcn_sched_barrier(0);
+                ld(xb, tau + 3 * SB);
+            }
+            run(xa, tau);
+            run(xb, tau + SB);
+            tau += 2 * SB;
+        }
+    }
+    for (; tau < L + 3; ++tau) tick(tau, tau < L ? sp[L - 1 - tau] : 0.f);
+}
+
 // ------------------------------------------------------------------ mixer + filtfilt (lfilter)
 // Value of component `comp` of (possibly frequency-shifted) sample n, in double.
 __device__ __forceinline__ double mix_pair(double xr, double xi, long n, int comp, bool mix, double c, double fs) {
@@ -704,9 +927,9 @@ int run_decimate(tetra_ctx *ctx, const tetra_compat_plan *P, const T *x, Lay lx,
         PROF(ctx, "compat_sos_fwd");
         bool two = false;
         if constexpr (std::is_same<T, float>::value) {
-            if (N % 2 == 0) {   // complex64 rows 16-byte aligned: 2 samples per load
+            if (N % 2 == 0) {   // complex64 rows 16-byte aligned: banked lanes, unique loads
                 two = true;
-                hipLaunchKernelGGL((k_sos_fwd<T, 2>), grid, dim3(blk), 0, ctx->stream, x, C, N, pad, coef, coef + 24,
+                hipLaunchKernelGGL(k_sos_fwd_bank, grid, dim3(blk), 0, ctx->stream, x, C, N, pad, coef, coef + 24,
                                    scr, Lp);
             }
         }
@@ -717,7 +940,20 @@ int run_decimate(tetra_ctx *ctx, const tetra_compat_plan *P, const T *x, Lay lx,
     {
         PROF(ctx, "compat_sos_bwd");
         // the decimation factors of 2.4 and 1.8 MSps captures (q = 10, 7) compiled in; others generic
-        if (P->q == 10)
+        bool bank = false;
+        if constexpr (std::is_same<T, float>::value) {
+            bank = true;
+            if (P->q == 10)
+                hipLaunchKernelGGL((k_sos_bwd_bank<10>), grid, dim3(blk), 0, ctx->stream, scr, Lp, C, N, pad, P->q,
+                                   coef, coef + 24, out, lo);
+            else if (P->q == 7)
+                hipLaunchKernelGGL((k_sos_bwd_bank<7>), grid, dim3(blk), 0, ctx->stream, scr, Lp, C, N, pad, P->q,
+                                   coef, coef + 24, out, lo);
+            else
+                bank = false;
+        }
+        if (bank) {
+        } else if (P->q == 10)
             hipLaunchKernelGGL((k_sos_bwd<T, 10>), grid, dim3(blk), 0, ctx->stream, scr, Lp, C, N, pad, P->q, coef,
                                coef + 24, out, lo);
         else if (P->q == 7)
