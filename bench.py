@@ -72,8 +72,15 @@ def traffic_from_profiles(kernel, workload_key):
     workload (profiles/*_summary.json, written by tools/pmc_summary.py from separate FETCH_SIZE /
     WRITE_SIZE passes with the gfx950 x2 FETCH correction), or None."""
     import glob
+    import re
+
+    def age(f):   # (round, version): r02_x beats r01_x_v10, v10 beats v9 (not a string sort)
+        b = os.path.basename(f)
+        r, v = re.match(r"r(\d+)_", b), re.search(r"_v(\d+)_", b)
+        return (int(r.group(1)) if r else 0, int(v.group(1)) if v else 0, b)
+
     best = None
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_summary.json"))):
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_summary.json")), key=age):
         try:
             d = json.load(open(f))
         except ValueError:
@@ -144,7 +151,8 @@ class CompatStep:
         return 8.0 + 17.0 * 18000.0 / FS
 
     def dominant(self):
-        return ("compat_sos_fwd", 8.0, "k_sos_fwd")   # reads each input sample once (8 B)
+        # reads each input sample once (8 B); complex64 rows always take the banked forward pass
+        return ("compat_sos_fwd", 8.0, "k_sos_fwd_bank")
 
     def cpu_baseline(self, budget_s):
         sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -170,8 +178,9 @@ def read_floor(c, step, reps=5):
     LDS footprint), timed with HIP events on the context stream."""
     ptr, rows, row_bytes, lds = step.floor_args()
     c.check(c.lib.tetra_profile(c.handle, 1), "profile")
-    read_profile(c)
-    for _ in range(reps + 1):
+    c.check(c.lib.tetra_read_floor(c.handle, ptr, rows, row_bytes, lds), "read_floor")   # warm-up launch
+    read_profile(c)   # drop the warm-up record: only the reps below are averaged
+    for _ in range(reps):
         c.check(c.lib.tetra_read_floor(c.handle, ptr, rows, row_bytes, lds), "read_floor")
     ms, n = read_profile(c).get("read_floor", (0.0, 0))
     c.check(c.lib.tetra_profile(c.handle, 0), "profile")

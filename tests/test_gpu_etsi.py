@@ -162,7 +162,10 @@ def test_bench_pipeline_matches_serial():
     from tetraear import _hip
     from tetraear.signal.etsi import BenchStep
     dev = torch.device("cuda", 0)
-    c = _hip.ctx()
+    # a context of this test's own: tetra_set_stream(None) puts it on the null stream (torch's
+    # current stream, where BenchStep's torch buffers are made), which must not leak into the
+    # shared thread-local context the other tests use
+    c = _hip.Context()
     c.check(c.lib.tetra_set_stream(c.handle, None), "set_stream")
     outs = []
     for pipe, demod, host in ((False, "fused", False), (True, "fused", False), (True, "split", False),
@@ -283,3 +286,53 @@ def test_lower_mac_empty_and_low_snr():
                 nblk += 1
                 nfail += not b["crc_ok"]
     assert nblk > 0
+
+
+def test_fused_demod_many_channels():
+    """The fused cf32 demod over more channels than the chip holds workgroups at once (two per CU: the
+    grid runs in three waves of workgroups): bit-identical to the component path (chanfilt -> y in HBM
+    -> k_timing) for every channel, and to the oracle for channels of the second and third waves."""
+    import torch
+    from tetraear import _hip
+    from tetraear.signal.etsi import etsi_plan, lengths
+    dev = torch.device("cuda", 0)
+    G = 2 * torch.cuda.get_device_properties(0).multi_processor_count
+    C, N = 2 * G + 37, 131072
+    c = _hip.ctx()
+    plan = etsi_plan()
+    _, M2, smax = lengths(plan, N)
+    iq = torch.empty((C, N, 2), dtype=torch.float32, device=dev)
+    nb = c.lib.tetra_synth_bursts_per_channel(N, 2.4e6)
+    cells = torch.empty(C, dtype=torch.int32, device=dev)
+    kinds = torch.empty((C, nb), dtype=torch.int32, device=dev)
+    pay = torch.empty((C, nb, 2, 268), dtype=torch.uint8, device=dev)
+    c.check(c.lib.tetra_synth_etsi(c.handle, C, N, 2.4e6, 77, 16.0, 600.0, _hip.ptr(iq), _hip.ptr(cells),
+                                   _hip.ptr(kinds), _hip.ptr(pay), None), "synth")
+
+    def outs():
+        return (torch.zeros((C, smax, 2), dtype=torch.float32, device=dev),
+                torch.zeros((C, 2 * smax), dtype=torch.int8, device=dev),
+                torch.zeros((C, smax), dtype=torch.uint8, device=dev),
+                torch.zeros(C, dtype=torch.int32, device=dev),
+                torch.zeros((C, 4), dtype=torch.float32, device=dev))
+    a = outs()
+    c.check(c.lib.tetra_demod_etsi_fmt(c.handle, plan, _hip.ptr(iq), _hip.TETRA_CF32, C, N, *[_hip.ptr(t) for t in a[:4]],
+                                       smax, _hip.ptr(a[4])), "demod")
+    y = torch.empty((C, M2, 2), dtype=torch.float32, device=dev)
+    c.check(c.lib.tetra_etsi_chanfilt(c.handle, plan, _hip.ptr(iq), C, N, _hip.ptr(y)), "chanfilt")
+    bo = outs()
+    c.check(c.lib.tetra_etsi_timing(c.handle, plan, _hip.ptr(y), C, M2, *[_hip.ptr(t) for t in bo[:4]], smax,
+                                    _hip.ptr(bo[4])), "timing")
+    torch.cuda.synchronize(dev)
+    assert torch.equal(a[3], bo[3]) and int(a[3].min()) > 900
+    assert torch.equal(a[0], bo[0]) and torch.equal(a[2], bo[2]) and torch.equal(a[4], bo[4])
+    assert torch.equal(a[1], bo[1])
+    rx = E.Receiver()
+    for ch in (3, G + 5, 2 * G + 1, C - 1):
+        x = iq[ch].cpu().numpy().view(np.complex64)[:, 0]
+        so, sbo, ho, _ = rx.demod(x)
+        n = int(a[3][ch])
+        assert n == len(so), ch
+        sym = a[0][ch, :n].cpu().numpy().view(np.complex64)[:, 0]
+        assert np.array_equal(sym, so) and np.array_equal(a[2][ch, :n - 1].cpu().numpy(), ho), ch
+        assert np.array_equal(a[1][ch, :2 * (n - 1)].cpu().numpy(), sbo), ch

@@ -352,7 +352,9 @@ struct BankLane {
     }
 };
 
-// Forward pass (k_sos_fwd's contract) for complex64 rows of even length.  Window of 8 samples:
+// Forward pass (k_sos_fwd's contract) for complex64 rows of any length: the window loads are
+// 4-byte-aligned vectors (f4u), so an odd-length row's 8-byte-aligned start is fine, and the
+// batches stop one sample short of the row end (below).  Window of 8 samples:
 // lane (sec = j) loads floats [2 n0 + 4 j + comp, +4): elements 0 and 2 are component `comp` of
 // samples n0 + 2j and n0 + 2j + 1.
 __global__ __launch_bounds__(256) void k_sos_fwd_bank(const float *__restrict__ x, int C, long N, int pad,
@@ -927,11 +929,9 @@ int run_decimate(tetra_ctx *ctx, const tetra_compat_plan *P, const T *x, Lay lx,
         PROF(ctx, "compat_sos_fwd");
         bool two = false;
         if constexpr (std::is_same<T, float>::value) {
-            if (N % 2 == 0) {   // complex64 rows 16-byte aligned: banked lanes, unique loads
-                two = true;
-                hipLaunchKernelGGL(k_sos_fwd_bank, grid, dim3(blk), 0, ctx->stream, x, C, N, pad, coef, coef + 24,
-                                   scr, Lp);
-            }
+            two = true;   // complex64: banked lanes, unique loads (any row length)
+            hipLaunchKernelGGL(k_sos_fwd_bank, grid, dim3(blk), 0, ctx->stream, x, C, N, pad, coef, coef + 24, scr,
+                               Lp);
         }
         if (!two)
             hipLaunchKernelGGL((k_sos_fwd<T, 1>), grid, dim3(blk), 0, ctx->stream, x, C, N, pad, coef, coef + 24, scr,

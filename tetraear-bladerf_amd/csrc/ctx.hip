@@ -229,20 +229,31 @@ int tetra_device_arch(tetra_ctx *ctx, char *buf, size_t n) {
 
 // ------------------------------------------------------------------ HBM read floor (diagnostic)
 // The access pattern of the channel filter without its arithmetic: one workgroup streams one row
-// of `row_bytes` with 16-B loads, five per thread in flight per pass, and folds them into one word
-// (so nothing is dead-code eliminated).  `lds_bytes` of dynamic LDS caps the workgroups per CU the
-// way the real kernel's LDS does.  bench.py reports it as the measured floor beside the roofline.
+// of `row_bytes` with 16-B nontemporal loads (the load form the channel filter uses), two groups of
+// five per thread in flight (a register ring, like the filter's two-tile prefetch), folded into one
+// word so nothing is dead-code eliminated.  `lds_bytes` of dynamic LDS caps the workgroups per CU
+// the way the real kernel's LDS does.  bench.py reports it as the measured floor beside the
+// roofline.  (tools/probes/probe_hbm.hip: plain loads 6.15-6.19 TB/s, nt 6.91-7.07 TB/s.)
 __global__ __launch_bounds__(256) void k_read_floor(const float4 *__restrict__ x, long row4, uint32_t *out) {
     extern __shared__ float4 pad_lds[];
     const float4 *p = x + (size_t)blockIdx.x * row4;
     uint32_t acc = 0;
-    for (long q = threadIdx.x; q < row4; q += 5 * 256) {
-        float4 v[5];
+    float4 v[2][5];
 #pragma unroll
-        for (int r = 0; r < 5; ++r) v[r] = p[min(q + r * 256, row4 - 1)];
+    for (int d = 0; d < 2; ++d)
 #pragma unroll
-        for (int r = 0; r < 5; ++r)
-            acc ^= __float_as_uint(v[r].x) ^ __float_as_uint(v[r].y) ^ __float_as_uint(v[r].z) ^ __float_as_uint(v[r].w);
+        for (int r = 0; r < 5; ++r) v[d][r] = ld_nt(p + min((long)(d * 5 + r) * 256 + threadIdx.x, row4 - 1));
+    for (long g = 0; g * 1280 < row4; g += 2) {
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+#pragma unroll
+            for (int r = 0; r < 5; ++r)
+                acc ^= __float_as_uint(v[d][r].x) ^ __float_as_uint(v[d][r].y) ^ __float_as_uint(v[d][r].z) ^
+                       __float_as_uint(v[d][r].w);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int r = 0; r < 5; ++r) v[d][r] = ld_nt(p + min((g + 2 + d) * 1280 + r * 256 + threadIdx.x, row4 - 1));
+        }
     }
     if (acc == 0x9E3779B9u) pad_lds[threadIdx.x] = make_float4(0.f, 0.f, 0.f, 0.f);   // keeps the LDS allocation
     if (acc == 0x9E3779B9u) out[blockIdx.x] = acc;   // practically never: no store traffic

@@ -297,7 +297,7 @@ constexpr int XIN4 = (HALO + TILE_IN) / 2;   // float4 entries of the input imag
 template <typename In> constexpr int cf_lds4() { return XIN4 + cf_lr<In>() / 2; }   // image + stage-1 buffer (float4)
 constexpr int CF_LDS2_SC16 = 2 * (XIN4 + CfCfg<uint2>::lr / 2);   // SC16 fused: y + timing scratch (float2)
 static_assert(XIN4 + CfCfg<uint2>::lr / 2 == 2460, "SC16 LDS: 39,360 B, four workgroups per CU");
-static_assert((XIN4 + CfCfg<float4>::lr / 2) * 16 + 4096 * 8 <= 72 * 1024, "cf32 LDS: two workgroups per CU + 16 KB");
+static_assert((XIN4 + CfCfg<float4>::lr / 2 + 12) * 16 + 4096 * 8 <= 72 * 1024, "cf32 LDS: two workgroups per CU + 16 KB");
 constexpr int CF_COEF = 64 + S2K * 64;       // device tap image: h1 (64) + A fragments [S2K][64 lanes]
 
 // Packed fp32 (v_pk_fma_f32): one real tap times a complex sample, each half a correctly rounded
@@ -341,10 +341,17 @@ __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, lon
     // only the image and the stage-1 buffer (39 KB: four workgroups per CU) and sends y through
     // HBM/L2
     constexpr int CF_LDS4 = cf_lds4<In>(), LR = cf_lr<In>(), S2_EVERY = CfCfg<In>::s2_every;
-    __shared__ float4 lds[YL ? CF_LDS4 + YLDS / 2 : CF_LDS4];
+    __shared__ float4 lds[(YL ? CF_LDS4 + YLDS / 2 : CF_LDS4) + 12];
     float4 *xin = lds;
     float2 *lin = reinterpret_cast<float2 *>(lds + XIN4);
     float *yb = reinterpret_cast<float *>(lds + CF_LDS4);   // YL only: y as (re, im) floats
+    // the 48 stage-1 taps in LDS, read as broadcast float4s beside the samples: as scalar operands
+    // hipcc re-loads them every tile (SGPR pressure), and those scalar loads share lgkmcnt with the
+    // LDS reads, so each sample read was waited for right before its use (one or two in flight)
+    float4 *htap = lds + (YL ? CF_LDS4 + YLDS / 2 : CF_LDS4);
+    if (threadIdx.x < 12)
+        htap[threadIdx.x] = make_float4(h1[4 * threadIdx.x], h1[4 * threadIdx.x + 1], h1[4 * threadIdx.x + 2],
+                                        h1[4 * threadIdx.x + 3]);
     const int ch = blockIdx.x;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;
@@ -375,7 +382,7 @@ __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, lon
 #pragma unroll
         for (int r = 0; r < 5; ++r) {
             const long q = (long)t * (TILE_IN / 2) + r * 256 + tid;   // sample-pair index
-            pf[r] = xp[min(q, nq - 1)];
+            pf[r] = ld_nt(xp + min(q, nq - 1));   // streamed once: nt (common.h)
         }
     };
     int u_done = 0;   // stage-2 output triples [0, u_done) are stored
@@ -398,10 +405,12 @@ __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, lon
             const float4 *w = xin + 5 * tid + 4;
             pf2 a = {0.f, 0.f};
 #pragma unroll
-            for (int jj = 0; jj < 24; ++jj) {
-                const float4 v = w[jj];
-                a = pfma(h1[2 * jj], pf2{v.x, v.y}, a);
-                a = pfma(h1[2 * jj + 1], pf2{v.z, v.w}, a);
+            for (int q = 0; q < 12; ++q) {
+                const float4 t4 = htap[q], x0 = w[2 * q], x1 = w[2 * q + 1];
+                a = pfma(t4.x, pf2{x0.x, x0.y}, a);
+                a = pfma(t4.y, pf2{x0.z, x0.w}, a);
+                a = pfma(t4.z, pf2{x1.x, x1.y}, a);
+                a = pfma(t4.w, pf2{x1.z, x1.w}, a);
             }
             lin[k - kbase] = make_float2(a.x, a.y);
         }
@@ -433,10 +442,22 @@ __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, lon
                 const int b0 = U0 <= u_hi ? 2 * (10 * U0 - kbase + kg) + comp : 2 * kg + comp;
                 const int b1 = U1 <= u_hi ? 2 * (10 * U1 - kbase + kg) + comp : 2 * kg + comp;
                 f4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+                // B operands a third of the chain ahead (hipcc otherwise waits lgkmcnt(0), one LDS
+                // round trip, before each MFMA pair)
+                float bv0[S2K], bv1[S2K];
 #pragma unroll
-                for (int s2 = 0; s2 < S2K; ++s2) {
-                    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(at[s2], lf[b0 + 8 * s2], c0, 0, 0, 0);
-                    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(at[s2], lf[b1 + 8 * s2], c1, 0, 0, 0);
+                for (int s3 = 0; s3 < 3; ++s3) {
+#pragma unroll
+                    for (int s2 = 13 * s3; s2 < 13 * s3 + 13; ++s2) {
+                        bv0[s2] = lf[b0 + 8 * s2];
+                        bv1[s2] = lf[b1 + 8 * s2];
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int s2 = 13 * s3; s2 < 13 * s3 + 13; ++s2) {
+                        c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(at[s2], bv0[s2], c0, 0, 0, 0);
+                        c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(at[s2], bv1[s2], c1, 0, 0, 0);
+                    }
                 }
                 // D: this lane holds rows i = 4 kg + r of its column; output m = 3 U + i
 #pragma unroll
@@ -470,15 +491,17 @@ __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, lon
         __syncthreads();
     };
     const int ntile = (M1 + 4 + TILE_K - 1) / TILE_K;   // tiles with kfirst < M1
-    In pa[5], pb[5];
-    load_tile(pa, 0);
-    load_tile(pb, 1);
+    In pr[PFD][5];
+#pragma unroll
+    for (int d = 0; d < PFD; ++d) load_tile(pr[d], d);
     int t = 0;
-    for (; t + 1 < ntile; t += 2) {
-        tile(t, pa);
-        tile(t + 1, pb);
+    for (; t + PFD <= ntile; t += PFD) {
+#pragma unroll
+        for (int d = 0; d < PFD; ++d) tile(t + d, pr[d]);
     }
-    if (t < ntile) tile(t, pa);
+#pragma unroll
+    for (int d = 0; d < PFD - 1; ++d)
+        if (t + d < ntile) tile(t + d, pr[d]);
     // the last tile ended with a barrier
     if constexpr (FUSE) {
         const float2 *ly = reinterpret_cast<const float2 *>(yb);   // YL: yb holds y[0, M2)
