@@ -56,7 +56,8 @@ def parse():
     ap.add_argument("--pipeline", choices=("auto", "on", "off"), default="auto",
                     help="etsi: overlap the demod of batch k+1 with the lower MAC of batch k on two streams "
                          "(auto: cf32 on; sc16 off -- its demod fills every CU's LDS, so the back-end "
-                         "kernels cannot co-reside and only slow it down)")
+                         "kernels cannot co-reside and only slow it down); compat: run consecutive batches' "
+                         "whole chains on two streams (auto: on)")
     ap.add_argument("--no-pipeline", action="store_true", help="same as --pipeline off")
     ap.add_argument("--host-input", action="store_true",
                     help="etsi: PCIe-inclusive mode -- each batch is copied from pinned host memory (double-buffered "
@@ -109,7 +110,28 @@ def read_profile(c):
 
 
 class CompatStep:
-    """process() + decode() lower MAC over the batch (tetra_demod_compat + tetra_lmac_compat)."""
+    """process() + decode() lower MAC over the batch (tetra_demod_compat + tetra_lmac_compat).
+
+    The chain's IIR passes are sequential per stream by construction (bit-exact scipy order): a
+    batch of 8192 channels is one wave per SIMD, issue-latency bound.  pipeline() runs consecutive
+    batches on two contexts / HIP streams, so batch k+1's kernels interleave with batch k's (two
+    waves per SIMD); every step still does the whole chain for one batch."""
+
+    class _Lane:
+        def __init__(self, c, C, smax, dev):
+            self.c = c
+            self.mc = torch.zeros(C, dtype=torch.float64, device=dev)
+            self.mo = torch.zeros(C, dtype=torch.uint8, device=dev)
+            self.soft = torch.empty((C, smax, 2), dtype=torch.float64, device=dev)
+            self.hard = torch.empty((C, smax), dtype=torch.uint8, device=dev)
+            self.hard64 = torch.empty((C, smax), dtype=torch.int64, device=dev)
+            self.nsym = torch.empty(C, dtype=torch.int32, device=dev)
+            self.nhard = torch.empty(C, dtype=torch.int32, device=dev)
+            self.nsync = torch.empty(C, dtype=torch.int32, device=dev)
+            self.rec = torch.empty((C, _hip.MAX_SYNC, _hip.F_FIELDS), dtype=torch.int32, device=dev)
+            self.fb = torch.empty((C, _hip.MAX_SYNC, 510), dtype=torch.uint8, device=dev)
+            self.bb = torch.empty((C, _hip.MAX_SYNC, 510), dtype=torch.uint8, device=dev)
+            self.stream = None   # torch's current stream
 
     def __init__(self, c, iq, C, N):
         from tetraear.signal.processor import compat_plan
@@ -119,32 +141,46 @@ class CompatStep:
         self.smax = m // self.plan.sps + 1
         dev = iq.device
         self.iq = iq
-        self.mc = torch.zeros(C, dtype=torch.float64, device=dev)
-        self.mo = torch.zeros(C, dtype=torch.uint8, device=dev)
-        self.soft = torch.empty((C, self.smax, 2), dtype=torch.float64, device=dev)
-        self.hard = torch.empty((C, self.smax), dtype=torch.uint8, device=dev)
-        self.hard64 = torch.empty((C, self.smax), dtype=torch.int64, device=dev)
-        self.nsym = torch.empty(C, dtype=torch.int32, device=dev)
-        self.nhard = torch.empty(C, dtype=torch.int32, device=dev)
         self.kmax = torch.from_numpy(cascade_table().copy()).to(dev)
-        self.nsync = torch.empty(C, dtype=torch.int32, device=dev)
-        self.rec = torch.empty((C, _hip.MAX_SYNC, _hip.F_FIELDS), dtype=torch.int32, device=dev)
-        self.fb = torch.empty((C, _hip.MAX_SYNC, 510), dtype=torch.uint8, device=dev)
-        self.bb = torch.empty((C, _hip.MAX_SYNC, 510), dtype=torch.uint8, device=dev)
         self.f32 = ctypes.c_int32(0)
+        self.lanes = [self._Lane(c, C, self.smax, dev)]
+        self.k = 0
+        self.pipelined = False
+
+    def pipeline(self):
+        dev = self.iq.device
+        back = _hip.Context()
+        s = torch.cuda.Stream(device=dev)
+        back.check(back.lib.tetra_set_stream(back.handle, ctypes.c_void_p(s.cuda_stream)), "set_stream")
+        lane = self._Lane(back, self.C, self.smax, dev)
+        lane.stream = s
+        self.lanes.append(lane)
+        self.pipelined = True
+        return self
+
+    def contexts(self):
+        return [ln.c for ln in self.lanes]
+
+    def __getattr__(self, name):   # the first lane's outputs (tests read st.hard, st.nsync, ...)
+        if name in ("soft", "hard", "nsym", "nsync", "rec", "fb", "bb"):
+            return getattr(self.__dict__["lanes"][0], name)
+        raise AttributeError(name)
 
     def __call__(self):
-        c = self.c
-        c.check(c.lib.tetra_demod_compat(c.handle, self.plan, _hip.ptr(self.iq), _hip.TETRA_CF32, self.C, self.N,
-                                         _hip.ptr(self.mc), _hip.ptr(self.mo), _hip.ptr(self.soft),
-                                         _hip.ptr(self.hard), _hip.ptr(self.nsym), self.smax, self.f32), "demod")
-        # hard symbols -> int64 stream rows for the lower MAC (torch ops on the same stream)
-        self.hard64.copy_(self.hard)
-        torch.sub(self.nsym, 1, out=self.nhard)
-        self.nhard.clamp_(min=0)
-        c.check(c.lib.tetra_lmac_compat(c.handle, _hip.ptr(self.hard64), _hip.ptr(self.nhard), self.C, self.smax,
-                                        _hip.ptr(self.kmax), _hip.ptr(self.nsync), _hip.ptr(self.rec),
-                                        _hip.ptr(self.fb), _hip.ptr(self.bb)), "lmac")
+        ln = self.lanes[self.k % len(self.lanes)]
+        self.k += 1
+        c = ln.c
+        with torch.cuda.stream(ln.stream or torch.cuda.current_stream(self.iq.device)):
+            c.check(c.lib.tetra_demod_compat(c.handle, self.plan, _hip.ptr(self.iq), _hip.TETRA_CF32, self.C, self.N,
+                                             _hip.ptr(ln.mc), _hip.ptr(ln.mo), _hip.ptr(ln.soft), _hip.ptr(ln.hard),
+                                             _hip.ptr(ln.nsym), self.smax, self.f32), "demod")
+            # hard symbols -> int64 stream rows for the lower MAC (torch ops on the lane's stream)
+            ln.hard64.copy_(ln.hard)
+            torch.sub(ln.nsym, 1, out=ln.nhard)
+            ln.nhard.clamp_(min=0)
+            c.check(c.lib.tetra_lmac_compat(c.handle, _hip.ptr(ln.hard64), _hip.ptr(ln.nhard), self.C, self.smax,
+                                            _hip.ptr(self.kmax), _hip.ptr(ln.nsync), _hip.ptr(ln.rec),
+                                            _hip.ptr(ln.fb), _hip.ptr(ln.bb)), "lmac")
 
     def algorithmic_bytes_per_sample(self):
         # 8 B cf32 in + per symbol (16 B complex128 soft + 1 B hard) + decoded bits (negligible)
@@ -220,6 +256,8 @@ def main():
         iq = (0.25 * torch.randn((C, N, 2), generator=g, device=dev, dtype=torch.float32))
         iq = torch.round(iq * 32768) / 32768   # SC16 grid, like capture.py:259-269
         step = CompatStep(c, iq, C, N)
+        if (a.pipeline if not a.no_pipeline else "off") != "off":
+            step.pipeline()
     torch.cuda.synchronize(dev)
     ctxs = step.contexts() if hasattr(step, "contexts") else [c]
 

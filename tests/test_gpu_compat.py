@@ -227,3 +227,46 @@ def test_parser_matches_golden(hip, g3):
     assert q._check_sync_pattern(np.array(q.SYNC_CONTINUOUS_DOWNLINK)) is True
     assert q._check_sync_pattern(np.zeros(22, int)) is False
     assert isinstance(q._detect_burst_type(np.zeros(255, int)), BurstType)
+
+
+def test_bench_compat_pipeline_matches_serial(hip):
+    """bench.py --chain compat: the two-stream pipeline (consecutive batches' whole chains on two
+    contexts / streams) gives every batch the serial chain's results."""
+    import os
+    import sys
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    C, N = 64, 131072
+    iq = torch.round(0.25 * torch.randn((C, N, 2), generator=g, device=dev) * 32768) / 32768
+    ser = bench.CompatStep(_hip_ctx_on_torch_stream(), iq, C, N)
+    ser()
+    torch.cuda.synchronize(dev)
+    want = [t.clone() for t in (ser.nsym, ser.hard, ser.soft, ser.nsync, ser.rec)]
+    pip = bench.CompatStep(_hip_ctx_on_torch_stream(), iq, C, N).pipeline()
+    for _ in range(3):
+        pip()
+    torch.cuda.synchronize(dev)
+    for ln in pip.lanes:
+        got = (ln.nsym, ln.hard, ln.soft, ln.nsync, ln.rec)
+        ns = want[0]
+        assert torch.equal(got[0], ns) and torch.equal(got[3], want[3])
+        for ch in range(C):
+            n = int(ns[ch])
+            assert torch.equal(got[1][ch, :n - 1], want[1][ch, :n - 1])
+            assert torch.equal(got[2][ch, :n], want[2][ch, :n])
+            k = int(want[3][ch])
+            assert torch.equal(got[4][ch, :k], want[4][ch, :k])
+
+
+def _hip_ctx_on_torch_stream():
+    import ctypes
+    import torch
+    from tetraear import _hip
+    c = _hip.Context()
+    s = torch.cuda.current_stream(torch.device("cuda", 0))
+    c.check(c.lib.tetra_set_stream(c.handle, ctypes.c_void_p(s.cuda_stream)), "set_stream")
+    return c

@@ -336,3 +336,55 @@ def test_fused_demod_many_channels():
         sym = a[0][ch, :n].cpu().numpy().view(np.complex64)[:, 0]
         assert np.array_equal(sym, so) and np.array_equal(a[2][ch, :n - 1].cpu().numpy(), ho), ch
         assert np.array_equal(a[1][ch, :2 * (n - 1)].cpu().numpy(), sbo), ch
+
+
+def test_c4_full_chain_4096_bursts():
+    """BASELINE configs[3] (C4): the full receive chain -- channel filter, timing, decision, burst
+    sync, descramble, deinterleave, RCPC Viterbi, CRC -- over >= 4096 synthetic TETRA bursts on one
+    GPU (bench.py's step on a C4-sized batch): every CRC-passing block carries a transmitted
+    payload, >= 97 % of the blocks pass at 18 dB Es/N0, and a sample of channels matches the oracle
+    burst for burst and bit for bit."""
+    import torch
+    from tetraear import _hip
+    from tetraear.signal.etsi import BenchStep
+    dev = torch.device("cuda", 0)
+    c = _hip.ctx()
+    C, N = 1536, 131072   # ~2.8 complete bursts per 131072-sample chunk
+    st = BenchStep(c, C, N, 2.4e6, seed=44, device=dev)
+    st()
+    torch.cuda.synchronize(dev)
+    nb = st.nburst.cpu().numpy()
+    assert int(nb.sum()) >= 4096, int(nb.sum())
+    nk, blocks, t1 = st.nblock.cpu().numpy(), st.blocks.cpu().numpy(), st.type1.cpu().numpy()
+    payload = st.payload.cpu().numpy()
+    n1 = {0: 268, 1: 124, 2: 60}
+    nblk = nok = 0
+    for ch in range(C):
+        sent = {tuple(p) for bb in payload[ch] for p in bb}
+        for j in range(int(nk[ch])):
+            kind, ok = int(blocks[ch, j, 0]), int(blocks[ch, j, 1])
+            nblk += 1
+            if ok:
+                nok += 1
+                bits = np.pad(t1[ch, j, :n1[kind]], (0, 268 - n1[kind]))
+                assert tuple(bits) in sent, (ch, j)
+    assert nok / nblk > 0.97, (nok, nblk)
+    # oracle, burst for burst, on a sample of channels
+    rx = E.Receiver()
+    soft, hard, ns = st.soft.cpu().numpy(), st.hard.cpu().numpy(), st.nsym.cpu().numpy()
+    cells = st.cells.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+    iq = st.iq
+    for ch in (0, 511, 1024, C - 1):
+        x = iq[ch].cpu().numpy().view(np.complex64)[:, 0]
+        so, sbo, ho, _ = rx.demod(x)
+        n = int(ns[ch])
+        assert n == len(so) and np.array_equal(hard[ch, :n - 1], ho) and np.array_equal(soft[ch, :2 * (n - 1)], sbo)
+        want = rx.lower_mac(sbo, ho, int(cells[ch]))
+        assert len(want) == int(nb[ch])
+        k = 0
+        for start, bk, blks in want:
+            for _, tb, okb in blks:
+                assert int(blocks[ch, k, 1]) == int(bool(okb))
+                assert np.array_equal(t1[ch, k, :len(tb)], tb)
+                k += 1
+        assert k == int(nk[ch])

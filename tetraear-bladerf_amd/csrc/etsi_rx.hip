@@ -134,16 +134,23 @@ __device__ __forceinline__ float2 csqrt_p(float x, float y) {
     return make_float2(y / (2.0f * s), s);
 }
 
-// The timing + decision stage for one channel, run by one wave (lane = 0..63).  y / dp may point
-// to global memory (k_timing) or LDS (k_demod_fused); every cross-lane exchange is a wave
-// reduction or shuffle, so no workgroup barrier is needed.
-__device__ __forceinline__ void timing_wave(const float2 *y, int M2, float gain, float soft_scale, float2 *sp,
-                                            float2 *dp, int8_t *sb, uint8_t *hp, int32_t *nsym_ch, float4 *diag_ch,
-                                            int smax, int lane) {
-    if (M2 < 16) {
-        if (lane == 0) *nsym_ch = 0;
-        return;
-    }
+// The timing + decision stage for one channel.  timing_track runs on one wave (lane = 0..63): the
+// Oerder-Meyr phase, block-Gardner tracking, and the CFO sums, which are folded into the Gardner
+// blocks (lane l produces the symbols j = 64 b + l, ascending -- the order the oracle's CFO loop
+// sums them in), so no second pass over d is needed; it leaves d_j in dp and returns the CFO
+// rotation and soft scale.  timing_decide (the decision pass: rotation, int8 soft bits, hard
+// dibits) is elementwise and is shared by `nw` waves.  y / dp may point to global memory (k_timing)
+// or LDS (the fused demod); every cross-lane exchange in timing_track is a wave reduction or
+// shuffle, so it needs no workgroup barrier.
+struct TrackOut {
+    int S;
+    float rr, ri, sc, base, delta;
+};
+
+__device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float gain, float soft_scale, float2 *sp,
+                                                 float2 *dp, int smax, int lane) {
+    TrackOut o{0, 1.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    if (M2 < 16) return o;
     // Oerder-Meyr: class sums of |y|^2 over n mod 4 (loads issued 8 ahead; same summation order)
     float s = 0.f;
     for (int n0 = lane; n0 < M2; n0 += 8 * 64) {
@@ -165,6 +172,7 @@ __device__ __forceinline__ void timing_wave(const float2 *y, int M2, float gain,
     int S = 0;
     float2 prev = make_float2(0.f, 0.f);
     bool have_prev = false;
+    float zr = 0.f, zi = 0.f, am = 0.f;   // CFO sums over this lane's d_j
     for (int kb = kstart;; kb += 64) {
         const float off = base + delta;
         const float t = (float)(4 * (kb + lane)) + off;
@@ -183,7 +191,14 @@ __device__ __forceinline__ void timing_wave(const float2 *y, int M2, float gain,
                 const float dr = on.x - pv.x, di = on.y - pv.y;
                 ev = fmaf(dr, mid.x, di * mid.y);
                 const int j = S + lane;
-                dp[j - 1] = make_float2(fmaf(on.x, pv.x, on.y * pv.y), fmaf(on.y, pv.x, -(on.x * pv.y)));
+                const float xr = fmaf(on.x, pv.x, on.y * pv.y), xi = fmaf(on.y, pv.x, -(on.x * pv.y));
+                dp[j - 1] = make_float2(xr, xi);
+                // CFO: 4th power and magnitude of d_j (j = lane mod 64, ascending: the oracle's order)
+                const float sr = fmaf(xr, xr, -(xi * xi)), si = (xr * xi) * 2.0f;
+                const float qr = fmaf(sr, sr, -(si * si)), qi = (sr * si) * 2.0f;
+                zr += qr;
+                zi += qi;
+                am += sqrtf(fmaf(xr, xr, xi * xi));
             }
             sp[S + lane] = on;
         }
@@ -198,29 +213,7 @@ __device__ __forceinline__ void timing_wave(const float2 *y, int M2, float gain,
         S += nv;
         if (nv < 64) break;
     }
-    __threadfence_block();   // dp written by other lanes above is read below
-    // CFO (4th power) and soft scale; lane l owns d_j with j & 63 == l, ascending j
-    float zr = 0.f, zi = 0.f, am = 0.f;
-    for (int j0 = lane; j0 < S; j0 += 4 * 64) {   // j = j0 + 64u, j >= 1; loads issued 4 ahead
-        float2 dv[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int j = j0 + 64 * u;
-            dv[u] = (j >= 1 && j < S) ? dp[j - 1] : make_float2(0.f, 0.f);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int j = j0 + 64 * u;
-            if (j >= 1 && j < S) {
-                const float2 d = dv[u];
-                const float sr = fmaf(d.x, d.x, -(d.y * d.y)), si = (d.x * d.y) * 2.0f;
-                const float qr = fmaf(sr, sr, -(si * si)), qi = (sr * si) * 2.0f;
-                zr += qr;
-                zi += qi;
-                am += sqrtf(fmaf(d.x, d.x, d.y * d.y));
-            }
-        }
-    }
+    // CFO rotation conj((-Z/|Z|)^(1/4)) and the soft scale from the mean |d|
     const float Zr = wave_sum(zr), Zi = wave_sum(zi), A = wave_sum(am);
     float rr = 1.0f, ri = 0.0f;
     const float zm = sqrtf(fmaf(Zr, Zr, Zi * Zi));
@@ -230,28 +223,47 @@ __device__ __forceinline__ void timing_wave(const float2 *y, int M2, float gain,
         rr = w.x;
         ri = -w.y;
     }
-    const float sc = (S > 1 && A > 0.0f) ? soft_scale / (A / (float)(S - 1)) : 0.0f;
-    for (int j0 = 1 + lane; j0 < S; j0 += 4 * 64) {
+    o.S = S;
+    o.rr = rr;
+    o.ri = ri;
+    o.sc = (S > 1 && A > 0.0f) ? soft_scale / (A / (float)(S - 1)) : 0.0f;
+    o.base = base;
+    o.delta = delta;
+    return o;
+}
+
+// Decision pass over d_j, j in [1, S): wave w of nw takes the 64-symbol blocks w, w + nw, ...
+__device__ __forceinline__ void timing_decide(const TrackOut &o, const float2 *dp, int8_t *sb, uint8_t *hp, int w,
+                                              int nw, int lane) {
+    for (int j0 = 1 + 64 * w + lane; j0 < o.S; j0 += 4 * 64 * nw) {
         float2 dv[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) dv[u] = j0 + 64 * u < S ? dp[j0 + 64 * u - 1] : make_float2(0.f, 0.f);
+        for (int u = 0; u < 4; ++u) dv[u] = j0 + 64 * nw * u < o.S ? dp[j0 + 64 * nw * u - 1] : make_float2(0.f, 0.f);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-        const int j = j0 + 64 * u;
-        if (j >= S) break;
-        const float2 d = dv[u];
-        const float xr = fmaf(d.x, rr, -(d.y * ri)), xi = fmaf(d.x, ri, d.y * rr);
-        float q1 = rintf(xi * sc), q2 = rintf(xr * sc);
-        q1 = q1 > 127.f ? 127.f : (q1 < -127.f ? -127.f : q1);
-        q2 = q2 > 127.f ? 127.f : (q2 < -127.f ? -127.f : q2);
-        sb[2 * (j - 1)] = (int8_t)q1;
-        sb[2 * (j - 1) + 1] = (int8_t)q2;
-        hp[j - 1] = (uint8_t)(((xi < 0.0f) << 1) | (xr < 0.0f));
+            const int j = j0 + 64 * nw * u;
+            if (j >= o.S) break;
+            const float2 d = dv[u];
+            const float xr = fmaf(d.x, o.rr, -(d.y * o.ri)), xi = fmaf(d.x, o.ri, d.y * o.rr);
+            float q1 = rintf(xi * o.sc), q2 = rintf(xr * o.sc);
+            q1 = q1 > 127.f ? 127.f : (q1 < -127.f ? -127.f : q1);
+            q2 = q2 > 127.f ? 127.f : (q2 < -127.f ? -127.f : q2);
+            sb[2 * (j - 1)] = (int8_t)q1;
+            sb[2 * (j - 1) + 1] = (int8_t)q2;
+            hp[j - 1] = (uint8_t)(((xi < 0.0f) << 1) | (xr < 0.0f));
         }
     }
+}
+
+__device__ __forceinline__ void timing_wave(const float2 *y, int M2, float gain, float soft_scale, float2 *sp,
+                                            float2 *dp, int8_t *sb, uint8_t *hp, int32_t *nsym_ch, float4 *diag_ch,
+                                            int smax, int lane) {
+    const TrackOut o = timing_track(y, M2, gain, soft_scale, sp, dp, smax, lane);
+    __threadfence_block();   // dp written by other lanes is read below
+    timing_decide(o, dp, sb, hp, 0, 1, lane);
     if (lane == 0) {
-        *nsym_ch = S;
-        if (diag_ch) *diag_ch = make_float4(base, delta, rr, ri);
+        *nsym_ch = o.S;
+        if (diag_ch && M2 >= 16) *diag_ch = make_float4(o.base, o.delta, o.rr, o.ri);
     }
 }
 
@@ -525,13 +537,22 @@ __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, lon
             ly = yl;
             scr = yl + M2;
         }
+        // the tracking is this workgroup's serial tail (wave 0, prioritised on its SIMD); the decision
+        // pass after it is shared by all four waves (the rotation and scale go through LDS)
+        const size_t so = (size_t)ch * to.smax;
+        __shared__ TrackOut tro;
         if (tid < 64) {
-            // the timing pass is this workgroup's serial tail: let it win issue slots on its SIMD
             __builtin_amdgcn_s_setprio(3);
-            const size_t so = (size_t)ch * to.smax;
-            timing_wave(ly, M2, to.gain, to.soft_scale, to.sym + so, scr, to.softbits + 2 * so, to.hard + so,
-                        to.nsym + ch, to.diag ? to.diag + ch : nullptr, to.smax, tid);
+            const TrackOut o = timing_track(ly, M2, to.gain, to.soft_scale, to.sym + so, scr, to.smax, tid);
+            if (tid == 0) {
+                tro = o;
+                to.nsym[ch] = o.S;
+                if (to.diag && M2 >= 16) to.diag[ch] = make_float4(o.base, o.delta, o.rr, o.ri);
+            }
         }
+        __syncthreads();
+        const TrackOut o = tro;
+        timing_decide(o, scr, to.softbits + 2 * so, to.hard + so, wv, 4, lane);
     } else if constexpr (YL) {
         flush(M2);
     }
