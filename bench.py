@@ -59,6 +59,8 @@ def parse():
                          "kernels cannot co-reside and only slow it down); compat: run consecutive batches' "
                          "whole chains on two streams (auto: on)")
     ap.add_argument("--no-pipeline", action="store_true", help="same as --pipeline off")
+    ap.add_argument("--compat-lanes", type=int, default=2,
+                    help="compat pipeline: batches in flight (contexts / streams)")
     ap.add_argument("--host-input", action="store_true",
                     help="etsi: PCIe-inclusive mode -- each batch is copied from pinned host memory (double-buffered "
                          "copy stream); value is then the host-fed rate, never the HBM-resident headline")
@@ -147,14 +149,15 @@ class CompatStep:
         self.k = 0
         self.pipelined = False
 
-    def pipeline(self):
+    def pipeline(self, lanes=2):
         dev = self.iq.device
-        back = _hip.Context()
-        s = torch.cuda.Stream(device=dev)
-        back.check(back.lib.tetra_set_stream(back.handle, ctypes.c_void_p(s.cuda_stream)), "set_stream")
-        lane = self._Lane(back, self.C, self.smax, dev)
-        lane.stream = s
-        self.lanes.append(lane)
+        for _ in range(lanes - 1):
+            back = _hip.Context()
+            s = torch.cuda.Stream(device=dev)
+            back.check(back.lib.tetra_set_stream(back.handle, ctypes.c_void_p(s.cuda_stream)), "set_stream")
+            lane = self._Lane(back, self.C, self.smax, dev)
+            lane.stream = s
+            self.lanes.append(lane)
         self.pipelined = True
         return self
 
@@ -257,7 +260,7 @@ def main():
         iq = torch.round(iq * 32768) / 32768   # SC16 grid, like capture.py:259-269
         step = CompatStep(c, iq, C, N)
         if (a.pipeline if not a.no_pipeline else "off") != "off":
-            step.pipeline()
+            step.pipeline(a.compat_lanes)
     torch.cuda.synchronize(dev)
     ctxs = step.contexts() if hasattr(step, "contexts") else [c]
 
