@@ -57,7 +57,8 @@ def parse():
                     help="etsi: overlap the demod of batch k+1 with the lower MAC of batch k on two streams "
                          "(auto: cf32 on; sc16 off -- its demod fills every CU's LDS, so the back-end "
                          "kernels cannot co-reside and only slow it down); compat: run consecutive batches' "
-                         "whole chains on two streams (auto: on)")
+                         "whole chains on two streams (auto: on); wideband: channeliser of capture k+1 beside "
+                         "the timing + lower MAC of capture k (auto: on)")
     ap.add_argument("--no-pipeline", action="store_true", help="same as --pipeline off")
     ap.add_argument("--compat-lanes", type=int, default=2,
                     help="compat pipeline: batches in flight (contexts / streams)")
@@ -244,6 +245,8 @@ def main():
     if a.chain == "wideband":
         from tetraear.signal.wideband import BenchStep as WbStep
         step = WbStep(c, a.wb_samples, seed=rank_seed(1000, rank), device=dev)
+        if (a.pipeline if not a.no_pipeline else "off") != "off":
+            step.pipeline()
         C, N = 1, a.wb_samples   # units: wideband samples
     elif a.chain == "etsi":
         from tetraear.signal.etsi import BenchStep as EtsiStep

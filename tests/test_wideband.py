@@ -134,3 +134,33 @@ def test_wideband_round_trip(capture):
                     assert tuple(np.pad(b["bits"], (0, 268 - len(b["bits"])))) in sent
     assert nblk >= 2 * M
     assert nok / nblk > 0.97, (nok, nblk)
+
+
+@pytest.mark.gpu
+def test_bench_wideband_pipeline_matches_serial():
+    """bench.py --chain wideband: the two-stream pipeline (channeliser of capture k+1 beside the
+    timing + lower MAC of capture k, y double-buffered) gives every step the serial chain's results."""
+    import torch
+    from tetraear import _hip
+    from tetraear.signal.wideband import BenchStep
+    dev = torch.device("cuda", 0)
+    outs = []
+    for pipe in (False, True):
+        c = _hip.Context()
+        c.check(c.lib.tetra_set_stream(c.handle, None), "set_stream")
+        st = BenchStep(c, 2_000_000, seed=3, device=dev)
+        if pipe:
+            st.pipeline()
+        for _ in range(3):
+            st()
+        torch.cuda.synchronize(dev)
+        ns, nb, nk = st.nsym.cpu(), st.nburst.cpu(), st.nblock.cpu()
+        soft, hard, blocks, t1 = st.soft.cpu(), st.hard.cpu(), st.blocks.cpu(), st.type1.cpu()
+        n1 = {0: 268, 1: 124, 2: 60}
+        outs.append([ns, nb, nk, st.wf.cpu()] + [x for ch in range(st.C) for x in (
+            soft[ch, :2 * max(int(ns[ch]) - 1, 0)], hard[ch, :max(int(ns[ch]) - 1, 0)],
+            blocks[ch, :int(nk[ch])])] + [t1[ch, j, :n1[int(blocks[ch, j, 0])]] for ch in range(st.C)
+                                          for j in range(int(nk[ch]))])
+        assert st.quality()["crc_ok"] > 0
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)

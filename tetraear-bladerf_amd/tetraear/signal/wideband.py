@@ -166,21 +166,60 @@ class BenchStep:
         self.wf = torch.empty((self.nfr, 2048), dtype=torch.float32, device=device)
         self.pipelined = False
 
-    def contexts(self):
-        return [self.c]
+    def pipeline(self):
+        """Two-stage software pipeline over consecutive captures: waterfall + channeliser of step k+1
+        on the front stream while the per-carrier timing + lower MAC of step k run on a back stream
+        (its own context).  The carrier samples y are what crosses the streams: double-buffered,
+        each stage waits only on the event that protects its buffer.  Every step still does the
+        whole chain."""
+        import torch
+        dev = self.x.device
+        self.back = _hip.Context()
+        self.s_front = torch.cuda.current_stream(dev)
+        self.s_back = torch.cuda.Stream(device=dev)
+        self.back.check(self.back.lib.tetra_set_stream(self.back.handle, ctypes.c_void_p(self.s_back.cuda_stream)),
+                        "set_stream")
+        self.back.check(self.back.lib.tetra_etsi_set_cells(self.back.handle, _hip.ptr(self.cells), self.C), "set_cells")
+        self.ys = [self.y, torch.empty_like(self.y)]
+        self.ev_front = [torch.cuda.Event() for _ in range(2)]
+        self.ev_back = [torch.cuda.Event() for _ in range(2)]
+        for e in self.ev_back:
+            e.record(self.s_back)
+        self.k = 0
+        self.pipelined = True
+        return self
 
-    def __call__(self):
-        c = self.c
+    def contexts(self):
+        return [self.c] + ([self.back] if self.pipelined else [])
+
+    def _front(self, c, y):
         c.check(c.lib.tetra_waterfall(c.handle, _hip.ptr(self.x), _hip.TETRA_CF32, 1, self.Nw, 2048, 2048, self.nfr,
                                       _hip.ptr(self.wf)), "waterfall")
-        c.check(c.lib.tetra_channelize(c.handle, self.plan.c, _hip.ptr(self.x), self.Nw, _hip.ptr(self.y),
+        c.check(c.lib.tetra_channelize(c.handle, self.plan.c, _hip.ptr(self.x), self.Nw, _hip.ptr(y),
                                        self.nchunk * self.m2), "channelize")
-        c.check(c.lib.tetra_etsi_timing(c.handle, self.etsi, _hip.ptr(self.y), self.C, self.m2, _hip.ptr(self.sym),
+
+    def _back(self, c, y):
+        c.check(c.lib.tetra_etsi_timing(c.handle, self.etsi, _hip.ptr(y), self.C, self.m2, _hip.ptr(self.sym),
                                         _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.sm, None),
                 "etsi_timing")
         c.check(c.lib.tetra_lmac_etsi(c.handle, _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.C,
                                       self.sm, _hip.ptr(self.nburst), _hip.ptr(self.bursts), _hip.ptr(self.nblock),
                                       _hip.ptr(self.blocks), _hip.ptr(self.type1)), "lmac_etsi")
+
+    def __call__(self):
+        if not self.pipelined:
+            self._front(self.c, self.y)
+            self._back(self.c, self.y)
+            return
+        i = self.k & 1
+        self.k += 1
+        y = self.ys[i]
+        self.s_front.wait_event(self.ev_back[i])   # the timing two steps back has consumed y[i]
+        self._front(self.c, y)
+        self.ev_front[i].record(self.s_front)
+        self.s_back.wait_event(self.ev_front[i])
+        self._back(self.back, y)
+        self.ev_back[i].record(self.s_back)
 
     def stage_bytes(self):
         """Algorithmic bytes per wideband input sample of each timed stage (cf32 = 8 B):
@@ -200,7 +239,7 @@ class BenchStep:
                             f"{self.plan.M} carriers x {self.nchunk} timing chunks of {self.m2}",
                 "wideband_samples_per_gpu": self.Nw, "sample_rate": self.fs, "carriers": self.plan.M,
                 "timing_chunks_per_carrier": self.nchunk, "parallelism": f"capture-sharded x{world}",
-                "pipeline": False}
+                "pipeline": self.pipelined}
 
     def realtime_channels(self, value_msps):
         return value_msps * 1e6 / self.fs * self.plan.M   # carriers served at real time
