@@ -343,8 +343,11 @@ struct TimingOut {
     int smax;
 };
 
+// SC16 is held to 128 VGPRs: four workgroups per CU (its LDS allows four; at 158-161 VGPRs it ran at
+// three, 1.10 -> 1.57 ms per batch)
+template <typename In> constexpr int cf_waves() { return std::is_same<In, float4>::value ? 2 : 4; }
 template <typename In, bool FUSE>
-__global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, long N, int M1, int M2,
+__global__ __launch_bounds__(256, cf_waves<In>()) void k_chanfilt(const In *__restrict__ iq, long N, int M1, int M2,
                                                   const float *__restrict__ h1, const float *__restrict__ afrag,
                                                   float2 *__restrict__ y, TimingOut to) {
     constexpr bool YL = std::is_same<In, float4>::value;
@@ -416,13 +419,22 @@ __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, lon
         if (k >= 0 && k < M1) {
             const float4 *w = xin + 5 * tid + 4;
             pf2 a = {0.f, 0.f};
+            if constexpr (YL) {
 #pragma unroll
-            for (int q = 0; q < 12; ++q) {
-                const float4 t4 = htap[q], x0 = w[2 * q], x1 = w[2 * q + 1];
-                a = pfma(t4.x, pf2{x0.x, x0.y}, a);
-                a = pfma(t4.y, pf2{x0.z, x0.w}, a);
-                a = pfma(t4.z, pf2{x1.x, x1.y}, a);
-                a = pfma(t4.w, pf2{x1.z, x1.w}, a);
+                for (int q = 0; q < 12; ++q) {
+                    const float4 t4 = htap[q], x0 = w[2 * q], x1 = w[2 * q + 1];
+                    a = pfma(t4.x, pf2{x0.x, x0.y}, a);
+                    a = pfma(t4.y, pf2{x0.z, x0.w}, a);
+                    a = pfma(t4.z, pf2{x1.x, x1.y}, a);
+                    a = pfma(t4.w, pf2{x1.z, x1.w}, a);
+                }
+            } else {   // SC16 keeps the scalar taps (VGPR budget, below)
+#pragma unroll
+                for (int jj = 0; jj < 24; ++jj) {
+                    const float4 v = w[jj];
+                    a = pfma(h1[2 * jj], pf2{v.x, v.y}, a);
+                    a = pfma(h1[2 * jj + 1], pf2{v.z, v.w}, a);
+                }
             }
             lin[k - kbase] = make_float2(a.x, a.y);
         }
@@ -454,21 +466,30 @@ __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, lon
                 const int b0 = U0 <= u_hi ? 2 * (10 * U0 - kbase + kg) + comp : 2 * kg + comp;
                 const int b1 = U1 <= u_hi ? 2 * (10 * U1 - kbase + kg) + comp : 2 * kg + comp;
                 f4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
-                // B operands a third of the chain ahead (hipcc otherwise waits lgkmcnt(0), one LDS
-                // round trip, before each MFMA pair)
-                float bv0[S2K], bv1[S2K];
+                if constexpr (YL) {
+                    // B operands a third of the chain ahead (hipcc otherwise waits lgkmcnt(0), one
+                    // LDS round trip, before each MFMA pair).  Not for SC16: the 26 extra VGPRs
+                    // take it from 120 to 161, four workgroups per CU to three (1.10 -> 1.57 ms)
+                    float bv0[S2K], bv1[S2K];
 #pragma unroll
-                for (int s3 = 0; s3 < 3; ++s3) {
+                    for (int s3 = 0; s3 < 3; ++s3) {
 #pragma unroll
-                    for (int s2 = 13 * s3; s2 < 13 * s3 + 13; ++s2) {
-                        bv0[s2] = lf[b0 + 8 * s2];
-                        bv1[s2] = lf[b1 + 8 * s2];
+                        for (int s2 = 13 * s3; s2 < 13 * s3 + 13; ++s2) {
+                            bv0[s2] = lf[b0 + 8 * s2];
+                            bv1[s2] = lf[b1 + 8 * s2];
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int s2 = 13 * s3; s2 < 13 * s3 + 13; ++s2) {
+                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(at[s2], bv0[s2], c0, 0, 0, 0);
+                            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(at[s2], bv1[s2], c1, 0, 0, 0);
+                        }
                     }
-                    __builtin_amdgcn_sched_barrier(0);
+                } else {
 #pragma unroll
-                    for (int s2 = 13 * s3; s2 < 13 * s3 + 13; ++s2) {
-                        c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(at[s2], bv0[s2], c0, 0, 0, 0);
-                        c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(at[s2], bv1[s2], c1, 0, 0, 0);
+                    for (int s2 = 0; s2 < S2K; ++s2) {
+                        c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(at[s2], lf[b0 + 8 * s2], c0, 0, 0, 0);
+                        c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(at[s2], lf[b1 + 8 * s2], c1, 0, 0, 0);
                     }
                 }
                 // D: this lane holds rows i = 4 kg + r of its column; output m = 3 U + i
@@ -503,17 +524,18 @@ __global__ __launch_bounds__(256) void k_chanfilt(const In *__restrict__ iq, lon
         __syncthreads();
     };
     const int ntile = (M1 + 4 + TILE_K - 1) / TILE_K;   // tiles with kfirst < M1
-    In pr[PFD][5];
-#pragma unroll
-    for (int d = 0; d < PFD; ++d) load_tile(pr[d], d);
+    // two register sets, explicitly (a pr[PFD][5] array with unrolled loops over it cost 22-30 VGPRs:
+    // SC16 at 142 instead of 120 lost its fourth workgroup per CU)
+    static_assert(PFD == 2, "pa / pb below");
+    In pa[5], pb[5];
+    load_tile(pa, 0);
+    load_tile(pb, 1);
     int t = 0;
-    for (; t + PFD <= ntile; t += PFD) {
-#pragma unroll
-        for (int d = 0; d < PFD; ++d) tile(t + d, pr[d]);
+    for (; t + 1 < ntile; t += 2) {
+        tile(t, pa);
+        tile(t + 1, pb);
     }
-#pragma unroll
-    for (int d = 0; d < PFD - 1; ++d)
-        if (t + d < ntile) tile(t + d, pr[d]);
+    if (t < ntile) tile(t, pa);
     // the last tile ended with a barrier
     if constexpr (FUSE) {
         const float2 *ly = reinterpret_cast<const float2 *>(yb);   // YL: yb holds y[0, M2)
