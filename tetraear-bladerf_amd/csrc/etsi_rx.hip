@@ -343,6 +343,26 @@ struct TimingOut {
     int smax;
 };
 
+// The fused demod's timing stage for channel ch on y in LDS (ly), after the workgroup's last barrier:
+// the tracking is the serial tail (wave 0, prioritised on its SIMD); the decision pass after it is
+// shared by all four waves (the rotation and scale go through LDS, *tro).
+__device__ __forceinline__ void timing_tail(const float2 *ly, float2 *scr, const TimingOut &to, int M2, int ch,
+                                            int tid, TrackOut *tro) {
+    const size_t so = (size_t)ch * to.smax;
+    if (tid < 64) {
+        __builtin_amdgcn_s_setprio(3);
+        const TrackOut o = timing_track(ly, M2, to.gain, to.soft_scale, to.sym + so, scr, to.smax, tid);
+        if (tid == 0) {
+            *tro = o;
+            to.nsym[ch] = o.S;
+            if (to.diag && M2 >= 16) to.diag[ch] = make_float4(o.base, o.delta, o.rr, o.ri);
+        }
+    }
+    __syncthreads();
+    const TrackOut o = *tro;
+    timing_decide(o, scr, to.softbits + 2 * so, to.hard + so, tid >> 6, 4, tid & 63);
+}
+
 // SC16 is held to 128 VGPRs: four workgroups per CU (its LDS allows four; at 158-161 VGPRs it ran at
 // three, 1.10 -> 1.57 ms per batch)
 template <typename In> constexpr int cf_waves() { return std::is_same<In, float4>::value ? 2 : 4; }
@@ -559,24 +579,189 @@ __global__ __launch_bounds__(256, cf_waves<In>()) void k_chanfilt(const In *__re
             ly = yl;
             scr = yl + M2;
         }
-        // the tracking is this workgroup's serial tail (wave 0, prioritised on its SIMD); the decision
-        // pass after it is shared by all four waves (the rotation and scale go through LDS)
-        const size_t so = (size_t)ch * to.smax;
         __shared__ TrackOut tro;
-        if (tid < 64) {
-            __builtin_amdgcn_s_setprio(3);
-            const TrackOut o = timing_track(ly, M2, to.gain, to.soft_scale, to.sym + so, scr, to.smax, tid);
-            if (tid == 0) {
-                tro = o;
-                to.nsym[ch] = o.S;
-                if (to.diag && M2 >= 16) to.diag[ch] = make_float4(o.base, o.delta, o.rr, o.ri);
-            }
-        }
-        __syncthreads();
-        const TrackOut o = tro;
-        timing_decide(o, scr, to.softbits + 2 * so, to.hard + so, wv, 4, lane);
+        timing_tail(ly, scr, to, M2, ch, tid, &tro);
     } else if constexpr (YL) {
         flush(M2);
+    }
+}
+
+// --------------------------------------------------------------------------- per-wave channel filter
+// cf32 with y in LDS (M2 <= YLDS): the workgroup's waves stream the channel's quarters
+// independently.  Wave w owns the stage-2 triples [U_w, U_w+1) and the stage-1 outputs
+// [K_w, K_w+1), K_w = 10 U_w (the last wave's end is M1), in 640-sample wave tiles (one stage-1
+// output per lane, five 16-B loads per lane, two tiles in flight) with its own LDS image and
+// stage-1 buffer, and runs a one-MFMA-tile stage-2 burst (40 triples: one dependent chain of 39
+// MFMAs) whenever 40 triples have their windows.  So the stream has no workgroup barrier until the
+// channel ends, and a burst stalls one wave's quarter of the loads in flight instead of the whole
+// workgroup's (k_chanfilt: every wave waits at the tile's barriers while three of them run the
+// burst's MFMA pairs).  Wave w's last triples need stage-1 outputs up to K_w+1 + 103, the first
+// ones of wave w + 1, which that wave also copies into a seam buffer; after the one barrier at the
+// channel's end each wave appends its seam and runs its last bursts, then the timing tail as in
+// k_chanfilt.  Every output is the same fma chain as in k_chanfilt (bit-identical to the oracle).
+constexpr int WT_IN4 = 320;                 // sample pairs per wave tile (640 samples)
+constexpr int WIMG4 = HALO / 2 + WT_IN4;    // wave image (float4): 48-sample halo + the tile
+constexpr int WLR = 664;                    // wave stage-1 buffer (float2): the windows of <= 51 triples
+constexpr int SEAM = 112;                   // >= the 104 outputs a left neighbour's last triples need
+constexpr int UMIN = 16;                    // triples per wave at least (10 UMIN >= SEAM)
+constexpr int WSMEM4 = 14 + 4 * WIMG4 + (4 * WLR + 3 * SEAM + YLDS) / 2;   // float4
+static_assert(WSMEM4 * 16 <= 80 * 1024, "per-wave demod LDS: two workgroups per CU");
+static_assert(sizeof(TrackOut) <= 32 && (4 * WLR + 3 * SEAM) % 2 == 0, "per-wave demod LDS carving");
+
+// cross-lane LDS hand-off inside one wave: a wave's LDS instructions execute in order, so only the
+// compiler has to be kept from moving accesses across this point (no s_waitcnt, no s_barrier)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <bool FUSE>
+__global__ __launch_bounds__(256, 2) void k_chanfilt_w(const float4 *__restrict__ iq, long N, int M1, int M2,
+                                                       const float *__restrict__ h1, const float *__restrict__ afrag,
+                                                       float2 *__restrict__ y, TimingOut to) {
+    // one LDS array, carved by hand: the taps first, so their broadcast reads address them with the
+    // instruction's 16-bit offset from one zero register (past 64 KiB each needs an address VGPR)
+    __shared__ float4 smem[WSMEM4];
+    float4 *htap = smem;                                                      // 12 stage-1 tap quads
+    TrackOut *tro = reinterpret_cast<TrackOut *>(smem + 12);                  // 2 float4
+    float4 *img = smem + 14;                                                  // 4 wave images
+    float2 *lin_all = reinterpret_cast<float2 *>(img + 4 * WIMG4);            // 4 stage-1 buffers
+    float2 *seam = lin_all + 4 * WLR;   // seam[w - 1]: wave w's first SEAM stage-1 outputs
+    float *yb = reinterpret_cast<float *>(seam + 3 * SEAM);                   // y as (re, im) floats
+    const int ch = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: the partition below is scalar
+    if (tid < 12)
+        htap[tid] = make_float4(h1[4 * tid], h1[4 * tid + 1], h1[4 * tid + 2], h1[4 * tid + 3]);
+    float4 *xw = img + wv * WIMG4;
+    float2 *lin = lin_all + wv * WLR;
+    // stage 2 reads whole windows, zero taps included: every entry must be finite
+    for (int i = lane; i < WLR; i += 64) lin[i] = make_float2(0.f, 0.f);
+    float at[S2K];
+#pragma unroll
+    for (int k = 0; k < S2K; ++k) at[k] = afrag[64 * k + lane];
+    // landed before the stream starts (else hipcc re-waits for them inside the loop, behind the
+    // prefetch loads)
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) (gfx9 encoding: expcnt 7, lgkmcnt 15 = no wait)
+    // the partition: nw waves of UQ triples (fewer waves for short chunks, so that every wave but
+    // the last owns >= SEAM stage-1 outputs)
+    const int UT = (M2 + 2) / 3;
+    const int nw = min(4, max(1, UT / UMIN));
+    const int UQ = (UT + nw - 1) / nw;
+    const bool active = wv < nw;
+    const bool has_right = wv + 1 < nw;
+    const int u_beg = min(wv * UQ, UT), u_end = has_right ? (wv + 1) * UQ : UT;
+    const int K0 = 10 * u_beg, K1 = has_right ? 10 * u_end : M1;
+    const int ntile = active ? (K1 - K0 + 4 + 63) / 64 : 0;   // wave tiles with kfirst < K1
+    // tile t: lane l computes x240[K0 + 64 t - 4 + l] from samples 10 K0 + 640 t - 40 + 10 l + [0, 48),
+    // image float4 4 + 5 l + [0, 24); loads past the wave's last needed pair re-read that pair
+    const float4 *xp = iq + (size_t)ch * (N / 2) + 5L * K0;
+    const int qlast = active ? (int)(min(5L * (K1 - 1) + 23, N / 2 - 1) - 5L * K0) : 0;
+    auto load_tile = [&](float4 (&pf)[5], int t) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < 5; ++r) pf[r] = ld_nt(xp + min(t * WT_IN4 + r * 64 + lane, qlast));
+    };
+    int kbase = K0;      // x240 index of lin[0]
+    int u_done = u_beg;  // triples [u_beg, u_done) are in yb
+    const int kg = lane >> 4, seg = (lane & 15) >> 1, comp = lane & 1;
+    const float *lf = reinterpret_cast<const float *>(lin);
+    // one MFMA tile: triples [u_done, u_done + 40) as 8 segments x 5 (columns = 2 seg + comp), only
+    // triples < u_lim stored; a column past u_lim reads the buffer's start (finite, never stored)
+    auto burst = [&](int u_lim) __attribute__((always_inline)) {
+        const int U0 = u_done + S2Q * seg;
+        const int b0 = U0 < u_lim ? 2 * (10 * U0 - kbase + kg) + comp : 2 * kg + comp;
+        // B operands one 13-step chunk ahead of the MFMAs that use them (hipcc otherwise waits one
+        // LDS round trip before every MFMA pair of the dependent chain)
+        float bv[S2K];
+        f4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s2 = 0; s2 < 13; ++s2) bv[s2] = lf[b0 + 8 * s2];
+#pragma unroll
+        for (int s3 = 0; s3 < 3; ++s3) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (s3 < 2) {
+#pragma unroll
+                for (int s2 = 13 * s3 + 13; s2 < 13 * s3 + 26; ++s2) bv[s2] = lf[b0 + 8 * s2];
+            }
+#pragma unroll
+            for (int s2 = 13 * s3; s2 < 13 * s3 + 13; ++s2)
+                c = __builtin_amdgcn_mfma_f32_16x16x4f32(at[s2], bv[s2], c, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = 4 * kg + r, q = i / 3, m = 3 * U0 + i;
+            if (i < 15 && U0 + q < u_lim && m < M2) yb[2 * m + comp] = c[r];
+        }
+    };
+    auto tile = [&](int t, float4 (&pf)[5]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < 5; ++r) xw[HALO / 2 + r * 64 + lane] = pf[r];
+        __builtin_amdgcn_sched_barrier(0);
+        load_tile(pf, t + PFD);
+        wave_sync();
+        const int k = K0 + 64 * t - 4 + lane;
+        if (k >= K0 && k < K1) {
+            const float4 *w = xw + 5 * lane + 4;
+            pf2 a = {0.f, 0.f};
+#pragma unroll
+            for (int q = 0; q < 12; ++q) {
+                const float4 t4 = htap[q], x0 = w[2 * q], x1 = w[2 * q + 1];
+                a = pfma(t4.x, pf2{x0.x, x0.y}, a);
+                a = pfma(t4.y, pf2{x0.z, x0.w}, a);
+                a = pfma(t4.z, pf2{x1.x, x1.y}, a);
+                a = pfma(t4.w, pf2{x1.z, x1.w}, a);
+            }
+            lin[k - kbase] = make_float2(a.x, a.y);
+            if (wv > 0 && k - K0 < SEAM) seam[(wv - 1) * SEAM + k - K0] = make_float2(a.x, a.y);
+        }
+        wave_sync();
+        // halo for the next tile: image samples [0, 48) = this tile's [640, 688)
+        if (lane < HALO / 2) xw[lane] = xw[WT_IN4 + lane];
+        // triple u has its window once 10 u + 113 <= kav
+        const int kav = min(K0 + 64 * t + 59, K1 - 1);
+        const int u_rdy = kav >= 113 ? min((kav - 113) / 10 + 1, u_end) : 0;
+        if (u_rdy - u_done >= S2T) {
+            burst(u_done + S2T);
+            u_done += S2T;
+            // keep x240[10 u_done, kav] (<= 167 entries) at the buffer's front
+            const int from = 10 * u_done - kbase, cnt = kav + 1 - 10 * u_done;
+            float2 v[3];
+#pragma unroll
+            for (int e = 0; e < 3; ++e) v[e] = lane + 64 * e < cnt ? lin[from + lane + 64 * e] : make_float2(0.f, 0.f);
+            wave_sync();
+#pragma unroll
+            for (int e = 0; e < 3; ++e)
+                if (lane + 64 * e < cnt) lin[lane + 64 * e] = v[e];
+            kbase = 10 * u_done;
+        }
+        wave_sync();
+    };
+    __syncthreads();   // htap
+    static_assert(PFD == 2, "pa / pb below");
+    float4 pa[5], pb[5];
+    if (ntile > 0) {
+        load_tile(pa, 0);
+        load_tile(pb, 1);
+    }
+    int t = 0;
+    for (; t + 1 < ntile; t += 2) {
+        tile(t, pa);
+        tile(t + 1, pb);
+    }
+    if (t < ntile) tile(t, pa);
+    __syncthreads();   // every wave's seam and in-loop bursts
+    if (active && u_done < u_end) {
+        if (has_right) {   // x240[K1, K1 + SEAM) from wave wv + 1 (K1 - kbase <= 510)
+            for (int i = lane; i < SEAM; i += 64) lin[K1 - kbase + i] = seam[wv * SEAM + i];
+            wave_sync();
+        }
+        for (; u_done < u_end; u_done += S2T) burst(u_end);   // <= 51 triples: two bursts at most
+    }
+    __syncthreads();
+    if constexpr (FUSE) {
+        timing_tail(reinterpret_cast<const float2 *>(yb), reinterpret_cast<float2 *>(img), to, M2, ch, tid, tro);
+    } else {
+        float2 *yp = y + (size_t)ch * M2;
+        for (int i = tid; i < M2; i += 256) yp[i] = make_float2(yb[2 * i], yb[2 * i + 1]);
     }
 }
 
@@ -1076,7 +1261,13 @@ static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void 
     PROF(ctx, fused ? "etsi_demod" : "etsi_chanfilt");
     const TimingOut to = fused ? *fused : TimingOut{};
     const dim3 g((unsigned)C), b(256);
-    if (fmt == TETRA_SC16 && fused)
+    if (fmt == TETRA_CF32 && M2 <= YLDS && fused)
+        hipLaunchKernelGGL((k_chanfilt_w<true>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1, (int)M2,
+                           coef, coef + 64, y, to);
+    else if (fmt == TETRA_CF32 && M2 <= YLDS)
+        hipLaunchKernelGGL((k_chanfilt_w<false>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1, (int)M2,
+                           coef, coef + 64, y, to);
+    else if (fmt == TETRA_SC16 && fused)
         hipLaunchKernelGGL((k_chanfilt<uint2, true>), g, b, 0, ctx->stream, (const uint2 *)x, (long)N, (int)M1, (int)M2,
                            coef, coef + 64, y, to);
     else if (fmt == TETRA_SC16)
@@ -1188,7 +1379,7 @@ int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *i
     // fused: timing runs in the channel filter's workgroup on y in LDS (cf32: y never leaves LDS;
     // SC16: y round-trips through a C x M2 scratch and is re-staged into the freed image/ring)
     // (measured: cf32 with y through L2 at four workgroups per CU, as SC16 does, is 2.5 % slower)
-    const bool fuse = fmt == TETRA_SC16 ? M2 + sm <= CF_LDS2_SC16 : (M2 <= YLDS && sm <= 2 * XIN4);
+    const bool fuse = fmt == TETRA_SC16 ? M2 + sm <= CF_LDS2_SC16 : (M2 <= YLDS && sm <= 2 * 4 * WIMG4);
     if (fuse) {
         float2 *ys = nullptr;
         if (fmt == TETRA_SC16 && !(ys = (float2 *)ws(ctx, S_W3, C * (size_t)M2 * 8))) return st.finish();
