@@ -13,7 +13,8 @@ def main():
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for d in dirs:
         for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
-            name = r["Kernel_Name"].split("(")[0].replace("void ", "").split("::")[-1]
+            name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+            name = name.split("(")[0].split("<")[0]
             acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
     res = {}
     for k, cs in acc.items():
