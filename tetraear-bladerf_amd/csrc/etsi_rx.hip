@@ -293,8 +293,7 @@ template <> struct CfCfg<uint2> { static constexpr int s2_every = 8, lr = 2312; 
 constexpr int TPP = 107;        // RRC taps per polyphase branch (Lp = 321 = 3 x 107)
 constexpr int PFD = 2;          // input tiles in flight per workgroup (register prefetch depth, pa/pb;
                                 // 3 and 4 measured no faster)
-constexpr int YLDS = 4096;      // cf32: stage-2 outputs held in LDS before a flush (a 131072-sample
-                                // chunk has 3932)
+constexpr int YLDS = 3904;      // cf32: stage-2 outputs held in LDS (a 131072-sample chunk has 3899)
 // Stage 2 on the matrix cores (v_mfma_f32_16x16x4_f32: bit-for-bit a k-ordered fmaf chain).  One
 // MFMA tile: 16 columns = 8 segments x (re, im), each segment S2Q consecutive triples; row
 // i = 3q + c of a column is output 3(U + q) + c; A[i][s] = tap of x240[10U + s] for that output
@@ -601,11 +600,14 @@ __global__ __launch_bounds__(256, cf_waves<In>()) void k_chanfilt(const In *__re
 // k_chanfilt.  Every output is the same fma chain as in k_chanfilt (bit-identical to the oracle).
 constexpr int WT_IN4 = 320;                 // sample pairs per wave tile (640 samples)
 constexpr int WIMG4 = HALO / 2 + WT_IN4;    // wave image (float4): 48-sample halo + the tile
-constexpr int WLR = 664;                    // wave stage-1 buffer (float2): the windows of <= 51 triples
+constexpr int WLR = 568;                    // wave stage-1 buffer (float2): < 567 entries in the stream,
+                                            // <= 265 in the channel's last (seam) burst
 constexpr int SEAM = 112;                   // >= the 104 outputs a left neighbour's last triples need
 constexpr int UMIN = 16;                    // triples per wave at least (10 UMIN >= SEAM)
 constexpr int WSMEM4 = 14 + 4 * WIMG4 + (4 * WLR + 3 * SEAM + YLDS) / 2;   // float4
-static_assert(WSMEM4 * 16 <= 80 * 1024, "per-wave demod LDS: two workgroups per CU");
+// two workgroups per CU with >= 9.5 KB of the CU's LDS left for the lower MAC's kernels
+// (k_etsi_viterbi 7 KB, k_etsi_sync 2.4 KB), which the bench's pipeline runs beside the next demod
+static_assert(2 * WSMEM4 * 16 + 7 * 1024 + 2560 <= 160 * 1024, "per-wave demod LDS");
 static_assert(sizeof(TrackOut) <= 32 && (4 * WLR + 3 * SEAM) % 2 == 0, "per-wave demod LDS carving");
 
 // cross-lane LDS hand-off inside one wave: a wave's LDS instructions execute in order, so only the
@@ -719,9 +721,12 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_w(const float4 *__restrict_
         // triple u has its window once 10 u + 113 <= kav
         const int kav = min(K0 + 64 * t + 59, K1 - 1);
         const int u_rdy = kav >= 113 ? min((kav - 113) / 10 + 1, u_end) : 0;
-        if (u_rdy - u_done >= S2T) {
-            burst(u_done + S2T);
-            u_done += S2T;
+        // bursts of 40; at the wave's last tile also the rest of the ready triples, so that only
+        // the seam's (<= 12) remain for after the barrier
+        while (u_rdy - u_done >= S2T || (t == ntile - 1 && u_rdy > u_done)) {
+            const int ul = min(u_done + S2T, u_rdy);
+            burst(ul);
+            u_done = ul;
             // keep x240[10 u_done, kav] (<= 167 entries) at the buffer's front
             const int from = 10 * u_done - kbase, cnt = kav + 1 - 10 * u_done;
             float2 v[3];
@@ -750,11 +755,11 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_w(const float4 *__restrict_
     if (t < ntile) tile(t, pa);
     __syncthreads();   // every wave's seam and in-loop bursts
     if (active && u_done < u_end) {
-        if (has_right) {   // x240[K1, K1 + SEAM) from wave wv + 1 (K1 - kbase <= 510)
+        if (has_right) {   // x240[K1, K1 + SEAM) from wave wv + 1 (K1 - kbase <= 120)
             for (int i = lane; i < SEAM; i += 64) lin[K1 - kbase + i] = seam[wv * SEAM + i];
             wave_sync();
         }
-        for (; u_done < u_end; u_done += S2T) burst(u_end);   // <= 51 triples: two bursts at most
+        burst(u_end);   // <= 12 triples
     }
     __syncthreads();
     if constexpr (FUSE) {
