@@ -304,14 +304,15 @@ class BenchStep:
         self.ev_back[i].record(self.s_back)
 
     def dominant(self):
-        # fused k_chanfilt<.., true>: reads 8 B (cf32) or 4 B (SC16) per input sample; writes per
-        # symbol (0.0075 per input sample) 8 B cf32 symbol + 2 B soft bits + 1 B hard dibit.
-        # split k_chanfilt<.., false>: the same reads, writes y (8 B per 72 kHz sample = 0.24 B per
-        # input sample)
+        # fused demod: reads 8 B (cf32) or 4 B (SC16) per input sample; writes per symbol (0.0075 per
+        # input sample) 8 B cf32 symbol + 2 B soft bits + 1 B hard dibit.  split: the same reads,
+        # writes y (8 B per 72 kHz sample = 0.24 B per input sample).  Kernel: the per-wave
+        # k_chanfilt_w for cf32 chunks of up to YLDS = 3904 outputs (etsi_rx.hip), else k_chanfilt.
         rd = 4.0 if self.fmt == _hip.TETRA_SC16 else 8.0
+        sym = "k_chanfilt_w" if self.fmt == _hip.TETRA_CF32 and self.M2 <= 3904 else "k_chanfilt"
         if self.demod_mode == "split":
-            return ("etsi_chanfilt", rd + 8.0 * self.M2 / self.N, "k_chanfilt")
-        return ("etsi_demod", rd + 11.0 * 18000.0 / self.fs, "k_chanfilt")
+            return ("etsi_chanfilt", rd + 8.0 * self.M2 / self.N, sym)
+        return ("etsi_demod", rd + 11.0 * 18000.0 / self.fs, sym)
 
     def floor_args(self):
         """bench.py's read floor over this batch: one row per channel, the fused cf32 kernel's
