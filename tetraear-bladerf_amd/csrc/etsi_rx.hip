@@ -658,9 +658,17 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_w(const float4 *__restrict_
     // image float4 4 + 5 l + [0, 24); loads past the wave's last needed pair re-read that pair
     const float4 *xp = iq + (size_t)ch * (N / 2) + 5L * K0;
     const int qlast = active ? (int)(min(5L * (K1 - 1) + 23, N / 2 - 1) - 5L * K0) : 0;
+    // a buffer resource over the wave's pairs [0, qlast]: loads past it return 0 without touching
+    // memory (those samples only feed outputs >= K1, never computed), and the offsets are 32-bit
+    // (lane part + instruction offset + the tile's scalar offset), so a load costs no address VALU
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float4 *>(xp), 0,
+                                                                        (qlast + 1) * 16, 0x00020000);
     auto load_tile = [&](float4 (&pf)[5], int t) __attribute__((always_inline)) {
 #pragma unroll
-        for (int r = 0; r < 5; ++r) pf[r] = ld_nt(xp + min(t * WT_IN4 + r * 64 + lane, qlast));
+        for (int r = 0; r < 5; ++r) {
+            const nt_f4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, (r * 64 + lane) * 16, t * WT_IN4 * 16, 2 /* nt */);
+            pf[r] = make_float4(v.x, v.y, v.z, v.w);
+        }
     };
     int kbase = K0;      // x240 index of lin[0]
     int u_done = u_beg;  // triples [u_beg, u_done) are in yb
