@@ -4,14 +4,16 @@
 // north_star asks for, restating oracle/etsi_oracle.c operation for operation (explicit fmaf,
 // emulated 64-lane reductions, a libm-free atan2), so GPU and oracle results are bit-identical.
 //
-//   k_chanfilt   stage 1: 48-tap decimate-by-10 FIR (2.4 MSps -> 240 kHz), stage 2: polyphase RRC
-//                (alpha 0.35, 321 taps at 720 kHz) resampler x3/10 -> 72 kHz = 4 samples/symbol.
-//                One workgroup streams one channel: 2560-sample input tiles (float4 / SC16 uint2
-//                loads, register prefetch two tiles deep), stage 1 on packed fp32 FMA, stage-1
-//                outputs in a linear LDS buffer, stage 2 every 8 tiles on the matrix cores
-//                (v_mfma_f32_16x16x4_f32, exact f32: banded tap matrix x 16 columns of 5 output
-//                triples), y held in LDS (cf32) or round-tripped through L2 (SC16), then the timing
-//                stage on wave 0 (fused).  HBM-bound: 8 B read per input sample (cf32), 0.013 B written.
+//   k_chanfilt_w stage 1: 48-tap decimate-by-10 FIR (2.4 MSps -> 240 kHz), stage 2: polyphase RRC
+//                (alpha 0.35, 321 taps at 720 kHz) resampler x3/10 -> 72 kHz = 4 samples/symbol,
+//                then the timing stage (fused).  cf32 chunks up to YLDS outputs: the workgroup's
+//                four waves stream the channel's quarters independently (640-sample wave tiles,
+//                register prefetch two tiles deep, private LDS image and stage-1 buffer, stage 2 in
+//                one-MFMA-tile bursts on v_mfma_f32_16x16x4_f32 -- exact f32: banded tap matrix x 16
+//                columns of 5 output triples), y held in LDS.  8 B read per input sample.
+//   k_chanfilt   the same filter with workgroup-wide 2560-sample tiles (barrier per tile, stage 2
+//                every 8 tiles): the SC16 form (4 B/sample in, y round-tripped through L2, four
+//                workgroups per CU) and chunks longer than YLDS outputs.
 //   k_timing     one wave per channel: Oerder-Meyr timing phase (wave reduction), block Gardner
 //                tracking (64 symbols per block = one per lane; error summed by xor-butterfly),
 //                cubic interpolation, differential decision, 4th-power CFO estimate, int8 soft bits.
