@@ -315,10 +315,11 @@ class BenchStep:
         return ("etsi_demod", rd + 11.0 * 18000.0 / self.fs, sym)
 
     def floor_args(self):
-        """bench.py's read floor over this batch: one row per channel, the fused cf32 kernel's
-        72 KB of LDS (two workgroups per CU) or SC16's 39 KB (four)."""
+        """bench.py's read floor over this batch: one row per channel at the demod kernel's LDS
+        footprint -- k_chanfilt_w's 74,336 B (two workgroups per CU) or SC16 k_chanfilt's 39,568 B
+        (four)."""
         row = self.N * (4 if self.fmt == _hip.TETRA_SC16 else 8)
-        return _hip.ptr(self.iq), self.C, row, (39 if self.fmt == _hip.TETRA_SC16 else 72) * 1024
+        return _hip.ptr(self.iq), self.C, row, 39568 if self.fmt == _hip.TETRA_SC16 else 74336
 
     def quality(self):
         """Decoded-block statistics of the last step (device results, checked on the host)."""
