@@ -212,10 +212,10 @@ def test_sc16_ingest_matches_cf32(synth_small):
 
 
 @pytest.mark.parametrize("fmt", ["cf32", "sc16"])
-@pytest.mark.parametrize("N", [262144, 131072, 70001, 40000, 23408, 20000, 9001, 3000])
+@pytest.mark.parametrize("N", [262144, 134408, 131072, 70001, 40000, 23408, 20000, 9001, 3000])
 def test_demod_lengths_vs_oracle(N, fmt):
     """Chunk lengths around the kernels' structure: longer than the fused path's LDS output buffer
-    (component path), the 128 Ki design point (fused; SC16 re-stages y into the freed image and
+    (component path; 134408 gives 4000 outputs, just past YLDS = 3904), the 128 Ki design point (fused; SC16 re-stages y into the freed image and
     stage-1 buffer), mid lengths on the per-wave cf32 filter (odd wave-tile counts, quarters that
     end mid-tile), short (the per-wave filter on fewer than four waves), odd (trimmed to even like
     demod_batch does), and barely long enough -- for both input formats (SC16 against the oracle on
