@@ -796,6 +796,69 @@ __device__ T pairwise_mean(F v, long n) {
     return ret / (T)n;
 }
 
+// The same sum as pairwise_mean's, with the tree unrolled at compile time (no stack in scratch, and
+// the leaves' loads 16 deep): at most D splits, then leaves of <= 128.  A part after d splits is at
+// most n / 2^d + 14 long (each split rounds down to a multiple of 8), so with D = 5 every leaf is
+// <= 128 for n <= 3584; callers take pairwise_mean beyond that.  Element i is |y[ph + i sps]|^2; the
+// leaf is one out-of-line function (32 inlined copies of its unrolled |z| code would be ~1 MB).
+template <typename T>
+struct PhasePower {
+    const T *yp;
+    size_t sy;
+    long ph;
+    int sps;
+    __device__ __forceinline__ T operator()(long i) const {
+        const size_t o = (size_t)(ph + i * sps) * sy;
+        const T a = np_cabs(yp[o], yp[o + 1]);
+        return a * a;
+    }
+};
+template <typename T>
+__device__ __noinline__ T pw_leaf(PhasePower<T> v, long s, long m) {
+    if (m < 8) {
+        T r = 0;
+        for (long i = 0; i < m; ++i) r += v(s + i);
+        return r;
+    }
+    T r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r[k] = v(s + k);
+    long i = 8;
+    const long mm = m - (m % 8);
+    for (; i + 8 < mm; i += 16) {   // two groups of 8 loads in flight, summed in order
+        T a[8], b[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            a[k] = v(s + i + k);
+            b[k] = v(s + i + 8 + k);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] += a[k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] += b[k];
+    }
+    for (; i < mm; i += 8) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] += v(s + i + k);
+    }
+    T res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < m; ++i) res += v(s + i);
+    return res;
+}
+template <int D, typename T>
+__device__ __forceinline__ T pw_sum(const PhasePower<T> &v, long s, long n) {
+    if constexpr (D == 0) {
+        return pw_leaf<T>(v, s, n);   // n <= 128 here whenever the root's n <= 3584 (see above)
+    } else {
+        if (n <= 128) return pw_leaf<T>(v, s, n);
+        long n2 = n / 2;
+        n2 -= n2 % 8;
+        const T l = pw_sum<D - 1, T>(v, s, n2);
+        const T r = pw_sum<D - 1, T>(v, s + n2, n - n2);
+        return l + r;
+    }
+}
+
 // 16 lanes per channel: lane k tries phase k*step (processor.py:196-210), then the group gathers
 // the chosen phase into sym[ch][0..ns).
 template <typename T>
@@ -813,12 +876,8 @@ __global__ __launch_bounds__(256) void k_extract(const T *__restrict__ y, Lay ly
     T power = (T)-2;
     long ns = (ok && k < nph) ? (M - ph) / sps : 0;
     if (ns > 0) {
-        auto v = [&](long i) -> T {
-            const size_t o = (size_t)(ph + i * sps) * sy;
-            const T a = np_cabs(yp[o], yp[o + 1]);
-            return a * a;
-        };
-        power = pairwise_mean<T>(v, ns);
+        const PhasePower<T> v{yp, sy, (long)ph, sps};
+        power = ns <= 3584 ? pw_sum<5, T>(v, 0, ns) / (T)ns : pairwise_mean<T>(v, ns);
     }
     T best = (T)-1;
     int bph = 0;
