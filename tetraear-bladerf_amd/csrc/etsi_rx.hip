@@ -597,9 +597,10 @@ __global__ __launch_bounds__(256, cf_waves<In>()) void k_chanfilt(const In *__re
 // channel ends, and a burst stalls one wave's quarter of the loads in flight instead of the whole
 // workgroup's (k_chanfilt: every wave waits at the tile's barriers while three of them run the
 // burst's MFMA pairs).  Wave w's last triples need stage-1 outputs up to K_w+1 + 103, the first
-// ones of wave w + 1, which that wave also copies into a seam buffer; after the one barrier at the
-// channel's end each wave appends its seam and runs its last bursts, then the timing tail as in
-// k_chanfilt.  Every output is the same fma chain as in k_chanfilt (bit-identical to the oracle).
+// ones of wave w + 1, which that wave also copies into a seam buffer.  A wave bursts every ready
+// triple at its last tile, so after the one barrier at the channel's end it appends its seam and
+// runs one burst of the <= 12 triples left, then the timing tail as in k_chanfilt.  Every output is
+// the same fma chain as in k_chanfilt (bit-identical to the oracle).
 constexpr int WT_IN4 = 320;                 // sample pairs per wave tile (640 samples)
 constexpr int WIMG4 = HALO / 2 + WT_IN4;    // wave image (float4): 48-sample halo + the tile
 constexpr int WLR = 568;                    // wave stage-1 buffer (float2): < 567 entries in the stream,
