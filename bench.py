@@ -232,11 +232,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RCCL ("nccl") on a node with one GPU per rank.  TETRA_BENCH_DIST=gloo rehearses the N>1
+    # path with several ranks sharing fewer GPUs (rank -> LOCAL_RANK mod device count; the timing
+    # all_reduce then runs on a host tensor).
+    backend = os.environ.get("TETRA_BENCH_DIST", "nccl")
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    os.environ["TETRA_HIP_DEVICE"] = str(local)
+        dist.init_process_group(backend, init_method="env://")
+    gpu = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    os.environ["TETRA_HIP_DEVICE"] = str(gpu)
     c = _hip.ctx()
     stream = torch.cuda.current_stream(dev)
     c.check(c.lib.tetra_set_stream(c.handle, ctypes.c_void_p(stream.cuda_stream)), "set_stream")
@@ -286,7 +291,8 @@ def main():
     prof = read_profile(ctxs)
     for x in ctxs:
         x.check(x.lib.tetra_profile(x.handle, 0), "profile")
-    elapsed = max_over_ranks(elapsed, dev)   # slowest rank (RCCL all_reduce MAX); identity at N=1
+    # slowest rank (RCCL all_reduce MAX); identity at N=1
+    elapsed = max_over_ranks(elapsed, dev if backend == "nccl" else None)
     ms_step = elapsed / a.steps * 1e3
     value = aggregate_msps(C * N, world, a.steps, elapsed)
 
