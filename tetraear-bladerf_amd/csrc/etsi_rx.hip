@@ -149,6 +149,8 @@ struct TrackOut {
     float rr, ri, sc, base, delta;
 };
 
+constexpr int CPOL_SC1 = 16;   // gfx940+ cache-policy bits: sc0 1, nt 2, sc1 16 (copy_out)
+
 __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float gain, float soft_scale, float2 *sp,
                                                  float2 *dp, int smax, int lane) {
     TrackOut o{0, 1.0f, 0.0f, 0.0f, 0.0f, 0.0f};
@@ -344,15 +346,58 @@ struct TimingOut {
     int smax;
 };
 
+// LDS -> global copy of n bytes by the workgroup's 256 threads, as device-scope (sc1) stores
+// through a buffer resource over the row: 16-B stores where the row is 16-B aligned (the LDS image
+// is), 8-B stores where it is 8-B aligned, byte stores for the rest.  sc1 writes the lines through
+// to memory as they are stored; with the default policy the dirty lines sit in L2 and are evicted
+// one by one into the channel filter's read stream (same box: demod 1.500 -> 1.423-1.437 ms; nt
+// stores no better than the default; sc0 sc1 / nt sc1 / sc0 sc1 nt 1.43-1.45).
+__device__ __forceinline__ void copy_out(uint8_t *g, const uint8_t *l, int n, int tid) {
+    if (n <= 0) return;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(g, 0, n, 0x00020000);   // n: the range check
+    const uintptr_t al = reinterpret_cast<uintptr_t>(g);
+    int done = 0;
+    if ((al & 15) == 0) {
+        typedef unsigned u4v __attribute__((ext_vector_type(4)));
+        const int n16 = n >> 4;
+        for (int i = tid; i < n16; i += 256) {
+            const uint4 v = reinterpret_cast<const uint4 *>(l)[i];
+            __builtin_amdgcn_raw_buffer_store_b128(u4v{v.x, v.y, v.z, v.w}, r, 16 * i, 0, CPOL_SC1);
+        }
+        done = 16 * n16;
+    } else if ((al & 7) == 0) {
+        typedef unsigned u2v __attribute__((ext_vector_type(2)));
+        const int n8 = n >> 3;
+        for (int i = tid; i < n8; i += 256) {
+            const uint2 v = reinterpret_cast<const uint2 *>(l)[i];
+            __builtin_amdgcn_raw_buffer_store_b64(u2v{v.x, v.y}, r, 8 * i, 0, CPOL_SC1);
+        }
+        done = 8 * n8;
+    }
+    for (int i = done + tid; i < n; i += 256) __builtin_amdgcn_raw_buffer_store_b8(l[i], r, i, 0, CPOL_SC1);
+}
+
+// Output staging of the fused demod's tail (stage != nullptr): the symbols, soft bits and hard
+// dibits of the channel collect in LDS and leave in wide stores once the channel is decided --
+// per-block float2 stores from the tracking loop and byte stores from the decision pass cost
+// 0.155 ms per 8192-channel batch (same box: 1.505 -> 1.350 ms with the stores left out).
+struct TailStage {
+    float2 *sym;     // [sm] (LDS)
+    int8_t *sb;      // [2 sm]
+    uint8_t *hard;   // [sm]
+};
+
 // The fused demod's timing stage for channel ch on y in LDS (ly), after the workgroup's last barrier:
 // the tracking is the serial tail (wave 0, prioritised on its SIMD); the decision pass after it is
 // shared by all four waves (the rotation and scale go through LDS, *tro).
 __device__ __forceinline__ void timing_tail(const float2 *ly, float2 *scr, const TimingOut &to, int M2, int ch,
-                                            int tid, TrackOut *tro) {
+                                            int tid, TrackOut *tro, const TailStage *stage = nullptr) {
     const size_t so = (size_t)ch * to.smax;
     if (tid < 64) {
         __builtin_amdgcn_s_setprio(3);
-        const TrackOut o = timing_track(ly, M2, to.gain, to.soft_scale, to.sym + so, scr, to.smax, tid);
+        // S <= M2 / 4 + 1 < the staging size either way: the bound only guards the LDS buffer
+        const TrackOut o = timing_track(ly, M2, to.gain, to.soft_scale, stage ? stage->sym : to.sym + so, scr,
+                                        stage ? min(to.smax, M2 / 4 + 2) : to.smax, tid);
         if (tid == 0) {
             *tro = o;
             to.nsym[ch] = o.S;
@@ -361,7 +406,17 @@ __device__ __forceinline__ void timing_tail(const float2 *ly, float2 *scr, const
     }
     __syncthreads();
     const TrackOut o = *tro;
-    timing_decide(o, scr, to.softbits + 2 * so, to.hard + so, tid >> 6, 4, tid & 63);
+    if (!stage) {
+        timing_decide(o, scr, to.softbits + 2 * so, to.hard + so, tid >> 6, 4, tid & 63);
+        return;
+    }
+    timing_decide(o, scr, stage->sb, stage->hard, tid >> 6, 4, tid & 63);
+    __syncthreads();
+    const int nd = o.S > 1 ? o.S - 1 : 0;
+    copy_out(reinterpret_cast<uint8_t *>(to.sym + so), reinterpret_cast<const uint8_t *>(stage->sym), 8 * o.S, tid);
+    copy_out(reinterpret_cast<uint8_t *>(to.softbits + 2 * so), reinterpret_cast<const uint8_t *>(stage->sb), 2 * nd,
+             tid);
+    copy_out(to.hard + so, stage->hard, nd, tid);
 }
 
 // SC16 is held to 128 VGPRs: four workgroups per CU (its LDS allows four; at 158-161 VGPRs it ran at
@@ -612,6 +667,9 @@ constexpr int WSMEM4 = 14 + 4 * WIMG4 + (4 * WLR + 3 * SEAM + YLDS) / 2;   // fl
 // (k_etsi_viterbi 7 KB, k_etsi_sync 2.4 KB), which the bench's pipeline runs beside the next demod
 static_assert(2 * WSMEM4 * 16 + 7 * 1024 + 2560 <= 160 * 1024, "per-wave demod LDS");
 static_assert(sizeof(TrackOut) <= 32 && (4 * WLR + 3 * SEAM) % 2 == 0, "per-wave demod LDS carving");
+// fused tail staging: sm symbols in the stage-1 buffers; 8 sm (d_j) + 2 sm + sm bytes in the images
+constexpr int WTAIL_SM = YLDS / 4 + 2;
+static_assert(WTAIL_SM * 8 <= 4 * WLR * 8 && 11 * WTAIL_SM + 32 <= 4 * WIMG4 * 16, "tail staging LDS");
 
 // cross-lane LDS hand-off inside one wave: a wave's LDS instructions execute in order, so only the
 // compiler has to be kept from moving accesses across this point (no s_waitcnt, no s_barrier)
@@ -774,10 +832,14 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_w(const float4 *__restrict_
     }
     __syncthreads();
     if constexpr (FUSE) {
-        timing_tail(reinterpret_cast<const float2 *>(yb), reinterpret_cast<float2 *>(img), to, M2, ch, tid, tro);
+        // the tail's LDS: d_j scratch, soft bits and hard dibits in the freed wave images, the
+        // symbols in the freed stage-1 buffers (the launch guarantees sm <= WTAIL_SM)
+        const int sm = M2 / 4 + 2;
+        int8_t *ib = reinterpret_cast<int8_t *>(img);
+        const TailStage st{lin_all, ib + ((8 * sm + 15) & ~15), reinterpret_cast<uint8_t *>(ib + ((10 * sm + 31) & ~15))};
+        timing_tail(reinterpret_cast<const float2 *>(yb), reinterpret_cast<float2 *>(img), to, M2, ch, tid, tro, &st);
     } else {
-        float2 *yp = y + (size_t)ch * M2;
-        for (int i = tid; i < M2; i += 256) yp[i] = make_float2(yb[2 * i], yb[2 * i + 1]);
+        copy_out(reinterpret_cast<uint8_t *>(y + (size_t)ch * M2), reinterpret_cast<const uint8_t *>(yb), 8 * M2, tid);
     }
 }
 
