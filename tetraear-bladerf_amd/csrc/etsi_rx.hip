@@ -582,8 +582,8 @@ __global__ __launch_bounds__(256, cf_waves<In>()) void k_chanfilt(const In *__re
             if constexpr (!YL) {
                 if (nt > 0) {   // coalesced store of this burst's outputs y[3 u_done, mend)
                     __syncthreads();
-                    const float2 *xs = reinterpret_cast<const float2 *>(ys);
-                    for (int i = tid; i < mend - yo; i += 256) yp[yo + i] = xs[i];
+                    // sc1 (copy_out): 1.11 -> 1.09 ms per SC16 batch, same box
+                    copy_out(reinterpret_cast<uint8_t *>(yp + yo), reinterpret_cast<const uint8_t *>(ys), 8 * (mend - yo), tid);
                 }
             }
             if (u_hi + 1 > u_done) u_done = u_hi + 1;
