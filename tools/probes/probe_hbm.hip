@@ -49,6 +49,39 @@ __global__ __launch_bounds__(256) void k_ring(const float4 *__restrict__ x, long
     if (acc == 0x9E3779B9u) out[blockIdx.x] = acc;
 }
 
+// register ring through a buffer resource with cache-policy bits AUX (gfx940+: sc0 1, nt 2, sc1 16)
+template <int AUX, int DEPTH>
+__global__ __launch_bounds__(256) void k_ringb(const float4 *__restrict__ x, long row4, uint32_t *out, int rows) {
+    extern __shared__ float4 pad_lds[];
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    uint32_t acc = 0;
+    for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float4 *>(x + (size_t)row * row4), 0,
+                                                                           (int)(row4 * 16), 0x00020000);
+        const long ng = (row4 + 1279) / 1280;
+        f4v v[DEPTH][5];
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+            for (int q = 0; q < 5; ++q) v[d][q] = __builtin_amdgcn_raw_buffer_load_b128(r, (q * 256 + threadIdx.x) * 16, d * 1280 * 16, AUX);
+        for (long g = 0; g < ng; g += DEPTH) {
+#pragma unroll
+            for (int d = 0; d < DEPTH; ++d) {
+#pragma unroll
+                for (int q = 0; q < 5; ++q)
+                    acc ^= __float_as_uint(v[d][q].x) ^ __float_as_uint(v[d][q].y) ^ __float_as_uint(v[d][q].z) ^
+                           __float_as_uint(v[d][q].w);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int q = 0; q < 5; ++q)
+                    v[d][q] = __builtin_amdgcn_raw_buffer_load_b128(r, (q * 256 + threadIdx.x) * 16, (int)((g + DEPTH + d) * 1280 * 16), AUX);
+            }
+        }
+    }
+    if (acc == 0x9E3779B9u) pad_lds[threadIdx.x] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (acc == 0x9E3779B9u) out[blockIdx.x] = acc;
+}
+
 // LDS-DMA: each wave streams its quarter of every 20 KB tile into its own LDS ring, keeping at most
 // INFL wave-instructions (1 KiB each) in flight
 template <int AUX, int INFL>
@@ -87,6 +120,16 @@ int main() {
     CK(hipEventCreate(&b));
     struct V { const char *name; KFn f; int grid; int lds; };
     std::vector<V> vs = {
+        {"ringb d2 aux0 (default) 2wg", k_ringb<0, 2>, rows, 72 * 1024},
+        {"ringb d2 aux2 (nt) 2wg", k_ringb<2, 2>, rows, 72 * 1024},
+        {"ringb d2 aux1 (sc0) 2wg", k_ringb<1, 2>, rows, 72 * 1024},
+        {"ringb d2 aux3 (sc0 nt) 2wg", k_ringb<3, 2>, rows, 72 * 1024},
+        {"ringb d2 aux16 (sc1) 2wg", k_ringb<16, 2>, rows, 72 * 1024},
+        {"ringb d2 aux17 (sc0 sc1) 2wg", k_ringb<17, 2>, rows, 72 * 1024},
+        {"ringb d2 aux18 (sc1 nt) 2wg", k_ringb<18, 2>, rows, 72 * 1024},
+        {"ringb d2 aux19 (sc0 sc1 nt) 2wg", k_ringb<19, 2>, rows, 72 * 1024},
+        {"ringb d3 aux2 (nt) 2wg", k_ringb<2, 3>, rows, 72 * 1024},
+        {"ringb d3 aux19 (sc0 sc1 nt) 2wg", k_ringb<19, 3>, rows, 72 * 1024},
         {"ring d1 plain 2wg/cu", k_ring<false, 1>, rows, 72 * 1024},
         {"ring d2 plain 2wg/cu", k_ring<false, 2>, rows, 72 * 1024},
         {"ring d2 nt    2wg/cu", k_ring<true, 2>, rows, 72 * 1024},
