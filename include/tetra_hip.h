@@ -176,6 +176,31 @@ int tetra_crc16(tetra_ctx *ctx, const uint8_t *bits, size_t F, size_t L, int rev
 /* _check_crc over F rows of L bits: ok [F]. */
 int tetra_check_crc(tetra_ctx *ctx, const uint8_t *bits, size_t F, size_t L, uint8_t *ok);
 
+/* MAC PDU header extraction of TetraProtocolParser.parse_mac_pdu (protocol.py:349-596; SURVEY.md
+ * §8f rank 4) over F frames of data bits (0/1), one row of `stride` bytes each, nbits[f] valid.
+ * Stateless per frame: the fragment buffer, the MCC/MNC/colour-code state and the statistics are
+ * applied in order by the host (tetraear.core.protocol.parse_mac_pdu_batch).
+ *   fields [F][TETRA_MAC_FIELDS] (below); data [F][data_stride] = BitArray(data bits).tobytes()
+ *   (MSB first, last byte zero-padded), data_stride >= (stride + 7) / 8. */
+enum {
+    TETRA_MAC_STATUS = 0,   /* 0 PDU; 1 None, no state touched (len < 8, truncated address/length,
+                               length check protocol.py:433/525, short SYSINFO); 2 None after the
+                               SYSINFO state write (MCC outside 200..799 or MNC > 999, :489-494) */
+    TETRA_MAC_PTYPE,        /* PDUType value: 0 RESOURCE, 1 FRAG, 2 END (header 3), 3 BROADCAST (header 2) */
+    TETRA_MAC_MODE,         /* (bits[2] << 1) | bits[3] (:389) */
+    TETRA_MAC_FILL,         /* bits[4] (RESOURCE, FRAG, END), else 0 */
+    TETRA_MAC_ADDR,         /* 24-bit address (RESOURCE), else -1 */
+    TETRA_MAC_LENGTH,       /* 6-bit length indicator (RESOURCE, END), else 0 */
+    TETRA_MAC_DATA_BITS,    /* number of data bits packed into data[f] */
+    TETRA_MAC_SYSINFO,      /* 1 if the SYSINFO MCC/MNC/colour code below were read (:482-485) */
+    TETRA_MAC_MCC,
+    TETRA_MAC_MNC,
+    TETRA_MAC_CC,
+    TETRA_MAC_FIELDS = 12
+};
+int tetra_mac_headers(tetra_ctx *ctx, const uint8_t *bits, const int32_t *nbits, size_t F, size_t stride,
+                      int32_t *fields, uint8_t *data, size_t data_stride);
+
 /* =====================================================================================
  * ETSI EN 300 392-2 receive chain (north star; no reference counterpart)
  * ===================================================================================== */

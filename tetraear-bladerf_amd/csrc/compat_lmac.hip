@@ -329,9 +329,111 @@ __global__ void k_check_crc(const uint8_t *__restrict__ bits, int F, long L, uin
     out[f] = check_crc([&](long i) -> uint32_t { return b[i] & 1u; }, L);
 }
 
+// parse_mac_pdu's per-frame part (protocol.py:349-596): one wave per frame; lane j packs data byte
+// j (MSB first, zero-padded past the data bits), lane 0 reads the header fields.  The stateful part
+// (fragment buffer, SYSINFO state, statistics) is the host's, in frame order.
+__global__ __launch_bounds__(64) void k_mac_headers(const uint8_t *__restrict__ bits, const int32_t *__restrict__ nbits,
+                                                    int F, long stride, int32_t *__restrict__ fields,
+                                                    uint8_t *__restrict__ data, long dstride) {
+    const int f = blockIdx.x, lane = threadIdx.x;
+    if (f >= F) return;
+    const uint8_t *b = bits + (size_t)f * stride;
+    const long n = nbits[f];
+    auto uint_at = [&](long p, int w) {   // int(''.join(str(x) for x in bits[p:p+w]), 2)
+        int v = 0;
+        for (int i = 0; i < w; ++i) v = (v << 1) | b[p + i];
+        return v;
+    };
+    // header (every lane computes it: the data range below depends on it)
+    int status = 1, ptype = 0, mode = 0, fill = 0, addr = -1, length = 0, sys = 0, mcc = 0, mnc = 0, cc = 0;
+    long dpos = 0, dbits = 0;
+    if (n >= 8) {
+        const int pti = (b[0] << 1) | b[1];
+        ptype = pti == 0 ? 0 : pti == 1 ? 1 : pti == 2 ? 3 : 2;
+        mode = (b[2] << 1) | b[3];
+        status = 0;
+        if (ptype == 0 || ptype == 2) {            // RESOURCE (:399-449) / END (:506-544)
+            fill = b[4];
+            long pos = 5;
+            if (ptype == 0) {
+                if (n < pos + 24) status = 1;
+                else { addr = uint_at(pos, 24); pos += 24; }
+            }
+            if (status == 0 && n < pos + 6) status = 1;
+            if (status == 0) {
+                length = uint_at(pos, 6);
+                pos += 6;
+                const long dl = 8L * length;
+                if (dl > n - pos + 16) status = 1;                          // :433-434, :525-526
+                else { dpos = pos; dbits = (dl > 0 && n >= pos + dl) ? dl : n - pos; }
+            }
+        } else if (ptype == 1) {                   // FRAG (:451-469)
+            fill = b[4];
+            dpos = 5;
+            dbits = n - 5;
+        } else {                                   // BROADCAST (:471-504)
+            if (mode == 0) {
+                if (n < 4 + 30) status = 1;
+                else {
+                    sys = 1;
+                    mcc = uint_at(4, 10);
+                    mnc = uint_at(14, 14);
+                    cc = uint_at(28, 6);
+                    if (mcc < 200 || mcc > 799 || mnc > 999) status = 2;
+                }
+            }
+            dpos = 4;
+            dbits = n - 4;
+        }
+    }
+    if (status != 0) dbits = 0;
+    uint8_t *o = data + (size_t)f * dstride;
+    for (long j = lane; 8 * j < dbits; j += 64) {
+        unsigned v = 0;
+        for (int k = 0; k < 8; ++k) v = (v << 1) | (8 * j + k < dbits ? (b[dpos + 8 * j + k] != 0) : 0u);
+        o[j] = (uint8_t)v;
+    }
+    if (lane == 0) {
+        int32_t *r = fields + (size_t)f * TETRA_MAC_FIELDS;
+        r[TETRA_MAC_STATUS] = status;
+        r[TETRA_MAC_PTYPE] = ptype;
+        r[TETRA_MAC_MODE] = mode;
+        r[TETRA_MAC_FILL] = fill;
+        r[TETRA_MAC_ADDR] = addr;
+        r[TETRA_MAC_LENGTH] = length;
+        r[TETRA_MAC_DATA_BITS] = (int32_t)dbits;
+        r[TETRA_MAC_SYSINFO] = sys;
+        r[TETRA_MAC_MCC] = mcc;
+        r[TETRA_MAC_MNC] = mnc;
+        r[TETRA_MAC_CC] = cc;
+        r[TETRA_MAC_CC + 1] = 0;
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+int tetra_mac_headers(tetra_ctx *ctx, const uint8_t *bits, const int32_t *nbits, size_t F, size_t stride,
+                      int32_t *fields, uint8_t *data, size_t data_stride) {
+    if (!ctx || (F && (!bits || !nbits || !fields || !data))) return TETRA_E_INVALID;
+    if (F == 0) return TETRA_OK;
+    if (data_stride < (stride + 7) / 8) return tetra_fail(ctx, TETRA_E_INVALID, "data_stride < (stride + 7) / 8");
+    std::vector<int32_t> nb(F);
+    HIP_TRY(ctx, hipMemcpy(nb.data(), nbits, F * 4, hipMemcpyDefault));
+    for (size_t f = 0; f < F; ++f)
+        if (nb[f] < 0 || (size_t)nb[f] > stride) return tetra_fail(ctx, TETRA_E_INVALID, "nbits[%zu] outside [0, stride]", f);
+    Staging st(ctx);
+    const uint8_t *b = (const uint8_t *)st.in(bits, F * stride);
+    const int32_t *n = (const int32_t *)st.in(nb.data(), F * 4);
+    int32_t *fo = (int32_t *)st.out(fields, F * TETRA_MAC_FIELDS * 4);
+    uint8_t *d = (uint8_t *)st.out(data, F * data_stride);
+    if (!b || !n || !fo || !d) return st.finish();
+    PROF(ctx, "mac_headers");
+    hipLaunchKernelGGL(k_mac_headers, dim3((unsigned)F), dim3(64), 0, ctx->stream, b, n, (int)F, (long)stride, fo, d,
+                       (long)data_stride);
+    return st.finish();
+}
 
 int tetra_lmac_compat(tetra_ctx *ctx, const int64_t *sym, const int32_t *nsym, size_t C, size_t stride,
                       const int8_t *k_of_max, int32_t *nsync, int32_t *rec, uint8_t *frame_bits, uint8_t *burst_bits) {

@@ -16,6 +16,9 @@ LIB_PATH = os.environ.get("TETRA_HIP_LIB", os.path.join(os.path.dirname(_PKG), "
 TETRA_CF32, TETRA_CF64, TETRA_SC16 = 0, 1, 2
 MAX_SYNC = 16
 F_POS, F_START, F_VALID, F_NBITS, F_NUMBER, F_BTYPE, F_CRC, F_HDR, F_FIELDS = range(9)
+(MAC_STATUS, MAC_PTYPE, MAC_MODE, MAC_FILL, MAC_ADDR, MAC_LENGTH, MAC_DATA_BITS, MAC_SYSINFO, MAC_MCC, MAC_MNC,
+ MAC_CC) = range(11)
+MAC_FIELDS = 12
 
 
 class TetraHipError(RuntimeError):
@@ -93,6 +96,7 @@ def _bind(L):
         "tetra_parse_bursts": (_i32, [_vp, _vp, _sz, _vp, _vp, _vp]),
         "tetra_crc16": (_i32, [_vp, _vp, _sz, _sz, _i32, _vp]),
         "tetra_check_crc": (_i32, [_vp, _vp, _sz, _sz, _vp]),
+        "tetra_mac_headers": (_i32, [_vp, _vp, _vp, _sz, _sz, _vp, _vp, _sz]),
         "tetra_etsi_lengths": (_i32, [ctypes.POINTER(EtsiPlan), _sz, _vp, _vp, _vp]),
         "tetra_etsi_chanfilt": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _sz, _sz, _vp]),
         "tetra_etsi_timing": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _sz, _sz, _vp, _vp, _vp, _vp, _sz, _vp]),

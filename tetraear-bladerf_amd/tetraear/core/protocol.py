@@ -5,9 +5,10 @@ Mirrors the hot-path part of /root/reference/tetraear/core/protocol.py:
                                                              protocol.py:34-139
   TetraProtocolParser.parse_burst and helpers, _check_crc, _calculate_crc16
                                                              protocol.py:142-347
-Burst typing, slicing and the CRC run in libtetra_hip.so.  The upper-MAC parsers of the
-reference (parse_mac_pdu, SDS, LIP, call metadata -- protocol.py:349-1300) are out of scope of
-this hot-path build and stay the reference's Python; ``upper_mac`` hooks are where they attach
+  parse_mac_pdu (MAC PDU headers, fragment reassembly)          protocol.py:349-596
+Burst typing, slicing, the CRC and the MAC PDU header fields run in libtetra_hip.so.  The rest of
+the reference's upper MAC (SDS, LIP, call metadata -- protocol.py:597-1300) is out of scope of
+this hot-path build and stays the reference's Python; ``upper_mac`` hooks are where it attaches
 (INTEGRATION.md).
 """
 import logging
@@ -211,9 +212,80 @@ class TetraProtocolParser:
         v = int(crc[0])
         return np.array([(v >> i) & 1 for i in range(15, -1, -1)])
 
-    # upper MAC (protocol.py:349-1300) is the reference's Python; attach it here
-    def parse_mac_pdu(self, bits):
-        return None
+    def parse_mac_pdu(self, bits) -> Optional[MacPDU]:
+        """MAC PDU of one slot's data bits (protocol.py:349-596): header fields and data bytes
+        from the GPU (tetra_mac_headers), fragment buffer / SYSINFO state / statistics here."""
+        if len(bits) < 8:   # protocol.py:360-361, without a launch
+            return None
+        return self.parse_mac_pdu_batch([bits])[0]
+
+    def parse_mac_pdu_batch(self, frames) -> list:
+        """parse_mac_pdu over many frames in order, one launch: [MacPDU or None].
+
+        Frames are 0/1 bit vectors, as parse_burst's data_bits.  (The reference would raise a
+        ValueError from int(..., 2) for other values inside a parsed numeric field and shift them
+        into the header fields; this build rejects them up front with a ValueError.)"""
+        rows = [np.asarray(f).ravel() for f in frames]
+        F = len(rows)
+        if F == 0:
+            return []
+        for r in rows:
+            if r.size and not np.all((r == 0) | (r == 1)):
+                raise ValueError("parse_mac_pdu: bits must be 0/1")
+        stride = max(8, max(r.size for r in rows))
+        bits = np.zeros((F, stride), np.uint8)
+        nbits = np.zeros(F, np.int32)
+        for i, r in enumerate(rows):
+            bits[i, :r.size] = r
+            nbits[i] = r.size
+        dstride = (stride + 7) // 8
+        fields = np.zeros((F, _hip.MAC_FIELDS), np.int32)
+        data = np.zeros((F, dstride), np.uint8)
+        c = _hip.ctx()
+        c.check(c.lib.tetra_mac_headers(c.handle, _hip.ptr(bits), _hip.ptr(nbits), F, stride, _hip.ptr(fields),
+                                        _hip.ptr(data), dstride), "tetra_mac_headers")
+        return [self._mac_state(fields[i], data[i]) for i in range(F)]
+
+    def _mac_state(self, r, data):
+        """The stateful half of parse_mac_pdu for one frame's device fields, in order."""
+        status = int(r[_hip.MAC_STATUS])
+        if r[_hip.MAC_SYSINFO]:   # set before the sanity check (protocol.py:483-485)
+            self.mcc, self.mnc, self.colour_code = int(r[_hip.MAC_MCC]), int(r[_hip.MAC_MNC]), int(r[_hip.MAC_CC])
+            if status == 2:
+                logger.debug(f"Invalid MCC {self.mcc} / MNC {self.mnc} in SYNC - not real TETRA")
+            else:
+                logger.info(f"Valid TETRA SYNC: MCC={self.mcc} MNC={self.mnc}")
+        if status != 0:
+            return None
+        ptype = PDUType(int(r[_hip.MAC_PTYPE]))
+        mode = int(r[_hip.MAC_MODE])
+        encrypted = mode > 0
+        address = int(r[_hip.MAC_ADDR]) if ptype == PDUType.MAC_RESOURCE else None
+        length = int(r[_hip.MAC_LENGTH])
+        data_bytes = bytes(data[:(int(r[_hip.MAC_DATA_BITS]) + 7) // 8])
+        if ptype == PDUType.MAC_RESOURCE:                                   # protocol.py:446-449
+            self.fragment_buffer = bytearray(data_bytes)
+            self.fragment_metadata = {'address': address, 'encrypted': encrypted, 'mode': mode}
+        elif ptype in (PDUType.MAC_FRAG, PDUType.MAC_END):                  # :463-469, :538-544
+            self.fragment_buffer.extend(data_bytes)
+            if self.fragment_metadata:
+                encrypted = self.fragment_metadata.get('encrypted', False)
+                address = self.fragment_metadata.get('address')
+        self.stats['encrypted_frames' if encrypted else 'clear_mode_frames'] += 1   # :546-549
+        pdu = MacPDU(pdu_type=ptype, encrypted=encrypted, address=address, length=length, data=data_bytes,
+                     fill_bits=int(r[_hip.MAC_FILL]), encryption_mode=mode)
+        if ptype == PDUType.MAC_END:                                        # :573-583
+            if self.fragment_buffer:
+                pdu.reassembled_data = bytes(self.fragment_buffer)
+                if self.fragment_metadata:
+                    if not pdu.address:
+                        pdu.address = self.fragment_metadata.get('address')
+                    pdu.encrypted = self.fragment_metadata.get('encrypted', False)
+                self.fragment_buffer = bytearray()
+                self.fragment_metadata = {}
+        elif ptype == PDUType.MAC_RESOURCE:                                 # :585-594
+            pdu.reassembled_data = bytes(data_bytes)
+        return pdu
 
     def get_statistics(self):
         return dict(self.stats)
