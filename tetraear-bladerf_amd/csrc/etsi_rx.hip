@@ -23,6 +23,8 @@
 //   k_etsi_viterbi  one lane per job: descramble + deinterleave + depuncture gathers from an LDS
 //                row, 16-state rate-1/4 Viterbi with metrics in registers, survivors coalesced in
 //                global scratch, traceback with the CRC-16 folded in.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -909,17 +911,24 @@ __host__ __device__ inline size_t job_cap(int kind, size_t C) { return kind == 1
 // indexed by (channel, slot), so results do not depend on the allocation order).
 constexpr int SYNC_WAVES = 4;   // channels per workgroup: one job-counter atomic per workgroup
 
-__global__ __launch_bounds__(64 * SYNC_WAVES) void k_etsi_sync(const uint8_t *__restrict__ hard, const int32_t *__restrict__ nsym,
-                                                  int smax, int32_t *__restrict__ nburst, int32_t *__restrict__ bursts,
-                                                  int32_t *__restrict__ nblock,
-                                                  unsigned long long *__restrict__ jcount, Job *__restrict__ jobs,
-                                                  int C) {
+struct SyncLds {
+    uint64_t words_all[SYNC_WAVES][LMAC_MAXBITS / 64 + 2];
+    int bstart_all[SYNC_WAVES][ETSI_MAXB], bkind_all[SYNC_WAVES][ETSI_MAXB];
+    int per_all[SYNC_WAVES][3];
+    unsigned long long block_old;
+};
+
+__device__ __forceinline__ void sync_group(SyncLds &L, int grp, const uint8_t *__restrict__ hard,
+                                           const int32_t *__restrict__ nsym, int smax, int32_t *__restrict__ nburst,
+                                           int32_t *__restrict__ bursts, int32_t *__restrict__ nblock,
+                                           unsigned long long *__restrict__ jcount, Job *__restrict__ jobs, int C) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int ch = blockIdx.x * SYNC_WAVES + wv;
-    __shared__ uint64_t words_all[SYNC_WAVES][LMAC_MAXBITS / 64 + 2];
-    __shared__ int bstart_all[SYNC_WAVES][ETSI_MAXB], bkind_all[SYNC_WAVES][ETSI_MAXB];
-    __shared__ int per_all[SYNC_WAVES][3];
-    __shared__ unsigned long long block_old;
+    const int ch = grp * SYNC_WAVES + wv;
+    auto &words_all = L.words_all;
+    auto &bstart_all = L.bstart_all;
+    auto &bkind_all = L.bkind_all;
+    auto &per_all = L.per_all;
+    auto &block_old = L.block_old;
     uint64_t *words = words_all[wv];
     int *bstart = bstart_all[wv], *bkind = bkind_all[wv];
     const int S = ch < C ? nsym[ch] : 0;
@@ -1030,6 +1039,24 @@ __global__ __launch_bounds__(64 * SYNC_WAVES) void k_etsi_sync(const uint8_t *__
     }
 }
 
+
+// Grid: one workgroup per SYNC_WAVES channels, walked with a grid stride (TETRA_SYNC_GRID caps it).
+__global__ __launch_bounds__(64 * SYNC_WAVES) void k_etsi_sync(const uint8_t *__restrict__ hard, const int32_t *__restrict__ nsym,
+                                                  int smax, int32_t *__restrict__ nburst, int32_t *__restrict__ bursts,
+                                                  int32_t *__restrict__ nblock,
+                                                  unsigned long long *__restrict__ jcount, Job *__restrict__ jobs,
+                                                  int C) {
+    __shared__ SyncLds L;
+#ifdef SYNC_NOOP   // timing-only variant: no bursts found (job counters stay 0), so no Viterbi work
+    return;
+#endif
+    const int ng = (C + SYNC_WAVES - 1) / SYNC_WAVES;
+    for (int g = blockIdx.x; g < ng; g += gridDim.x) {
+        sync_group(L, g, hard, nsym, smax, nburst, bursts, nblock, jcount, jobs, C);
+        __syncthreads();   // L is reused by the next group
+    }
+}
+
 // --------------------------------------------------------------------------- E4 Viterbi
 // Four LANES per coded block (one DPP quad) holding the 16 path metrics (layout below).  The quad gathers
 // (descramble + deinterleave) into one shared LDS row; each lane packs its 4 decision bits of 8
@@ -1107,6 +1134,7 @@ __device__ __forceinline__ void viterbi_wave(int8_t *rows, const Job *__restrict
     const size_t j = jbase + jl;
     const Job jb = act ? jobs[j] : Job{0, 0, 0, 0, KIND, 0};
     int8_t *row = rows + jw * VROW;
+#ifndef VIT_SKIP_GATHER   // timing-only variant (tools/build_variant.sh): rows left as they are
     if (act) {   // the quad splits the gather: lane q takes 8-position blocks 4k + q
         const int8_t *sb = softbits + (size_t)jb.ch * 2 * smax + jb.off;
         const uint8_t *scr = KIND == 2 ? bsch_scr : cell_scr + (size_t)jb.ch * 432;
@@ -1131,6 +1159,7 @@ __device__ __forceinline__ void viterbi_wave(int8_t *rows, const Job *__restrict
             for (int u = 0; u < 8; ++u) row[i0 - 1 + u] = sc[u] ? (int8_t)(-v[u]) : v[u];
         }
     }
+#endif
     __syncthreads();   // the quad's row (one wave per workgroup)
     int32_t pm[4];
 #pragma unroll
@@ -1191,20 +1220,27 @@ __global__ __launch_bounds__(64) void k_etsi_viterbi(const Job *__restrict__ job
                                                      uint32_t *__restrict__ surv, int32_t *__restrict__ blocks,
                                                      uint8_t *__restrict__ type1) {
     __shared__ __attribute__((aligned(16))) int8_t rows[16 * VROW];
-    const int b = blockIdx.x;
-    const int nb0 = (int)((job_cap(0, C) + 15) / 16), nb1 = (int)((job_cap(1, C) + 15) / 16);
+#ifdef VIT_NOOP   // timing-only variant: the lower MAC without its Viterbi
+    return;
+#endif
     const size_t ss = 32 * (size_t)C;
     const unsigned long long cnt = *jcount;
     const int n0 = (int)(cnt & 0x1FFFFFull), n1 = (int)((cnt >> 21) & 0x1FFFFFull), n2 = (int)(cnt >> 42);
-    if (b < nb0)
-        viterbi_wave<0>(rows, jobs, n0, job_base(0, C), b, ss, softbits, smax, cell_scr, bsch_scr, surv, blocks,
-                        type1);
-    else if (b < nb0 + nb1)
-        viterbi_wave<1>(rows, jobs, n1, job_base(1, C), b - nb0, ss, softbits, smax, cell_scr, bsch_scr, surv,
-                        blocks, type1);
-    else
-        viterbi_wave<2>(rows, jobs, n2, job_base(2, C), b - nb0 - nb1, ss, softbits, smax, cell_scr, bsch_scr,
-                        surv, blocks, type1);
+    // the waves the job counts need (16 blocks each), walked with a grid stride: a grid smaller
+    // than that keeps the lower MAC's LDS beside the demod's bounded when the two run side by side
+    const int nb0 = (n0 + 15) / 16, nb1 = (n1 + 15) / 16, nb2 = (n2 + 15) / 16;
+    for (int b = blockIdx.x; b < nb0 + nb1 + nb2; b += gridDim.x) {
+        if (b < nb0)
+            viterbi_wave<0>(rows, jobs, n0, job_base(0, C), b, ss, softbits, smax, cell_scr, bsch_scr, surv, blocks,
+                            type1);
+        else if (b < nb0 + nb1)
+            viterbi_wave<1>(rows, jobs, n1, job_base(1, C), b - nb0, ss, softbits, smax, cell_scr, bsch_scr, surv,
+                            blocks, type1);
+        else
+            viterbi_wave<2>(rows, jobs, n2, job_base(2, C), b - nb0 - nb1, ss, softbits, smax, cell_scr, bsch_scr,
+                            surv, blocks, type1);
+        __syncthreads();   // rows are rewritten by the next wave-batch
+    }
 }
 
 // --------------------------------------------------------------------------- component kernels
@@ -1548,12 +1584,17 @@ int tetra_lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard,
     {
         PROF(ctx, "etsi_sync");
         HIP_TRY(ctx, hipMemsetAsync(jcount, 0, 16, ctx->stream));
-        hipLaunchKernelGGL(k_etsi_sync, dim3((unsigned)((C + SYNC_WAVES - 1) / SYNC_WAVES)), dim3(64 * SYNC_WAVES), 0,
+        unsigned ngrp = (unsigned)((C + SYNC_WAVES - 1) / SYNC_WAVES);
+        static const long sgrid = [] { const char *e = getenv("TETRA_SYNC_GRID"); return e ? atol(e) : 0L; }();
+        if (sgrid > 0 && (unsigned long)sgrid < ngrp) ngrp = (unsigned)sgrid;
+        hipLaunchKernelGGL(k_etsi_sync, dim3(ngrp), dim3(64 * SYNC_WAVES), 0,
                            ctx->stream, hd, ns, (int)smax, nbo, bo, nko, jcount, jobs, (int)C);
     }
     {
         PROF(ctx, "etsi_viterbi");
-        const unsigned nblk = (unsigned)((job_cap(0, C) + 15) / 16 + (job_cap(1, C) + 15) / 16 + (job_cap(2, C) + 15) / 16);
+        unsigned nblk = (unsigned)((job_cap(0, C) + 15) / 16 + (job_cap(1, C) + 15) / 16 + (job_cap(2, C) + 15) / 16);
+        static const long vgrid = [] { const char *e = getenv("TETRA_VIT_GRID"); return e ? atol(e) : 0L; }();
+        if (vgrid > 0 && (unsigned long)vgrid < nblk) nblk = (unsigned)vgrid;
         hipLaunchKernelGGL(k_etsi_viterbi, dim3(nblk), dim3(64), 0, ctx->stream, jobs, jcount, (int)C, sb, (int)smax,
                            cells, cells + ctx->cells * 432, surv, ko, to);
     }
