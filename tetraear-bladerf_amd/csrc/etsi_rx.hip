@@ -20,8 +20,9 @@
 //   k_etsi_sync  one wave per channel: hard bits packed by ballots, head/training/tail correlation
 //                by XOR+popcount, greedy burst scan, one decode job per coded block (dense atomic
 //                allocation).
-//   k_etsi_viterbi  one lane per job: descramble + deinterleave + depuncture gathers from an LDS
-//                row, 16-state rate-1/4 Viterbi with metrics in registers, survivors coalesced in
+//   k_etsi_viterbi  four lanes per job: the block's type-5 soft bits loaded as dwords and
+//                descrambled into an LDS row, deinterleave + depuncture applied on the trellis's
+//                reads, 16-state rate-1/4 Viterbi with metrics in registers, survivors coalesced in
 //                global scratch, traceback with the CRC-16 folded in.
 #include <cstdlib>
 
@@ -1058,8 +1059,11 @@ __global__ __launch_bounds__(64 * SYNC_WAVES) void k_etsi_sync(const uint8_t *__
 }
 
 // --------------------------------------------------------------------------- E4 Viterbi
-// Four LANES per coded block (one DPP quad) holding the 16 path metrics (layout below).  The quad gathers
-// (descramble + deinterleave) into one shared LDS row; each lane packs its 4 decision bits of 8
+// Four LANES per coded block (one DPP quad) holding the 16 path metrics (layout below).  The quad loads
+// the block's type-5 soft bits into one shared LDS row, descrambled (load_seg: 16 contiguous bytes
+// per quad per load; the byte gather this replaced -- two scattered byte loads per soft bit -- was
+// what the Viterbi cost the demod running beside it), and the trellis reads that row through the
+// deinterleaver (acs_groups4); each lane packs its 4 decision bits of 8
 // steps into one survivor dword ([group][job][lane], coalesced); all four lanes trace back (same
 // path) and lane 0 writes the block with the CRC accumulated on the fly.  16 blocks per 64-lane
 // workgroup keep LDS at 7 KB, so Viterbi workgroups fit beside the demod's on a CU.
@@ -1070,6 +1074,39 @@ __device__ __forceinline__ int32_t quad_perm(int32_t v) {
     return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
 }
 
+// One contiguous segment of a block's type-5 soft bits (ND dwords) into the LDS row, descrambled.
+// The quad reads the segment as aligned dwords, lane q taking dwords 4 i + q (16 contiguous bytes
+// per quad per load), and realigns them with v_alignbyte, the next dword coming from the neighbour
+// lane (quad rotate) or, for lane 3, from lane 0 of the next load.  A dword is loaded only if it
+// starts at or before the buffer's last byte (`last`, a dword that holds it): a clamped load reads
+// bytes the segment does not use.  Descrambling negates the int8 values whose scrambler byte is 1
+// (four at a time: x ^ 0xFF + 1 per flagged byte, carry-free SWAR), as -v in int8 does.
+template <int ND>
+__device__ __forceinline__ void load_seg(const int8_t *seg, const int8_t *last, const uint32_t *__restrict__ scr32,
+                                         uint32_t *d32, int q) {
+    constexpr int NI = (ND + 1 + 3) / 4;   // loads per lane: dwords 0 .. ND of the aligned window
+    const uintptr_t pa = (uintptr_t)seg, lim = (uintptr_t)last & ~(uintptr_t)3;
+    const int sh = (int)(pa & 3);
+    const uintptr_t a0 = pa - sh;
+    uint32_t R[NI], S[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int j = 4 * i + q;
+        R[i] = *(const uint32_t *)std::min(a0 + 4 * (uintptr_t)j, lim);
+        S[i] = scr32[std::min(j, ND - 1)];
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int j = 4 * i + q;
+        const uint32_t nq = (uint32_t)quad_perm<0x39>((int32_t)R[i]);   // lane (q + 1) & 3
+        const uint32_t n0 = i + 1 < NI ? (uint32_t)quad_perm<0x00>((int32_t)R[i + 1]) : 0u;
+        const uint32_t v = __builtin_amdgcn_alignbyte(q == 3 ? n0 : nq, R[i], (uint32_t)sh);
+        const uint32_t m = S[i] * 0xFFu, x = v ^ m;   // scrambler bytes are 0 / 1
+        const uint32_t dv = ((x & 0x7F7F7F7Fu) + (m & 0x01010101u)) ^ (x & 0x80808080u);
+        if (j < ND) d32[j] = dv;
+    }
+}
+
 // Strided state layout: lane l of the quad holds states n = 4 i + l in pm[i].  New state n has
 // predecessors p0 = n >> 1 = 2 i + (l >> 1) (register i >> 1 of lane (2 i + (l >> 1)) & 3) and
 // p1 = p0 | 8 (register (i >> 1) + 2, same lane): for a given i both sit in one register of a lane
@@ -1078,17 +1115,26 @@ __device__ __forceinline__ int32_t quad_perm(int32_t v) {
 // Survivors: a lane packs its 4 decision bits of 8 consecutive steps into one dword (bit
 // 4 (t & 7) + i for state 4 i + l at step t) and stores it once per 8 steps, [group][job][lane]:
 // one coalesced 256-B store per wave per 8 steps.
-template <int GROUPS>
+// The row holds the descrambled block in type-5 order; the deinterleaver is applied on the read:
+// type-3 value i (1-based) is type-5 value k(i) = 1 + (A i mod K).  The index walk is the same for
+// every lane of the wave (one block kind per wave), so it stays in scalar registers.
+template <int GROUPS, int A, int K>
 __device__ __forceinline__ void acs_groups4(int32_t (&pm)[4], int q, const int8_t *row, uint32_t *sv, size_t gstride) {
     // rate-2/3 puncturing: step 2g sees mother outputs (g1, g2) = type-3 (3g, 3g+1); step 2g+1 sees
     // g1 = type-3 3g+2; the other mother outputs are erased.
     const bool bb = q & 1, d0 = (q >> 1) & 1;   // bits 0 and 1 of this lane's states
+    int r = 0;   // A i mod K for the type-3 value read last
+    auto next = [&r]() {
+        r += A;
+        if (r >= K) r -= K;
+        return r;
+    };
     for (int gi = 0; gi < GROUPS; ++gi) {
         uint32_t word = 0;
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-            const int g = 4 * gi + g4;
-            const int32_t a = row[3 * g], b = row[3 * g + 1], c = row[3 * g + 2];
+            const int i0 = next(), i1 = next(), i2 = next();
+            const int32_t a = row[i0], b = row[i1], c = row[i2];
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
                 // branch metric for d3 = 0 (d3 = 1 negates every generator output):
@@ -1123,7 +1169,7 @@ __device__ __forceinline__ void acs_groups4(int32_t (&pm)[4], int q, const int8_
 template <int KIND>
 __device__ __forceinline__ void viterbi_wave(int8_t *rows, const Job *__restrict__ jobs, int nj, size_t jbase, int lb,
                                              size_t ss, const int8_t *__restrict__ softbits, int smax,
-                                             const uint8_t *__restrict__ cell_scr,
+                                             const int8_t *sb_last, const uint8_t *__restrict__ cell_scr,
                                              const uint8_t *__restrict__ bsch_scr, uint32_t *__restrict__ surv,
                                              int32_t *__restrict__ blocks, uint8_t *__restrict__ type1) {
     constexpr KindP P = kind_params(KIND);
@@ -1135,28 +1181,15 @@ __device__ __forceinline__ void viterbi_wave(int8_t *rows, const Job *__restrict
     const Job jb = act ? jobs[j] : Job{0, 0, 0, 0, KIND, 0};
     int8_t *row = rows + jw * VROW;
 #ifndef VIT_SKIP_GATHER   // timing-only variant (tools/build_variant.sh): rows left as they are
-    if (act) {   // the quad splits the gather: lane q takes 8-position blocks 4k + q
+    if (act) {   // the quad loads the block's type-5 soft bits and scrambler bytes as dwords
         const int8_t *sb = softbits + (size_t)jb.ch * 2 * smax + jb.off;
         const uint8_t *scr = KIND == 2 ? bsch_scr : cell_scr + (size_t)jb.ch * 432;
-        for (int i0 = 1 + 8 * q; i0 <= P.K; i0 += 32) {
-            int r = (int)(((long)P.a * (i0 - 1)) % P.K);   // a*i mod K, incrementally below
-            int kk[8];
-            int8_t v[8];
-            uint8_t sc[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                r += P.a;
-                if (r >= P.K) r -= P.K;
-                kk[u] = r;   // 0-based type-5 index: k(i) - 1 = (a*i mod K)
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int pos = (KIND == 0 && kk[u] >= 216) ? kk[u] + 52 : kk[u];   // SCH/F: BKN2 268 after BKN1
-                v[u] = sb[pos];
-                sc[u] = scr[kk[u]];
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) row[i0 - 1 + u] = sc[u] ? (int8_t)(-v[u]) : v[u];
+        uint32_t *d32 = (uint32_t *)row;
+        if constexpr (KIND == 0) {   // SCH/F: BKN1 = type-5 [0, 216), BKN2 = [216, 432) 268 bits on
+            load_seg<54>(sb, sb_last, (const uint32_t *)scr, d32, q);
+            load_seg<54>(sb + 268, sb_last, (const uint32_t *)scr + 54, d32 + 54, q);
+        } else {
+            load_seg<P.K / 4>(sb, sb_last, (const uint32_t *)scr, d32, q);
         }
     }
 #endif
@@ -1168,7 +1201,7 @@ __device__ __forceinline__ void viterbi_wave(int8_t *rows, const Job *__restrict
     uint32_t *sv = surv + 4 * j + q;
     if (act) {
         constexpr int NG = P.n2 / 8;   // n2 is a multiple of 8
-        acs_groups4<NG>(pm, q, row, sv, gstride);
+        acs_groups4<NG, P.a, P.K>(pm, q, row, sv, gstride);
         __threadfence_block();   // the quad's survivor words are read back below (same wave)
         // traceback from state 0 (tail bits), CRC over type-1 + CRC bits on the fly.  The words do
         // not depend on the state: each lane loads its own for 8 groups (64 steps) at a time, the
@@ -1224,6 +1257,7 @@ __global__ __launch_bounds__(64) void k_etsi_viterbi(const Job *__restrict__ job
     return;
 #endif
     const size_t ss = 32 * (size_t)C;
+    const int8_t *sb_last = softbits + (size_t)C * 2 * smax - 1;   // the soft-bit buffer's last byte
     const unsigned long long cnt = *jcount;
     const int n0 = (int)(cnt & 0x1FFFFFull), n1 = (int)((cnt >> 21) & 0x1FFFFFull), n2 = (int)(cnt >> 42);
     // the waves the job counts need (16 blocks each), walked with a grid stride: a grid smaller
@@ -1231,13 +1265,13 @@ __global__ __launch_bounds__(64) void k_etsi_viterbi(const Job *__restrict__ job
     const int nb0 = (n0 + 15) / 16, nb1 = (n1 + 15) / 16, nb2 = (n2 + 15) / 16;
     for (int b = blockIdx.x; b < nb0 + nb1 + nb2; b += gridDim.x) {
         if (b < nb0)
-            viterbi_wave<0>(rows, jobs, n0, job_base(0, C), b, ss, softbits, smax, cell_scr, bsch_scr, surv, blocks,
+            viterbi_wave<0>(rows, jobs, n0, job_base(0, C), b, ss, softbits, smax, sb_last, cell_scr, bsch_scr, surv, blocks,
                             type1);
         else if (b < nb0 + nb1)
-            viterbi_wave<1>(rows, jobs, n1, job_base(1, C), b - nb0, ss, softbits, smax, cell_scr, bsch_scr, surv,
+            viterbi_wave<1>(rows, jobs, n1, job_base(1, C), b - nb0, ss, softbits, smax, sb_last, cell_scr, bsch_scr, surv,
                             blocks, type1);
         else
-            viterbi_wave<2>(rows, jobs, n2, job_base(2, C), b - nb0 - nb1, ss, softbits, smax, cell_scr, bsch_scr,
+            viterbi_wave<2>(rows, jobs, n2, job_base(2, C), b - nb0 - nb1, ss, softbits, smax, sb_last, cell_scr, bsch_scr,
                             surv, blocks, type1);
         __syncthreads();   // rows are rewritten by the next wave-batch
     }
