@@ -290,6 +290,40 @@ def test_lower_mac_empty_and_low_snr():
     assert nblk > 0
 
 
+@pytest.mark.parametrize("extra", [1, 2, 3, 4])
+def test_lower_mac_row_alignments(synth_small, extra):
+    """The Viterbi loads a block as aligned dwords and realigns them (load_seg): rows of odd and even
+    width (row bases at every byte alignment mod 4), each channel's symbols shifted to END at its
+    row's end, so the last channel's last blocks reach the buffer's final bytes.  Block for block
+    equal to the oracle on the same rows."""
+    from tetraear.signal.etsi import EtsiReceiver
+    from tetraear.core.etsi import EtsiLowerMac
+    iq, cells, _, _, _ = synth_small
+    hard, soft, _, ns = EtsiReceiver().demod_batch(iq)
+    C = len(iq)
+    sm = int(ns.max()) + extra
+    h2 = np.zeros((C, sm), np.uint8)
+    s2 = np.zeros((C, 2 * sm), np.int8)
+    ns2 = np.full(C, sm, np.int32)
+    for ch in range(C):
+        n = int(ns[ch])
+        pad = sm - n
+        h2[ch, pad:pad + n - 1] = hard[ch, :n - 1]
+        s2[ch, 2 * pad:2 * (pad + n - 1)] = soft[ch, :2 * (n - 1)]
+    res = EtsiLowerMac().decode_batch(s2, h2, ns2, cells)
+    rx = E.Receiver()
+    nblk = 0
+    for ch in range(C):
+        want = rx.lower_mac(s2[ch, :2 * (sm - 1)], h2[ch, :sm - 1], int(cells[ch]))
+        got = res[ch]
+        assert [(f["position"], f["burst_kind"]) for f in got] == [(s, k) for s, k, _ in want], ch
+        for f, (_, _, dec) in zip(got, want):
+            for b, (_, bits, ok) in zip(f["blocks"], dec):
+                assert b["crc_ok"] == ok and np.array_equal(b["bits"], bits), ch
+                nblk += 1
+    assert nblk >= 12
+
+
 def test_fused_demod_many_channels():
     """The fused cf32 demod over more channels than the chip holds workgroups at once (two per CU: the
     grid runs in three waves of workgroups): bit-identical to the component path (chanfilt -> y in HBM
