@@ -883,16 +883,16 @@ constexpr int LMAC_MAXBITS = 2 * 2048;
 // 1-bits at distance d from the end of T[d].  Lets the serial traceback, which emits bits last
 // to first, check the CRC on the fly instead of a second serial pass.
 struct CrcTab {
-    uint16_t t[288];
-    uint16_t init[289];
+    uint32_t t[288];   // dwords: read with wave-uniform scalar loads
+    uint32_t init[289];
 };
 constexpr uint32_t crc_step(uint32_t r) { return ((r & 0x8000u) ? ((r << 1) ^ 0x1021u) : (r << 1)) & 0xFFFFu; }
 constexpr CrcTab make_crc_tab() {
     CrcTab c{};
     uint32_t r = crc_step(0x8000u);
-    for (int d = 0; d < 288; ++d) { c.t[d] = (uint16_t)r; r = crc_step(r); }
+    for (int d = 0; d < 288; ++d) { c.t[d] = r; r = crc_step(r); }
     uint32_t s = 0xFFFFu;
-    for (int L = 0; L <= 288; ++L) { c.init[L] = (uint16_t)s; s = crc_step(s); }
+    for (int L = 0; L <= 288; ++L) { c.init[L] = s; s = crc_step(s); }
     return c;
 }
 __constant__ CrcTab CRC_TAB = make_crc_tab();
@@ -1170,8 +1170,7 @@ template <int KIND>
 __device__ __forceinline__ void viterbi_wave(int8_t *rows, const Job *__restrict__ jobs, int nj, size_t jbase, int lb,
                                              size_t ss, const int8_t *__restrict__ softbits, int smax,
                                              const int8_t *sb_last, const uint8_t *__restrict__ cell_scr,
-                                             const uint8_t *__restrict__ bsch_scr, uint32_t *__restrict__ surv,
-                                             int32_t *__restrict__ blocks, uint8_t *__restrict__ type1) {
+                                             const uint8_t *__restrict__ bsch_scr, uint32_t *__restrict__ surv) {
     constexpr KindP P = kind_params(KIND);
     const int lane = threadIdx.x, jw = lane >> 2, q = lane & 3;
     const int jl = lb * 16 + jw;
@@ -1202,46 +1201,52 @@ __device__ __forceinline__ void viterbi_wave(int8_t *rows, const Job *__restrict
     if (act) {
         constexpr int NG = P.n2 / 8;   // n2 is a multiple of 8
         acs_groups4<NG, P.a, P.K>(pm, q, row, sv, gstride);
-        __threadfence_block();   // the quad's survivor words are read back below (same wave)
-        // traceback from state 0 (tail bits), CRC over type-1 + CRC bits on the fly.  The words do
-        // not depend on the state: each lane loads its own for 8 groups (64 steps) at a time, the
-        // quad broadcasts them (DPP), and a step only selects lane s2 >> 2's word.
-        constexpr int L = P.n1 + 16;
-        uint32_t c = CRC_TAB.init[L];
-        int s2 = 0;
-        uint8_t *op = type1 + ((size_t)jb.ch * ETSI_MAXJ + jb.slot) * 268;
-        for (int g0 = NG - 1; g0 >= 0; g0 -= 8) {
-            uint32_t w[8];
+    }
+}
+
+// Traceback + CRC of one block per LANE (k_etsi_traceback): 64 blocks per wave, a quarter of the
+// wave instructions the quad-per-block trellis waves would spend on the same serial chain (all four
+// lanes of a quad followed the same path).  From state 0 (tail bits); a group's four survivor words
+// ([group][job][lane]) are one 16-B load, eight groups (64 steps) in flight; the CRC over type-1 +
+// CRC bits accumulates on the fly; type-1 bits go out four per dword store.
+template <int KIND>
+__device__ __forceinline__ void traceback_lane(const Job &jb, const uint32_t *__restrict__ sv, size_t gstride,
+                                               int32_t *__restrict__ blocks, uint8_t *__restrict__ type1) {
+    constexpr KindP P = kind_params(KIND);
+    constexpr int NG = P.n2 / 8;
+    constexpr int L = P.n1 + 16;
+    static_assert(P.n1 % 4 == 0, "type-1 bits stored four per dword");
+    uint32_t c = CRC_TAB.init[L];
+    int s2 = 0;
+    uint32_t acc = 0;
+    uint32_t *op = (uint32_t *)(type1 + ((size_t)jb.ch * ETSI_MAXJ + jb.slot) * 268);
+    for (int g0 = NG - 1; g0 >= 0; g0 -= 8) {
+        uint4 w[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) w[u] = g0 - u >= 0 ? sv[(size_t)(g0 - u) * gstride] : 0u;
+        for (int u = 0; u < 8; ++u) w[u] = *(const uint4 *)(sv + (size_t)max(g0 - u, 0) * gstride);
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int gi = g0 - u;
-                if (gi < 0) break;
-                const int32_t wi = (int32_t)w[u];
-                const uint32_t w0 = (uint32_t)quad_perm<0x00>(wi), w1 = (uint32_t)quad_perm<0x55>(wi),
-                               w2 = (uint32_t)quad_perm<0xAA>(wi), w3 = (uint32_t)quad_perm<0xFF>(wi);
+        for (int u = 0; u < 8; ++u) {
+            const int gi = g0 - u;
+            if (gi < 0) break;
 #pragma unroll
-                for (int st = 7; st >= 0; --st) {
-                    const int t = 8 * gi + st;
-                    const int bit = s2 & 1;
-                    if (q == 0 && t < P.n1) op[t] = (uint8_t)bit;
-                    if (bit && t < L) c ^= CRC_TAB.t[L - 1 - t];
-                    // state s2's decision: lane s2 & 3, bit 4 st + (s2 >> 2)
-                    const int ln = s2 & 3;
-                    const uint32_t ww = ln & 2 ? (ln & 1 ? w3 : w2) : (ln & 1 ? w1 : w0);
-                    s2 = (s2 >> 1) | ((int)((ww >> (4 * st + (s2 >> 2))) & 1u) << 3);
-                }
+            for (int st = 7; st >= 0; --st) {
+                const int t = 8 * gi + st;
+                const uint32_t bit = s2 & 1;
+                acc = (acc << 8) | bit;
+                if ((st & 3) == 0 && t < P.n1) op[t >> 2] = acc;   // bytes t .. t+3
+                // unconditional, wave-uniform table read (scalar load, hoisted); a per-lane branch
+                // around it made every step wait a global load
+                const uint32_t tv = CRC_TAB.t[L - 1 - t < 0 ? 0 : L - 1 - t];
+                c ^= tv & (0u - (bit & (uint32_t)(t < L)));
+                // state s2's decision: word of lane s2 & 3, bit 4 st + (s2 >> 2)
+                const int ln = s2 & 3;
+                const uint32_t ww = ln & 2 ? (ln & 1 ? w[u].w : w[u].z) : (ln & 1 ? w[u].y : w[u].x);
+                s2 = (s2 >> 1) | ((int)((ww >> (4 * st + (s2 >> 2))) & 1u) << 3);
             }
         }
-        if (q == 0) {
-            int32_t *bm = blocks + ((size_t)jb.ch * ETSI_MAXJ + jb.slot) * 4;
-            bm[0] = KIND;
-            bm[1] = c == 0x1D0Fu;
-            bm[2] = jb.burst;
-            bm[3] = jb.blk;
-        }
     }
+    int32_t *bm = blocks + ((size_t)jb.ch * ETSI_MAXJ + jb.slot) * 4;
+    *(int4 *)bm = int4{KIND, c == 0x1D0Fu, jb.burst, jb.blk};
 }
 
 // Grid: the SCH/F region's waves, then SCH/HD's, then BSCH's (one trellis length per wave).
@@ -1250,8 +1255,7 @@ __global__ __launch_bounds__(64) void k_etsi_viterbi(const Job *__restrict__ job
                                                      const int8_t *__restrict__ softbits, int smax,
                                                      const uint8_t *__restrict__ cell_scr,
                                                      const uint8_t *__restrict__ bsch_scr,
-                                                     uint32_t *__restrict__ surv, int32_t *__restrict__ blocks,
-                                                     uint8_t *__restrict__ type1) {
+                                                     uint32_t *__restrict__ surv) {
     __shared__ __attribute__((aligned(16))) int8_t rows[16 * VROW];
 #ifdef VIT_NOOP   // timing-only variant: the lower MAC without its Viterbi
     return;
@@ -1265,15 +1269,36 @@ __global__ __launch_bounds__(64) void k_etsi_viterbi(const Job *__restrict__ job
     const int nb0 = (n0 + 15) / 16, nb1 = (n1 + 15) / 16, nb2 = (n2 + 15) / 16;
     for (int b = blockIdx.x; b < nb0 + nb1 + nb2; b += gridDim.x) {
         if (b < nb0)
-            viterbi_wave<0>(rows, jobs, n0, job_base(0, C), b, ss, softbits, smax, sb_last, cell_scr, bsch_scr, surv, blocks,
-                            type1);
+            viterbi_wave<0>(rows, jobs, n0, job_base(0, C), b, ss, softbits, smax, sb_last, cell_scr, bsch_scr, surv);
         else if (b < nb0 + nb1)
-            viterbi_wave<1>(rows, jobs, n1, job_base(1, C), b - nb0, ss, softbits, smax, sb_last, cell_scr, bsch_scr, surv,
-                            blocks, type1);
+            viterbi_wave<1>(rows, jobs, n1, job_base(1, C), b - nb0, ss, softbits, smax, sb_last, cell_scr, bsch_scr,
+                            surv);
         else
-            viterbi_wave<2>(rows, jobs, n2, job_base(2, C), b - nb0 - nb1, ss, softbits, smax, sb_last, cell_scr, bsch_scr,
-                            surv, blocks, type1);
+            viterbi_wave<2>(rows, jobs, n2, job_base(2, C), b - nb0 - nb1, ss, softbits, smax, sb_last, cell_scr,
+                            bsch_scr, surv);
         __syncthreads();   // rows are rewritten by the next wave-batch
+    }
+}
+
+// One lane per block (64 per wave), the kinds' regions one after another; grid stride as above.
+__global__ __launch_bounds__(64) void k_etsi_traceback(const Job *__restrict__ jobs,
+                                                       const unsigned long long *__restrict__ jcount, int C,
+                                                       const uint32_t *__restrict__ surv,
+                                                       int32_t *__restrict__ blocks, uint8_t *__restrict__ type1) {
+    const size_t gstride = 4 * 32 * (size_t)C;   // dwords between survivor groups
+    const unsigned long long cnt = *jcount;
+    const int n[3] = {(int)(cnt & 0x1FFFFFull), (int)((cnt >> 21) & 0x1FFFFFull), (int)(cnt >> 42)};
+    const int nb0 = (n[0] + 63) / 64, nb1 = (n[1] + 63) / 64, nb2 = (n[2] + 63) / 64;
+    for (int b = blockIdx.x; b < nb0 + nb1 + nb2; b += gridDim.x) {
+        const int kind = b < nb0 ? 0 : b < nb0 + nb1 ? 1 : 2;
+        const int jl = 64 * (b - (kind == 0 ? 0 : kind == 1 ? nb0 : nb0 + nb1)) + (int)threadIdx.x;
+        if (jl >= n[kind]) continue;
+        const size_t j = job_base(kind, C) + jl;
+        const Job jb = jobs[j];
+        const uint32_t *sv = surv + 4 * j;
+        if (kind == 0) traceback_lane<0>(jb, sv, gstride, blocks, type1);
+        else if (kind == 1) traceback_lane<1>(jb, sv, gstride, blocks, type1);
+        else traceback_lane<2>(jb, sv, gstride, blocks, type1);
     }
 }
 
@@ -1630,7 +1655,12 @@ int tetra_lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard,
         static const long vgrid = [] { const char *e = getenv("TETRA_VIT_GRID"); return e ? atol(e) : 0L; }();
         if (vgrid > 0 && (unsigned long)vgrid < nblk) nblk = (unsigned)vgrid;
         hipLaunchKernelGGL(k_etsi_viterbi, dim3(nblk), dim3(64), 0, ctx->stream, jobs, jcount, (int)C, sb, (int)smax,
-                           cells, cells + ctx->cells * 432, surv, ko, to);
+                           cells, cells + ctx->cells * 432, surv);
+    }
+    {
+        PROF(ctx, "etsi_traceback");
+        const unsigned ntb = (unsigned)((job_cap(0, C) + 63) / 64 + (job_cap(1, C) + 63) / 64 + (job_cap(2, C) + 63) / 64);
+        hipLaunchKernelGGL(k_etsi_traceback, dim3(ntb), dim3(64), 0, ctx->stream, jobs, jcount, (int)C, surv, ko, to);
     }
     return st.finish();
 }
