@@ -23,7 +23,8 @@
 //   k_etsi_viterbi  four lanes per job: the block's type-5 soft bits loaded as dwords and
 //                descrambled into an LDS row, deinterleave + depuncture applied on the trellis's
 //                reads, 16-state rate-1/4 Viterbi with metrics in registers, survivors coalesced in
-//                global scratch, traceback with the CRC-16 folded in.
+//                global scratch.
+//   k_etsi_traceback  one lane per job: traceback with the CRC-16 folded in.
 #include <cstdlib>
 
 #include "common.h"
