@@ -911,7 +911,10 @@ __host__ __device__ inline size_t job_cap(int kind, size_t C) { return kind == 1
 // One wave per channel: pack hard bits, greedy burst scan, then allocate this channel's coded
 // blocks dense job indices in each kind's region (one atomic per kind per channel; outputs are
 // indexed by (channel, slot), so results do not depend on the allocation order).
-constexpr int SYNC_WAVES = 4;   // channels per workgroup: one job-counter atomic per workgroup
+#ifndef SYNC_WAVES_N
+#define SYNC_WAVES_N 4
+#endif
+constexpr int SYNC_WAVES = SYNC_WAVES_N;   // channels per workgroup: one job-counter atomic per workgroup
 
 struct SyncLds {
     uint64_t words_all[SYNC_WAVES][LMAC_MAXBITS / 64 + 2];
@@ -937,37 +940,34 @@ __device__ __forceinline__ void sync_group(SyncLds &L, int grp, const uint8_t *_
     int nbits = 2 * (S > 1 ? S - 1 : 0);
     if (nbits > LMAC_MAXBITS) nbits = LMAC_MAXBITS;
     const uint8_t *hp = hard + (size_t)ch * smax;
-    // pack hard bits with ballots: 64 dibit symbols per step -> 2 words (bit 2i = b1, 2i+1 = b2)
+    // pack hard bits with ballots: a word holds 32 dibit symbols (bit 2i = b1, 2i+1 = b2), so lane j
+    // of the ballot contributes bit j of the word: component j & 1 of symbol j >> 1.  Two ballots per
+    // 64 symbols and no bit interleave (interleaving two 32-bit ballots was ~80 scalar 64-bit ops per
+    // word, on the CU's one scalar unit shared by all its waves)
     const int nsy = nbits / 2;
     // symbols loaded 8 steps (512 symbols) at a time, all before the first ballot: a load per step
     // in the dependent loop cost one memory latency per 64 symbols
     constexpr int PK = 8;
+    const int sl = lane >> 1, comp = lane & 1;
     for (int s00 = 0; s00 < nsy + 64; s00 += 64 * PK) {
-    uint32_t hb[PK];
+    uint32_t hA[PK], hB[PK];
 #pragma unroll
     for (int u = 0; u < PK; ++u) {
-        const int s = s00 + 64 * u + lane;
-        hb[u] = hp[min(s, smax - 1)];   // unconditional (in the row): no branch join waits per load
+        const int s = s00 + 64 * u + sl;
+        hA[u] = hp[min(s, smax - 1)];   // unconditional (in the row): no branch join waits per load
+        hB[u] = hp[min(s + 32, smax - 1)];
     }
 #pragma unroll
     for (int u = 0; u < PK; ++u) {
         const int s0 = s00 + 64 * u;
         if (s0 >= nsy + 64) break;   // uniform
-        const int s = s0 + lane;
-        const uint32_t h = s < nsy ? hb[u] : 0u;
-        const uint64_t m1 = __ballot((h >> 1) & 1u), m2 = __ballot(h & 1u);
-        auto spread = [](uint64_t x) {   // bit i -> bit 2i (32 -> 64)
-            x &= 0xFFFFFFFFull;
-            x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
-            x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
-            x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
-            x = (x | (x << 2)) & 0x3333333333333333ull;
-            x = (x | (x << 1)) & 0x5555555555555555ull;
-            return x;
-        };
+        const int s = s0 + sl;
+        const uint32_t a = s < nsy ? (comp ? hA[u] : hA[u] >> 1) & 1u : 0u;
+        const uint32_t b = s + 32 < nsy ? (comp ? hB[u] : hB[u] >> 1) & 1u : 0u;
+        const uint64_t wa = __ballot(a), wb = __ballot(b);
         if (lane == 0 && s0 / 32 + 1 < LMAC_MAXBITS / 64 + 2) {
-            words[s0 / 32] = spread(m1) | (spread(m2) << 1);
-            words[s0 / 32 + 1] = spread(m1 >> 32) | (spread(m2 >> 32) << 1);
+            words[s0 / 32] = wa;
+            words[s0 / 32 + 1] = wb;
         }
     }
     }
