@@ -324,6 +324,61 @@ def test_lower_mac_row_alignments(synth_small, extra):
     assert nblk >= 12
 
 
+def test_lower_mac_unaligned_device_buffers(synth_small):
+    """tetra_lmac_etsi on caller-owned device buffers at odd offsets (soft bits and type-1 bits at byte
+    offset 1, burst / block records at 4 bytes): the same results as the host-buffer call."""
+    import torch
+    from tetraear import _hip
+    from tetraear.signal.etsi import EtsiReceiver
+    iq, cells, _, _, _ = synth_small
+    hard, soft, _, ns = EtsiReceiver().demod_batch(iq)
+    C, sm = hard.shape
+    MB, MJ = _hip.ETSI_MAXB, _hip.ETSI_MAXJ
+    c = _hip.ctx()
+    c.check(c.lib.tetra_etsi_set_cells(c.handle, _hip.ptr(np.ascontiguousarray(cells, np.uint32)), C))
+
+    def run(dev):
+        if not dev:
+            outs = [np.zeros(C, np.int32), np.zeros((C, MB, 2), np.int32), np.zeros(C, np.int32),
+                    np.zeros((C, MJ, 4), np.int32), np.zeros((C, MJ, 268), np.uint8)]
+            ins = [soft, hard, ns]
+            ptrs = [_hip.ptr(a) for a in ins + outs]
+        else:
+            d = torch.device("cuda:0")
+            sb = torch.zeros(C * 2 * sm + 1, dtype=torch.int8, device=d)
+            sb[1:] = torch.from_numpy(soft.reshape(-1))
+            hd = torch.from_numpy(hard.reshape(-1)).to(d)
+            nsd = torch.from_numpy(ns).to(d)
+            i32 = [torch.zeros(n + 1, dtype=torch.int32, device=d) for n in (C, C * MB * 2, C, C * MJ * 4)]
+            t1 = torch.zeros(C * MJ * 268 + 1, dtype=torch.uint8, device=d)
+            ptrs = [sb.data_ptr() + 1, hd.data_ptr(), nsd.data_ptr()] + [t.data_ptr() + 4 for t in i32] + \
+                [t1.data_ptr() + 1]
+            outs = (i32, t1)
+        c.check(c.lib.tetra_lmac_etsi(c.handle, ptrs[0], ptrs[1], ptrs[2], C, sm, *ptrs[3:]))
+        if dev:
+            torch.cuda.synchronize()
+            i32, t1 = outs
+            return [t[1:].cpu().numpy() for t in i32] + [t1[1:].cpu().numpy()]
+        return [o.reshape(-1) for o in outs]
+
+    want, got = run(False), run(True)
+    # compared over the entries the call writes (the host-buffer path copies back the rest unset)
+    assert np.array_equal(want[0], got[0]) and np.array_equal(want[2], got[2])
+    nb, nk = want[0], want[2]
+    wb, gb = want[1].reshape(C, MB, 2), got[1].reshape(C, MB, 2)
+    wk, gk = want[3].reshape(C, MJ, 4), got[3].reshape(C, MJ, 4)
+    wt, gt = want[4].reshape(C, MJ, 268), got[4].reshape(C, MJ, 268)
+    ngood = 0
+    for ch in range(C):
+        assert np.array_equal(wb[ch, :nb[ch]], gb[ch, :nb[ch]])
+        assert np.array_equal(wk[ch, :nk[ch]], gk[ch, :nk[ch]])
+        for j in range(nk[ch]):
+            n1 = E.KIND_PARAMS[int(wk[ch, j, 0])][3]
+            assert np.array_equal(wt[ch, j, :n1], gt[ch, j, :n1]), (ch, j)
+            ngood += int(wk[ch, j, 1])
+    assert ngood >= 12
+
+
 def test_fused_demod_many_channels():
     """The fused cf32 demod over more channels than the chip holds workgroups at once (two per CU: the
     grid runs in three waves of workgroups): bit-identical to the component path (chanfilt -> y in HBM

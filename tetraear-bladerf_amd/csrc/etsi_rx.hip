@@ -1220,7 +1220,9 @@ __device__ __forceinline__ void traceback_lane(const Job &jb, const uint32_t *__
     uint32_t c = CRC_TAB.init[L];
     int s2 = 0;
     uint32_t acc = 0;
-    uint32_t *op = (uint32_t *)(type1 + ((size_t)jb.ch * ETSI_MAXJ + jb.slot) * 268);
+    uint8_t *ob = type1 + ((size_t)jb.ch * ETSI_MAXJ + jb.slot) * 268;
+    uint32_t *op = (uint32_t *)ob;
+    const bool al4 = ((uintptr_t)type1 & 3) == 0;   // a caller's device pointer may be unaligned
     for (int g0 = NG - 1; g0 >= 0; g0 -= 8) {
         uint4 w[8];
 #pragma unroll
@@ -1234,7 +1236,14 @@ __device__ __forceinline__ void traceback_lane(const Job &jb, const uint32_t *__
                 const int t = 8 * gi + st;
                 const uint32_t bit = s2 & 1;
                 acc = (acc << 8) | bit;
-                if ((st & 3) == 0 && t < P.n1) op[t >> 2] = acc;   // bytes t .. t+3
+                if ((st & 3) == 0 && t < P.n1) {   // bytes t .. t+3
+                    if (al4) {
+                        op[t >> 2] = acc;
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) ob[t + k] = (uint8_t)(acc >> (8 * k));
+                    }
+                }
                 // unconditional, wave-uniform table read (scalar load, hoisted); a per-lane branch
                 // around it made every step wait a global load
                 const uint32_t tv = CRC_TAB.t[L - 1 - t < 0 ? 0 : L - 1 - t];
@@ -1247,7 +1256,10 @@ __device__ __forceinline__ void traceback_lane(const Job &jb, const uint32_t *__
         }
     }
     int32_t *bm = blocks + ((size_t)jb.ch * ETSI_MAXJ + jb.slot) * 4;
-    *(int4 *)bm = int4{KIND, c == 0x1D0Fu, jb.burst, jb.blk};
+    bm[0] = KIND;   // four dword stores: the caller's pointer need not be 16-B aligned
+    bm[1] = c == 0x1D0Fu;
+    bm[2] = jb.burst;
+    bm[3] = jb.blk;
 }
 
 // Grid: the SCH/F region's waves, then SCH/HD's, then BSCH's (one trellis length per wave).
