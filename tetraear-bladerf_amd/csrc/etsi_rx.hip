@@ -863,9 +863,10 @@ constexpr uint64_t W_HEAD = packb(QB + 10, 12), W_TAIL = packb(QB, 10), W_N = pa
                    W_Y = packb(YB, 38);
 
 __device__ __forceinline__ uint64_t bits_at(const uint64_t *w, int pos, int len) {
+    // branch-free: (x << 1) << (63 - r) is x << (64 - r) for r > 0 and 0 for r = 0 (a per-lane
+    // `if (r)` here made every extraction a divergent branch in the burst scan)
     const int q = pos >> 6, r = pos & 63;
-    uint64_t v = w[q] >> r;
-    if (r) v |= w[q + 1] << (64 - r);
+    const uint64_t v = (w[q] >> r) | ((w[q + 1] << 1) << (63 - r));
     return len == 64 ? v : (v & ((1ull << len) - 1));
 }
 __device__ __forceinline__ int matches(uint64_t v, uint64_t pat, int len) {
@@ -949,7 +950,11 @@ __device__ __forceinline__ void sync_group(SyncLds &L, int grp, const uint8_t *_
     // in the dependent loop cost one memory latency per 64 symbols
     constexpr int PK = 8;
     const int sl = lane >> 1, comp = lane & 1;
+#ifdef SYNC_SKIP_PACK   // timing-only variant: words left as they are
+    for (int s00 = 0; s00 < 0; s00 += 64 * PK) {
+#else
     for (int s00 = 0; s00 < nsy + 64; s00 += 64 * PK) {
+#endif
     uint32_t hA[PK], hB[PK];
 #pragma unroll
     for (int u = 0; u < PK; ++u) {
@@ -973,6 +978,9 @@ __device__ __forceinline__ void sync_group(SyncLds &L, int grp, const uint8_t *_
     }
     __syncthreads();
     int nb = 0;
+#ifdef SYNC_SKIP_SCAN   // timing-only variant: no burst scan
+    nbits = 0;
+#endif
     for (int cur = 0; cur + 510 <= nbits && nb < ETSI_MAXB;) {
         const int s = cur + lane;
         int kind = -1;
@@ -988,7 +996,7 @@ __device__ __forceinline__ void sync_group(SyncLds &L, int grp, const uint8_t *_
         const unsigned long long bal = __ballot(kind >= 0);
         if (bal) {
             const int first = __ffsll((long long)bal) - 1;
-            const int k = __shfl(kind, first, 64);
+            const int k = __builtin_amdgcn_readlane(kind, first);   // first is wave-uniform
             if (lane == 0) { bstart[nb] = cur + first; bkind[nb] = k; }
             ++nb;
             cur = cur + first + 500;
