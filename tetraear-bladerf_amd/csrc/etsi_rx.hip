@@ -869,6 +869,14 @@ __device__ __forceinline__ uint64_t bits_at(const uint64_t *w, int pos, int len)
     const uint64_t v = (w[q] >> r) | ((w[q + 1] << 1) << (63 - r));
     return len == 64 ? v : (v & ((1ull << len) - 1));
 }
+// up to 32 stream bits from pos, from the 32-bit view of the words: one funnel shift
+__device__ __forceinline__ uint32_t bits32_at(const uint32_t *w, int pos) {
+    const int q = pos >> 5;
+    return __builtin_amdgcn_alignbit(w[q + 1], w[q], (uint32_t)(pos & 31));
+}
+__device__ __forceinline__ int matches32(uint32_t v, uint32_t pat, int len) {
+    return len - __popc((v ^ pat) & (len == 32 ? 0xFFFFFFFFu : ((1u << len) - 1)));
+}
 __device__ __forceinline__ int matches(uint64_t v, uint64_t pat, int len) {
     return len - __popcll((v ^ pat) & ((1ull << len) - 1));
 }
@@ -985,10 +993,15 @@ __device__ __forceinline__ void sync_group(SyncLds &L, int grp, const uint8_t *_
         const int s = cur + lane;
         int kind = -1;
         if (s + 510 <= nbits) {
-            const int ht = matches(bits_at(words, s, 12), W_HEAD, 12) + matches(bits_at(words, s + 500, 10), W_TAIL, 10);
-            const uint64_t t22 = bits_at(words, s + 244, 22);
-            const int mn = ht + matches(t22, W_N, 22), mp = ht + matches(t22, W_P, 22);
-            const int my = ht + matches(bits_at(words, s + 214, 38), W_Y, 38);
+            // 32-bit funnel-shift extractions (words viewed as little-endian dwords: stream bit p is
+            // bit p & 31 of dword p >> 5)
+            const uint32_t *w32 = reinterpret_cast<const uint32_t *>(words);
+            const int ht = matches32(bits32_at(w32, s), (uint32_t)W_HEAD, 12) +
+                           matches32(bits32_at(w32, s + 500), (uint32_t)W_TAIL, 10);
+            const uint32_t t22 = bits32_at(w32, s + 244);
+            const int mn = ht + matches32(t22, (uint32_t)W_N, 22), mp = ht + matches32(t22, (uint32_t)W_P, 22);
+            const int my = ht + matches32(bits32_at(w32, s + 214), (uint32_t)W_Y, 32) +
+                           matches32(bits32_at(w32, s + 246), (uint32_t)(W_Y >> 32), 6);
             if (my >= 54) kind = 2;
             else if (mn >= 40 && mn >= mp) kind = 0;
             else if (mp >= 40) kind = 1;
