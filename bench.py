@@ -55,8 +55,8 @@ def parse():
                     help="etsi: input sample format in HBM (sc16 = the BladeRF wire format, 4 B/sample)")
     ap.add_argument("--pipeline", choices=("auto", "on", "off"), default="auto",
                     help="etsi: overlap the demod of batch k+1 with the lower MAC of batch k on two streams "
-                         "(auto: cf32 on; sc16 off -- its demod fills every CU's LDS, so the back-end "
-                         "kernels cannot co-reside and only slow it down); compat: run consecutive batches' "
+                         "(auto: on for cf32 and sc16 -- sc16 since the lower MAC's traceback kernel: 1.210 -> "
+                         "1.197 ms per step); compat: run consecutive batches' "
                          "whole chains on two streams (auto: on); wideband: channeliser of capture k+1 beside "
                          "the timing + lower MAC of capture k (auto: on)")
     ap.add_argument("--no-pipeline", action="store_true", help="same as --pipeline off")
@@ -257,7 +257,7 @@ def main():
         from tetraear.signal.etsi import BenchStep as EtsiStep
         step = EtsiStep(c, C, N, FS, seed=rank_seed(1000, rank), device=dev, iq_format=a.iq, demod=a.demod)
         pipe = "off" if a.no_pipeline else a.pipeline
-        if pipe == "on" or (pipe == "auto" and a.iq == "cf32"):
+        if pipe != "off":
             step.pipeline()
         if a.host_input:
             step.host_feed()

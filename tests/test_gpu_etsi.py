@@ -157,7 +157,8 @@ def test_full_size_round_trip():
 def test_bench_pipeline_matches_serial():
     """bench.py's step variants give the same per-step results as the single-stream fused chain:
     the two-stream pipeline (front: fused demod, back: lower MAC, double-buffered symbol outputs),
-    the split demod (chanfilt -> y in HBM -> timing) pipelined, and the host-fed (PCIe) mode."""
+    the split demod (chanfilt -> y in HBM -> timing) pipelined, and the host-fed (PCIe) mode; the
+    SC16 pipeline against the SC16 single-stream chain."""
     import torch
     from tetraear import _hip
     from tetraear.signal.etsi import BenchStep
@@ -167,10 +168,12 @@ def test_bench_pipeline_matches_serial():
     # shared thread-local context the other tests use
     c = _hip.Context()
     c.check(c.lib.tetra_set_stream(c.handle, None), "set_stream")
-    outs = []
-    for pipe, demod, host in ((False, "fused", False), (True, "fused", False), (True, "split", False),
-                              (True, "fused", True), (False, "split", True)):
-        st = BenchStep(c, 64, 131072, 2.4e6, seed=11, device=dev, demod=demod)
+    outs = {"cf32": [], "sc16": []}   # SC16 steps compare among themselves (other input)
+    for pipe, demod, host, fmt in ((False, "fused", False, "cf32"), (True, "fused", False, "cf32"),
+                                   (True, "split", False, "cf32"), (True, "fused", True, "cf32"),
+                                   (False, "split", True, "cf32"), (True, "fused", False, "sc16"),
+                                   (False, "fused", False, "sc16")):
+        st = BenchStep(c, 64, 131072, 2.4e6, seed=11, device=dev, demod=demod, iq_format=fmt)
         if pipe:
             st.pipeline()
         if host:
@@ -182,14 +185,15 @@ def test_bench_pipeline_matches_serial():
         nb, bursts, nk, blocks, t1 = st.nburst.cpu(), st.bursts.cpu(), st.nblock.cpu(), st.blocks.cpu(), st.type1.cpu()
         # the written parts only (the buffers are torch.empty: padding differs between instances)
         n1 = {0: 268, 1: 124, 2: 60}   # type-1 bits per block kind (the rest of a type1 row is padding)
-        outs.append([ns, nb, nk] + [x for ch in range(64) for x in (
+        outs[fmt].append([ns, nb, nk] + [x for ch in range(64) for x in (
             soft[ch, :2 * max(int(ns[ch]) - 1, 0)], hard[ch, :max(int(ns[ch]) - 1, 0)], bursts[ch, :int(nb[ch])],
             blocks[ch, :int(nk[ch])])] + [t1[ch, j, :n1[int(blocks[ch, j, 0])]] for ch in range(64)
                                           for j in range(int(nk[ch]))])
         assert st.quality()["crc_ok"] > 64
-    for o in outs[1:]:
-        for a, b in zip(outs[0], o):
-            assert torch.equal(a, b)
+    for group in outs.values():
+        for o in group[1:]:
+            for a, b in zip(group[0], o):
+                assert torch.equal(a, b)
 
 
 def test_sc16_ingest_matches_cf32(synth_small):
