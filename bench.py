@@ -346,6 +346,8 @@ def main():
                 **({"measured_read_floor_GBs": floor, "frac_of_floor": round(achieved / floor, 4)} if floor else {}),
             },
             "stages_ms_per_step": {k: round(v[0] / a.steps, 4) for k, v in prof.items()},
+            # the last step's decoded blocks (read back after the timed region): the chain's work done
+            **({"decoded_last_step": step.quality()} if hasattr(step, "quality") else {}),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
