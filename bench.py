@@ -49,7 +49,7 @@ def parse():
                     help="wideband: 20 MSps samples per rank per step (C3: 0.5 s)")
     ap.add_argument("--channels", type=int, default=8192, help="channels per rank")
     ap.add_argument("--samples", type=int, default=131072, help="samples per channel chunk")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (rank 0)")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline budget (rank 0)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--iq", choices=("cf32", "sc16"), default="cf32",
                     help="etsi: input sample format in HBM (sc16 = the BladeRF wire format, 4 B/sample)")
@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--host-input", action="store_true",
                     help="etsi: PCIe-inclusive mode -- each batch is copied from pinned host memory (double-buffered "
                          "copy stream); value is then the host-fed rate, never the HBM-resident headline")
+    ap.add_argument("--cells", choices=("acquire", "given"), default="acquire",
+                    help="etsi: the lower MAC acquires each channel's cell from its BSCH (colour code 0 first, "
+                         "state kept across steps) or is given the synthesised cells")
     ap.add_argument("--demod", choices=("fused", "split"), default="fused",
                     help="etsi: fused channel filter + timing in one launch, or split (y through HBM, timing "
                          "launched separately -- beside the next batch's channel filter when pipelined)")
@@ -91,8 +94,12 @@ def traffic_from_profiles(kernel, workload_key):
             continue
         k = d.get("kernels", {}).get(kernel, {})
         if workload_key in d.get("workload", "") and "hbm_bytes_per_launch" in k:
-            best = (k["hbm_bytes_per_launch"], os.path.basename(f))
-    return None if best is None else {"bytes": best[0], "source": best[1]}
+            best = (k["hbm_bytes_per_launch"], os.path.basename(f), k.get("timed_avg_ns", k.get("avg_ns")))
+    if best is None:
+        return None
+    # the same summary's rocprof average duration of the kernel (timed launches when recorded), so the
+    # line's live launch_ms can be checked against the committed profile
+    return {"bytes": best[0], "source": best[1], "rocprof_avg_ms": round(best[2] / 1e6, 4) if best[2] else None}
 
 
 def read_profile(c):
@@ -158,6 +165,7 @@ class CompatStep:
             back.check(back.lib.tetra_set_stream(back.handle, ctypes.c_void_p(s.cuda_stream)), "set_stream")
             lane = self._Lane(back, self.C, self.smax, dev)
             lane.stream = s
+            s.wait_stream(torch.cuda.current_stream(dev))   # the lane's inputs are zeroed on the current stream
             self.lanes.append(lane)
         self.pipelined = True
         return self
@@ -194,23 +202,25 @@ class CompatStep:
         # reads each input sample once (8 B); complex64 rows always take the banked forward pass
         return ("compat_sos_fwd", 8.0, "k_sos_fwd_bank")
 
-    def cpu_baseline(self, budget_s):
-        sys.path.insert(0, os.path.join(REPO, "oracle"))
-        sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
-        import compat as oracle   # the CPU restatement (cpu_baseline leg only)
-        import _signals
-        rng = np.random.default_rng(0)
-        chunks = [_signals.family("tetra", rng, self.N, FS)[0] for _ in range(4)]
-        t0 = time.perf_counter()
-        n = 0
-        while time.perf_counter() - t0 < budget_s:
-            p = oracle.SignalProcessor(FS)
-            h = p.process(chunks[n % 4], 0)
-            oracle.decode_frames(h)
-            n += 1
-        dt = time.perf_counter() - t0
-        return dict(value=n * self.N / dt / 1e6, unit="Msamples/s", cores=1, kind="port",
-                    sample=f"{n} chunks x {self.N} cf32 @2.4 MSps, oracle process()+decode lower MAC, 1 thread")
+
+def cpu_baseline(a, step):
+    """BASELINE.md §3 on this box's host cores (tools/cpu_baseline.py -- the checker, timed; never
+    in the timed region): the compat restatement of the reference's process() + decode(), single-core
+    and all-core (worker processes); for the ETSI chain also its C oracle (thread pool) under
+    "etsi_oracle"; for C3 the wideband restatement."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import cpu_baseline as CB
+    if a.chain == "wideband":
+        return CB.wideband_rate(step, a.cpu_seconds)
+    out = CB.compat_rate(a.samples, 0.25 * a.cpu_seconds, 0.4 * a.cpu_seconds)
+    if a.chain == "etsi":
+        x = step.iq[:4].float().cpu().numpy()
+        if step.fmt == _hip.TETRA_SC16:
+            x = x / 32768   # the oracle filters cf32; SC16 -> cf32 is exact
+        x = np.ascontiguousarray(x, np.float32).view(np.complex64)[..., 0]
+        cells = step.cells[:4].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+        out["etsi_oracle"] = CB.etsi_rate(x, cells, 0.35 * a.cpu_seconds)
+    return out
 
 
 def read_floor(c, step, reps=5):
@@ -225,6 +235,27 @@ def read_floor(c, step, reps=5):
     ms, n = read_profile(c).get("read_floor", (0.0, 0))
     c.check(c.lib.tetra_profile(c.handle, 0), "profile")
     return round(rows * row_bytes / (ms / n * 1e-3) / 1e9, 2) if n else None
+
+
+def time_steps(step, steps, warmup, world, sync, on_timed=None):
+    """The driver contract's timing: `warmup` untimed steps, then exactly `steps` steps bracketed by
+    a barrier (N > 1) and a device synchronize on both sides; returns this rank's elapsed seconds
+    (bench takes the max over ranks with max_over_ranks)."""
+    for _ in range(warmup):
+        step()
+    sync()
+    if on_timed is not None:
+        on_timed()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    return time.perf_counter() - t0
 
 
 def main():
@@ -255,7 +286,8 @@ def main():
         C, N = 1, a.wb_samples   # units: wideband samples
     elif a.chain == "etsi":
         from tetraear.signal.etsi import BenchStep as EtsiStep
-        step = EtsiStep(c, C, N, FS, seed=rank_seed(1000, rank), device=dev, iq_format=a.iq, demod=a.demod)
+        step = EtsiStep(c, C, N, FS, seed=rank_seed(1000, rank), device=dev, iq_format=a.iq, demod=a.demod,
+                        cells=a.cells)
         pipe = "off" if a.no_pipeline else a.pipeline
         if pipe != "off":
             step.pipeline()
@@ -272,22 +304,12 @@ def main():
     torch.cuda.synchronize(dev)
     ctxs = step.contexts() if hasattr(step, "contexts") else [c]
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    for x in ctxs:
-        x.check(x.lib.tetra_profile(x.handle, 1), "profile")
-    read_profile(ctxs)   # drop warm-up records
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    def profile_on():
+        for x in ctxs:
+            x.check(x.lib.tetra_profile(x.handle, 1), "profile")
+        read_profile(ctxs)   # drop warm-up records
+
+    elapsed = time_steps(step, a.steps, a.warmup, world, lambda: torch.cuda.synchronize(dev), profile_on)
     prof = read_profile(ctxs)
     for x in ctxs:
         x.check(x.lib.tetra_profile(x.handle, 0), "profile")
@@ -308,7 +330,7 @@ def main():
         units_per_launch = C * N
         achieved = per_sample * units_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
         floor = read_floor(c, step) if hasattr(step, "floor_args") else None
-        cpu = None if a.no_cpu else step.cpu_baseline(a.cpu_seconds)
+        cpu = None if a.no_cpu else cpu_baseline(a, step)
         out = {
             "metric": "IQ Msamples/s demod+Viterbi; real-time 25 kHz TETRA channels @1/2/4/8 GPU",
             "value": round(value, 3),
@@ -331,6 +353,7 @@ def main():
                 **({"input": "host-fed over PCIe (pinned, double-buffered copy stream)"}
                    if getattr(step, "hostfed", False) else {}),
                 **({"demod": step.demod_mode} if hasattr(step, "demod_mode") else {}),
+                **({"cells": step.cells_mode} if hasattr(step, "cells_mode") else {}),
             },
             "realtime_channels": int(step.realtime_channels(value) if hasattr(step, "realtime_channels")
                                      else value * 1e6 / FS),

@@ -177,7 +177,8 @@ int tetra_crc16(tetra_ctx *ctx, const uint8_t *bits, size_t F, size_t L, int rev
 int tetra_check_crc(tetra_ctx *ctx, const uint8_t *bits, size_t F, size_t L, uint8_t *ok);
 
 /* MAC PDU header extraction of TetraProtocolParser.parse_mac_pdu (protocol.py:349-596; SURVEY.md
- * §8f rank 4) over F frames of data bits (0/1), one row of `stride` bytes each, nbits[f] valid.
+ * §8f rank 4) over F frames of data bits, one byte per bit (any nonzero byte reads as 1, in the
+ * header fields and the data bytes alike), one row of `stride` bytes each, nbits[f] valid.
  * Stateless per frame: the fragment buffer, the MCC/MNC/colour-code state and the statistics are
  * applied in order by the host (tetraear.core.protocol.parse_mac_pdu_batch).
  *   fields [F][TETRA_MAC_FIELDS] (below); data [F][data_stride] = BitArray(data bits).tobytes()
@@ -244,6 +245,15 @@ int tetra_etsi_chanfilt_fmt(tetra_ctx *ctx, const tetra_etsi_plan *plan, const v
 int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *plan, const void *iq, int iq_fmt, size_t C,
                          size_t N, void *soft, int8_t *softbits, uint8_t *hard, int32_t *nsym, size_t smax,
                          float *diag);
+/* Differential decision on n given symbol-spaced samples x (TETRA_CF32 / TETRA_CF64): hard [n-1]
+ * dibits by EN 300 392-2 Table 5.1 (the fused demod's decision, no CFO rotation).  Replaces the
+ * reference's demodulate_dqpsk (/root/reference/tetraear/signal/processor.py:102-166) in ETSI mode,
+ * whose shifted decision regions SURVEY.md §0.3 documents. */
+int tetra_etsi_decide(tetra_ctx *ctx, const void *x, int iq_fmt, size_t n, uint8_t *hard);
+/* The channel-filter kernel a demod (fused != 0) or chanfilt call on N-sample rows of iq_fmt runs:
+ * its symbol name and static LDS bytes per workgroup (the occupancy the bench's read floor mimics). */
+int tetra_etsi_kernel_info(tetra_ctx *ctx, const tetra_etsi_plan *plan, int iq_fmt, size_t N, int fused, char *name,
+                           size_t name_len, int64_t *lds_bytes);
 /* Cell configuration: scrambling code init per channel ((MCC<<20|MNC<<6|CC)<<2|3). */
 int tetra_etsi_set_cells(tetra_ctx *ctx, const uint32_t *scramb_init, size_t C);
 /* Lower MAC: burst sync + descramble + deinterleave + depuncture + Viterbi + CRC per channel.
@@ -253,6 +263,20 @@ int tetra_etsi_set_cells(tetra_ctx *ctx, const uint32_t *scramb_init, size_t C);
 int tetra_lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard, const int32_t *nsym,
                     size_t C, size_t smax, int32_t *nburst, int32_t *bursts, int32_t *nblock,
                     int32_t *blocks, uint8_t *type1);
+/* Lower MAC with cell acquisition: the same outputs as tetra_lmac_etsi, without a configured cell.
+ * cell_init [C] (in/out, host or device) holds each channel's scrambling init before the chunk
+ * (3 = colour code 0 / not yet acquired).  The chunk's BSCH blocks are decoded first (colour code
+ * 0, as every receiver must before it knows the cell); the last CRC-good one sets the channel's
+ * extended colour code from its type-1 bits -- MAC-SYNC colour code bits 4..9, D-MLE-SYNC MCC bits
+ * 31..40 and MNC bits 41..54 (EN 300 392-2 §21.4.4.2, §18.4.2.1) -- and the SCH/F / SCH/HD blocks
+ * are then descrambled with it (§8.2.5.2).  cell_init returns the updated inits, so a stream of
+ * chunks keeps the cell it acquired, as the reference parser keeps the MCC/MNC/colour code it
+ * reads from a SYSINFO broadcast (/root/reference/tetraear/core/protocol.py:479-485).  The
+ * scrambling table is cached per channel in the context and regenerated on the device only for
+ * channels whose init changed. */
+int tetra_lmac_etsi_acquire(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard, const int32_t *nsym,
+                            size_t C, size_t smax, uint32_t *cell_init, int32_t *nburst, int32_t *bursts,
+                            int32_t *nblock, int32_t *blocks, uint8_t *type1);
 /* Component: decode F type-5 soft blocks of one kind (K = 432/216/120): type1 [F][n1], crc_ok [F]. */
 int tetra_etsi_decode_blocks(tetra_ctx *ctx, const int8_t *soft5, size_t F, int kind,
                              const uint32_t *scramb_init, uint8_t *type1, uint8_t *crc_ok);
@@ -263,7 +287,8 @@ int tetra_etsi_encode_blocks(tetra_ctx *ctx, const uint8_t *type1, size_t F, int
 /* Synthetic capture generator (device side; bench.py and tests).  Per channel: a continuous
  * downlink of coded bursts (1/2 normal-n, 1/4 normal-p, 1/4 sync), pi/4-DQPSK + RRC(0.35) at fs,
  * random carrier phase, CFO uniform in [-cfo_max, cfo_max] Hz, AWGN at Es/N0 = snr_db (no noise if
- * snr_db >= 200), SC16 quantisation.  Outputs: iq [C][N] cf32, cell_init [C] scrambling inits,
+ * snr_db >= 200), SC16 quantisation.  Each sync burst's BSCH carries a SYNC PDU of the channel's
+ * cell (colour code at type-1 bits 4..9, MCC 31..40, MNC 41..54, the rest random).  Outputs: iq [C][N] cf32, cell_init [C] scrambling inits,
  * and optionally kinds [C][NB] burst kinds, payload [C][NB][2][268] type-1 bits (zero-padded),
  * t0 [C] symbol time of sample 0; NB = tetra_synth_bursts_per_channel(N, fs). */
 int tetra_synth_bursts_per_channel(size_t N, double fs);

@@ -336,3 +336,48 @@ def decode_frames(symbols):
                      enc_mode=int(fb[2] * 2 + fb[3]))
         frames.append(f)
     return frames
+
+
+_ENC_MODES = {1: ("TEA1", "Class 2 (SCK)"), 2: ("TEA2", "Class 3 (DCK)"), 3: ("TEA3", "Reserved")}
+_PDU_NAMES = {0: "MAC_RESOURCE", 1: "MAC_FRAG", 2: "MAC_END", 3: "MAC_BROADCAST"}
+
+
+def decode_with_mac(symbols, mac_parser=None):
+    """decode() through decode_frame's MAC PDU stage (decoder.py:835-888, 890-1100) with the
+    oracle's parse_mac_pdu (oracle/mac.py): [dict(number, header, burst_crc, encrypted,
+    encryption_algorithm, encryption_mode, mac_pdu)] of the frames the reference keeps.
+
+    decoder.py:1093-1095: no MAC PDU and a failed CRC drops the frame.  decoder.py:1008-1053: a PDU
+    settles 'encrypted' / 'encryption_algorithm' from its mode, or by the data-entropy rule."""
+    from mac import MacParser
+    mp = mac_parser if mac_parser is not None else MacParser()
+    out = []
+    for f in decode_frames(symbols):
+        if f["nbits"] < 510:
+            continue
+        enc = f["enc_mode"]
+        alg, mode_txt = _ENC_MODES.get(enc, (None, None))
+        d = dict(number=f["number"], header=f["header"], burst_crc=bool(f["crc_ok"]), encrypted=enc > 0,
+                 encryption_algorithm=alg, encryption_mode=mode_txt, mac_pdu=None)
+        pdu = mp.parse(f["data"])
+        if pdu is None:
+            if not f["crc_ok"]:
+                continue
+            out.append(d)
+            continue
+        d["mac_pdu"] = dict(type=_PDU_NAMES[pdu["pdu_type"]], encrypted=bool(pdu["encrypted"]),
+                            address=pdu["address"], length=pdu["length"], data=bytes(pdu["data"]).hex())
+        if pdu["encrypted"]:
+            d["encrypted"] = True
+            if pdu["encryption_mode"] in _ENC_MODES:
+                d["encryption_algorithm"], d["encryption_mode"] = _ENC_MODES[pdu["encryption_mode"]]
+            elif not d["encryption_algorithm"]:
+                d["encryption_algorithm"] = "TEA1"
+        else:
+            data = bytes(pdu["data"])
+            if len(data) > 0 and len(set(data)) / max(len(data), 1) > 0.7 and len(data) > 8:
+                d["encrypted"] = True
+            else:
+                d["encrypted"], d["encryption_algorithm"] = False, None
+        out.append(d)
+    return out

@@ -56,6 +56,7 @@ def lib():
         L.eo_timing.restype = ctypes.c_int
         L.eo_sync.argtypes = [u8p, ctypes.c_int, i32p, i32p, ctypes.c_int]
         L.eo_sync.restype = ctypes.c_int
+        L.eo_decide.argtypes = [f32p, ctypes.c_int, u8p]
         _bound = True
     return L
 
@@ -179,6 +180,19 @@ def modulate(bits, n, fs=FS_NOMINAL, t0=0.0, phase0=0.0, cfo=0.0, snr_db=None, r
     return x.astype(np.complex64)
 
 
+def bsch_cell_init(type1):
+    """Scrambling init of the cell a decoded BSCH announces: extended colour code = MCC (type-1 bits
+    31..40) | MNC (41..54) | colour code (4..9) (EN 300 392-2 §21.4.4.2 MAC-SYNC, §18.4.2.1
+    D-MLE-SYNC), init = (ecc << 2) | 3 (§8.2.5.2)."""
+    t = [int(v) & 1 for v in type1]
+    cc = mm = 0
+    for v in t[4:10]:
+        cc = (cc << 1) | v
+    for v in t[31:55]:
+        mm = (mm << 1) | v
+    return (((mm << 6) | cc) << 2) | 3
+
+
 # ------------------------------------------------------------------------------ receiver
 
 class Receiver:
@@ -212,6 +226,16 @@ class Receiver:
 
     def demod(self, x):
         return self.timing(self.chanfilt(x))
+
+    @staticmethod
+    def decide(symbols):
+        """Table 5.1 differential decision on given symbols (eo_decide): uint8 [n-1]."""
+        x = np.ascontiguousarray(np.asarray(symbols, np.complex64)).view(np.float32)
+        n = len(x) // 2
+        out = np.zeros(max(n - 1, 0), np.uint8)
+        if n >= 2:
+            lib().eo_decide(x, n, out)
+        return out
 
     @staticmethod
     def hard_bits(hard):
@@ -252,3 +276,17 @@ class Receiver:
             dec = [(k,) + self.decode_block(v, k, scr) for k, v, scr in blocks]
             out.append((s, bk, dec))
         return out
+
+    def lower_mac_acquire(self, softbits, hard, cell_init):
+        """Cell acquisition: the chunk's BSCH blocks first (colour code 0); the last CRC-good one
+        sets the cell, with which every SCH block of the chunk is then decoded.  Returns
+        (lower_mac result, cell init after the chunk)."""
+        sb = np.asarray(softbits, np.int8)
+        bsch = scramble_seq(3, 120)
+        init = int(cell_init)
+        for s, bk in self.sync(hard):
+            if bk == BURST_SB:
+                t, ok = self.decode_block(sb[s + 94:s + 214], 2, bsch)
+                if ok:
+                    init = bsch_cell_init(t)
+        return self.lower_mac(softbits, hard, init), init

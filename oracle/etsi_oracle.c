@@ -420,3 +420,15 @@ int eo_sync(const uint8_t *bits, int nbits, int *starts, int *kinds, int maxb)
     }
     return nb;
 }
+
+/* Differential decision on given symbol-spaced samples (interleaved re/im, n samples): hard[n-1]
+ * dibits per EN 300 392-2 Table 5.1, d = x[k] conj(x[k-1]), (Im d < 0, Re d < 0) -- the decision of
+ * eo_timing without its CFO rotation. */
+void eo_decide(const float *x, int n, uint8_t *hard)
+{
+    for (int k = 1; k < n; ++k) {
+        float ar = x[2 * k], ai = x[2 * k + 1], br = x[2 * k - 2], bi = x[2 * k - 1];
+        float dr = fmaf(ar, br, ai * bi), di = fmaf(ai, br, -(ar * bi));
+        hard[k - 1] = (uint8_t)(((di < 0.0f) << 1) | (dr < 0.0f));
+    }
+}

@@ -40,3 +40,17 @@ def g2():
 @pytest.fixture(scope="session")
 def g3():
     return np.load(os.path.join(GOLDEN, "g3_burst.npz"))
+
+
+def decoded_view(frame):
+    """The fields of one decode() frame dict the golden g2 'decoded' records compare on: the
+    lower-MAC fields and the MAC PDU stage (decoder.py:960-1053)."""
+    info = frame.get("additional_info", {})
+    mp = frame.get("mac_pdu")
+    if mp is not None and not isinstance(mp.get("data"), str):
+        mp = dict(type=mp["type"], encrypted=bool(mp["encrypted"]),
+                  address=None if mp["address"] is None else int(mp["address"]),
+                  length=int(mp["length"]), data=bytes(mp["data"]).hex())
+    return dict(number=frame["number"], header=frame["header"], burst_crc=frame.get("burst_crc"),
+                encrypted=bool(frame["encrypted"]), encryption_algorithm=frame["encryption_algorithm"],
+                encryption_mode=frame.get("encryption_mode", info.get("encryption_mode")), mac_pdu=mp)

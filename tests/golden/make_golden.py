@@ -159,6 +159,110 @@ def crafted_streams(rng):
     return streams
 
 
+def _bits_of(v, n):
+    return [(v >> (n - 1 - i)) & 1 for i in range(n)]
+
+
+def _crc_fix(parser, frame, free):
+    """Set frame bits `free` so the normal-burst data (frame[0:108] + frame[122:230]) carries a
+    valid CRC-16 in its last 16 bits although frame[216:230] is the training sequence.  The CRC is
+    affine over GF(2), so this is a small linear solve (uses the reference's own _calculate_crc16)."""
+    def residue(f):
+        d = np.concatenate([f[0:108], f[122:230]])
+        return (np.asarray(parser._calculate_crc16(d[:-16])) ^ d[-16:])[2:]   # bits 2..15: TS-bound
+    f0 = frame.copy()
+    f0[free] = 0
+    r0 = residue(f0)
+    cols = []
+    for j in free:
+        f1 = f0.copy()
+        f1[j] = 1
+        cols.append(residue(f1) ^ r0)
+    A = np.array(cols, np.uint8).T          # 14 x len(free)
+    aug = np.concatenate([A, r0[:, None]], axis=1)
+    rows, piv = aug.shape[0], []
+    r = 0
+    for c in range(A.shape[1]):
+        p = next((i for i in range(r, rows) if aug[i, c]), None)
+        if p is None:
+            continue
+        aug[[r, p]] = aug[[p, r]]
+        for i in range(rows):
+            if i != r and aug[i, c]:
+                aug[i] ^= aug[r]
+        piv.append(c)
+        r += 1
+        if r == rows:
+            break
+    x = np.zeros(len(free), np.uint8)
+    for i, c in enumerate(piv):
+        x[c] = aug[i, -1]
+    f0[free] = x
+    d = np.concatenate([f0[0:108], f0[122:230]])
+    f0[214:216] = np.asarray(parser._calculate_crc16(d[:-16]))[0:2]
+    return f0
+
+
+def mac_streams(rng):
+    """Burst-aligned symbol streams whose slots carry MAC PDU headers (decode_frame's MAC stage,
+    decoder.py:994-1100): RESOURCE / FRAG / END / BROADCAST (SYSINFO with valid and invalid
+    MCC/MNC), clear and encrypted modes, low- and high-entropy payloads, CRC-good and CRC-bad slots
+    and synchronisation bursts (whole 510-bit data, protocol.py:249-290)."""
+    parser = TetraProtocolParser()
+    streams = []
+    for s in range(24):
+        nfr = int(rng.integers(2, 9))
+        frames = []
+        for k in range(nfr):
+            f = rng.integers(0, 2, 510).astype(np.uint8)
+            pti = int(rng.integers(0, 4))
+            mode = int(rng.choice([0, 0, 1, 2, 3]))
+            hdr = _bits_of(pti, 2) + _bits_of(mode, 2)
+            if pti == 0:     # RESOURCE: fill(1) address(24) length(6)
+                hdr += [int(rng.integers(0, 2))] + _bits_of(int(rng.integers(0, 1 << 24)), 24)
+                hdr += _bits_of(int(rng.choice([0, 3, 9, 20, 22, 23, int(rng.integers(0, 64))])), 6)
+            elif pti == 3:   # END: fill(1) length(6)
+                hdr += [int(rng.integers(0, 2))] + _bits_of(int(rng.choice([0, 5, 12, 25, 26, 27, 40])), 6)
+            elif pti == 2 and rng.random() < 0.7:   # BROADCAST SYSINFO: MCC(10) MNC(14) CC(6)
+                hdr[2:4] = [0, 0]
+                mcc = int(rng.choice([int(rng.integers(200, 800)), int(rng.integers(0, 200))]))
+                mnc = int(rng.choice([int(rng.integers(0, 1000)), int(rng.integers(1000, 16384))]))
+                hdr += _bits_of(mcc, 10) + _bits_of(mnc, 14) + _bits_of(int(rng.integers(0, 64)), 6)
+            f[:len(hdr)] = hdr
+            ent = rng.random()
+            if ent < 0.35:   # low-entropy payload: a repeated byte pattern after the header
+                f[48:108] = np.tile(np.array(_bits_of(int(rng.integers(0, 256)), 8), np.uint8), 8)[:60]
+                f[122:200] = np.tile(np.array(_bits_of(int(rng.integers(0, 256)), 8), np.uint8), 10)[:78]
+            f[216:238] = _signals.TS_N if rng.random() < 0.7 else _signals.TS_P
+            kind = rng.random()
+            if kind < 0.15:    # synchronisation burst: sync pattern at bits 255:277, CRC over 494 bits
+                f[255:277] = parser.SYNC_CONTINUOUS_DOWNLINK if rng.random() < 0.5 else \
+                    parser.SYNC_DISCONTINUOUS_DOWNLINK
+                f[494:510] = np.asarray(parser._calculate_crc16(f[:494]))
+                if rng.random() < 0.3:
+                    f[int(rng.integers(300, 494))] ^= 1
+                    f[int(rng.integers(300, 494))] ^= 1
+                    f[int(rng.integers(300, 494))] ^= 1
+            else:
+                f[255:277] = 0 if rng.random() < 0.5 else 1    # keep normal-burst detection
+                if kind < 0.75:   # CRC-good normal burst (0-2 bit errors stay good)
+                    f = _crc_fix(parser, f, list(range(150, 200)))
+                    for _ in range(int(rng.integers(0, 3))):
+                        f[int(rng.integers(60, 100))] ^= 1
+            frames.append(f)
+        bits = np.concatenate(frames + [rng.integers(0, 2, 2 * int(rng.integers(0, 40))).astype(np.uint8)])
+        streams.append((bits[0::2] << 1 | bits[1::2]).astype(np.uint8))
+    return streams
+
+
+def _mac_dict(m):
+    if m is None:
+        return None
+    return dict(type=m["type"], encrypted=bool(m["encrypted"]),
+                address=None if m["address"] is None else int(m["address"]),
+                length=int(m["length"]), data=bytes(m["data"]).hex())
+
+
 def decode_record(dec, sym):
     """decode() with its internal cascade exposed (decoder.py:835-888)."""
     rec = {}
@@ -197,7 +301,12 @@ def decode_record(dec, sym):
     rec["frames"] = frames
     out = dec.decode(sym)
     rec["decoded"] = [dict(number=f["number"], timeslot=f["timeslot"], type=f["type"], header=f["header"],
-                           position=f["position"], burst_crc=f.get("burst_crc")) for f in out]
+                           position=f["position"], burst_crc=f.get("burst_crc"),
+                           encrypted=bool(f["encrypted"]), encryption_algorithm=f["encryption_algorithm"],
+                           additional_info=dict(f["additional_info"]), mac_pdu=_mac_dict(f.get("mac_pdu")),
+                           upper_keys=sorted(k for k in f if k in ("call_metadata", "sds_message", "decoded_text",
+                                                                    "is_reassembled")))
+                      for f in out]
     rec["stats"] = dict(dec.protocol_parser.stats)
     return rec
 
@@ -208,6 +317,7 @@ def g2(g1_arrays, g1_meta):
     for i, m in enumerate(g1_meta):
         if len(g1_arrays[f"c{i}_hard"]) >= 255:
             streams.append(g1_arrays[f"c{i}_hard"])
+    streams += mac_streams(np.random.default_rng(20261017))   # round 3: decode_frame's MAC stage
     arrays = {}
     recs = []
     for i, sym in enumerate(streams):

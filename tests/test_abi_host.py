@@ -92,3 +92,42 @@ def test_compat_plan_decisions(g1):
         # filter applied <=> filtered dtype is complex128 for an unshifted chunk
         if f"c{i}_filtered" in z.files and not m["freq_offset"]:
             assert bool(p.filt) == (z[f"c{i}_filtered"].dtype == np.complex128), (i, m)
+
+
+def test_mode_selection_from_environment(monkeypatch):
+    """TETRAEAR_DEMOD picks the chain for callers that construct SignalProcessor / TetraDecoder as
+    the reference's GUI and scanner do (modern.py:1886-1887, scanner.py:164-172); an explicit mode=
+    wins; TETRAEAR_BACKEND other than hip is refused (no CPU path in this build)."""
+    from tetraear import _hip
+    from tetraear.signal import SignalProcessor
+    from tetraear.core import TetraDecoder
+    monkeypatch.delenv("TETRAEAR_DEMOD", raising=False)
+    assert SignalProcessor(sample_rate=2.4e6).mode == "compat"
+    assert TetraDecoder(auto_decrypt=False).mode == "compat"
+    monkeypatch.setenv("TETRAEAR_DEMOD", "etsi")
+    assert SignalProcessor(sample_rate=2.4e6).mode == "etsi"
+    assert TetraDecoder(auto_decrypt=False).mode == "etsi"
+    assert SignalProcessor(2.4e6, mode="compat").mode == "compat"
+    monkeypatch.setenv("TETRAEAR_DEMOD", "fast")
+    with pytest.raises(ValueError):
+        SignalProcessor()
+    monkeypatch.setenv("TETRAEAR_DEMOD", "compat")
+    monkeypatch.setenv("TETRAEAR_BACKEND", "cpu")
+    with pytest.raises(_hip.TetraHipError):
+        TetraDecoder()
+
+
+def test_mac_batch_rejects_bad_frames_after_applying_earlier_ones(monkeypatch):
+    """parse_mac_pdu_batch: a frame that is not integer 0/1 (bool arrays included, which the
+    reference's int(..., 2) rejects) raises ValueError after the frames before it were applied."""
+    from tetraear.core.protocol import TetraProtocolParser
+    p = TetraProtocolParser()
+    seen = []
+    monkeypatch.setattr(TetraProtocolParser, "_mac_batch", lambda self, rows: seen.append(len(rows)) or [])
+    good = np.zeros(40, np.int64)
+    with pytest.raises(ValueError):
+        p.parse_mac_pdu_batch([good, good, np.zeros(40, bool), good])
+    with pytest.raises(ValueError):
+        p.parse_mac_pdu_batch([good, np.full(40, 2)])
+    assert seen == [2, 1]
+    assert p.parse_mac_pdu_batch([np.zeros(5, bool)]) == []   # < 8 bits: None without a check

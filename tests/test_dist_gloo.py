@@ -1,7 +1,9 @@
-"""N>1 path on CPU: world_size-2 gloo processes shard channels and reduce timing like bench.py.
+"""N>1 path on CPU: world_size-2 gloo processes run bench.py's own distributed code.
 
-Each rank runs its channel block through the CPU oracle (no GPU here); the gathered results must
-equal a single-process run over all channels, and max-over-ranks must be the slowest rank's time."""
+Each rank imports bench.py and uses its seeding (rank_seed), its timing (time_steps: warm-up,
+barrier-bracketed timed steps), its max-over-ranks reduction and its whole-job aggregate, with a
+CPU step in place of the GPU chain (no GPU here).  A second test shards channels (rank_channels)
+through the oracle and checks the gathered results against a single-process run."""
 import os
 import socket
 
@@ -44,6 +46,54 @@ def _worker(rank, world, port, total, q):
         q.put((merged, mx, aggregate_msps(count * 4000, world, 1, mx)))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _bench_worker(rank, world, port, q):
+    import sys
+    import time
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [repo, os.path.join(repo, "tetraear-bladerf_amd"), os.path.join(repo, "oracle")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    import bench
+    import compat as oracle
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    seed = bench.rank_seed(1000, rank)            # the bench's per-rank data seed
+    rng = np.random.default_rng(seed)
+    x = (0.3 * (rng.standard_normal(8000) + 1j * rng.standard_normal(8000))).astype(np.complex64)
+    done = []
+
+    def step():                                   # one "step": this rank's batch through the chain
+        done.append(oracle.SignalProcessor(2.4e6).process(x, 0))
+        time.sleep(0.05 * (rank + 1))             # rank 1 is the slower one
+
+    elapsed = bench.time_steps(step, 3, 2, world, lambda: None)
+    mx = bench.max_over_ranks(elapsed)            # bench's reduction (host tensor on gloo)
+    value = bench.aggregate_msps(8000, world, 3, mx)
+    allv = [None] * world
+    dist.all_gather_object(allv, (seed, elapsed, len(done), done[-1].tolist()))
+    if rank == 0:
+        q.put((allv, mx, value))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_runs_bench_timing_and_aggregate():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_bench_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    allv, mx, value = q.get(timeout=180)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (s0, e0, n0, h0), (s1, e1, n1, h1) = allv
+    assert s0 != s1 and h0 != h1                  # each rank works on its own data
+    assert n0 == n1 == 5                          # warm-up 2 + timed 3 steps on every rank
+    assert mx == max(e0, e1) and e1 >= 3 * 0.1    # the slowest rank's time
+    assert abs(value - 2 * 3 * 8000 / mx / 1e6) < 1e-12   # whole-job: both ranks' samples / max time
 
 
 def test_rank_channels_partition():

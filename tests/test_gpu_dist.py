@@ -1,0 +1,46 @@
+"""bench.py's N>1 path on the GPU box, launched the way the driver launches it (torchrun, one rank
+per GPU), as a fresh child process.  A one-GPU box runs both ranks on its card with
+TETRA_BENCH_DIST=gloo (rank -> LOCAL_RANK mod device count, the timing reduction on a host tensor);
+the driver's 8-GPU run takes the same code path with RCCL.  SURVEY.md §8e: channels are independent
+shards, weak scaling, no data-path collective."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_torchrun_two_ranks_bench():
+    C, N, steps = 256, 131072, 3
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO, "bench.py"), "--gpus", "2", "--channels", str(C), "--samples", str(N),
+           "--steps", str(steps), "--warmup", "1", "--no-cpu", "--cells", "given"]
+    env = dict(os.environ, TETRA_BENCH_DIST="gloo", OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-2000:]          # rank 0 prints the one line
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["steps"] == steps and d["scaling"] == "weak"
+    assert d["config"]["channels_per_gpu"] == C
+    q = d["decoded_last_step"]
+    assert q["blocks"] >= 3 * C and q["crc_ok"] == q["blocks"], q   # every decoded block CRC-good
+    # whole-job aggregate = both ranks' samples / the slowest rank's time
+    elapsed = d["ms_per_step"] * steps / 1e3
+    want = 2 * C * N * steps / elapsed / 1e6
+    assert abs(d["value"] - want) <= 1e-3 * want, (d["value"], want)

@@ -116,21 +116,140 @@ def test_block_codec_vs_oracle(kind):
 
 
 def test_process_and_decode_surface():
-    """SignalProcessor(mode='etsi').process -> TetraDecoder(mode='etsi').decode round trip."""
+    """SignalProcessor(mode='etsi').process -> TetraDecoder(mode='etsi').decode round trip with no
+    cell configured: four consecutive chunks of one capture through one decoder, which acquires the
+    cell from a BSCH and keeps it.  Frames carry the reference's frame-dict keys."""
     from tetraear.signal import SignalProcessor
     from tetraear.core import TetraDecoder
     from tetraear.signal.etsi import synth
-    iq, cells, kinds, payload, t0 = synth(1, 131072, seed=11, snr_db=20.0, cfo_max=300.0)
+    iq, cells, kinds, payload, t0 = synth(1, 4 * 131072, seed=11, snr_db=20.0, cfo_max=300.0)
     p = SignalProcessor(2.4e6, mode="etsi")
-    hard = p.process(iq[0])
-    assert hard.dtype == np.uint8 and len(p.symbols) == len(hard) + 1
     d = TetraDecoder(mode="etsi")
-    d._etsi_rx().cell = int(cells[0])
-    frames = d.decode(hard)
-    oks = [b for f in frames for b in f["blocks"] if b["crc_ok"]]
-    assert len(oks) >= 2
-    sent = {tuple(p) for bb in payload[0] for p in bb}
+    sent = {tuple(x) for bb in payload[0] for x in bb}
+    oks = []
+    for k in range(4):
+        hard = p.process(iq[0, k * 131072:(k + 1) * 131072])
+        assert hard.dtype == np.uint8 and len(p.symbols) == len(hard) + 1
+        frames = d.decode(hard)
+        for f in frames:
+            for key in ("type", "type_name", "number", "timeslot", "bits", "header", "position", "encrypted",
+                        "encryption_algorithm", "key_id", "additional_info", "burst_crc"):
+                assert key in f, key
+        oks += [b for f in frames for b in f["blocks"] if b["crc_ok"]]
+    assert len(oks) >= 4
     assert all(tuple(np.pad(b["bits"], (0, 268 - len(b["bits"])))) in sent for b in oks)
+    from tetraear.core.etsi import cell_of
+    assert (d._etsi.mcc, d._etsi.mnc, d._etsi.colour_code) == cell_of(int(cells[0]))
+
+
+def test_cell_acquisition_vs_oracle(synth_small):
+    """tetra_lmac_etsi_acquire (no cell given): BSCH first with colour code 0, the cell from the
+    last CRC-good SYNC PDU, then SCH/F + SCH/HD with it -- block for block equal to the oracle's
+    restatement (etsi.Receiver.lower_mac_acquire), the acquired inits equal to the oracle's, and
+    to the synthesised cell wherever a BSCH decoded."""
+    from tetraear.signal.etsi import EtsiReceiver
+    from tetraear.core.etsi import EtsiLowerMac, UNKNOWN_CELL
+    iq, cells, kinds, payload, t0 = synth_small
+    hard, soft, sym, ns = EtsiReceiver().demod_batch(iq)
+    lm = EtsiLowerMac()
+    res = lm.decode_batch(soft, hard, ns)
+    rx = E.Receiver()
+    nacq = nok = 0
+    for ch in range(len(iq)):
+        n = int(ns[ch])
+        want, init = rx.lower_mac_acquire(soft[ch, :2 * (n - 1)], hard[ch, :n - 1], UNKNOWN_CELL)
+        assert int(lm.cell_state[ch]) == init, ch
+        if init != UNKNOWN_CELL:
+            nacq += 1
+            assert init == int(cells[ch]), ch
+        got = res[ch]
+        assert [(f["position"], f["burst_kind"]) for f in got] == [(s, k) for s, k, _ in want], ch
+        for f, (_, _, dec) in zip(got, want):
+            for b, (kind, bits, ok) in zip(f["blocks"], dec):
+                assert b["crc_ok"] == ok and np.array_equal(b["bits"], bits), ch
+                nok += ok
+    assert nacq >= 2 and nok >= 12
+
+
+def test_cell_acquisition_stream():
+    """A 4-chunk capture per channel decoded chunk by chunk with no cell configured: the cell is
+    acquired from the first CRC-good BSCH and kept by the next chunks; every acquired cell is the
+    transmitted one; >= 97 % of the blocks of chunks decoded with the cell known pass the CRC; the
+    oracle's restatement carried across the same chunks gives the same inits and blocks."""
+    from tetraear.signal.etsi import synth, EtsiReceiver
+    from tetraear.core.etsi import EtsiLowerMac, UNKNOWN_CELL
+    C, L, K = 48, 131072, 4
+    iq, cells, kinds, payload, t0 = synth(C, K * L, seed=23, snr_db=18.0, cfo_max=600.0)
+    rx, lm, orc = EtsiReceiver(), EtsiLowerMac(), E.Receiver()
+    state = [UNKNOWN_CELL] * C
+    nblk = nok = 0
+    for k in range(K):
+        hard, soft, sym, ns = rx.demod_batch(iq[:, k * L:(k + 1) * L])
+        known_before = np.array([int(v) != UNKNOWN_CELL for v in lm.cell_state]) if lm.cell_state is not None \
+            else np.zeros(C, bool)
+        res = lm.decode_batch(soft, hard, ns)
+        for ch in range(C):
+            n = int(ns[ch])
+            want, state[ch] = orc.lower_mac_acquire(soft[ch, :2 * (n - 1)], hard[ch, :n - 1], state[ch])
+            assert int(lm.cell_state[ch]) == state[ch], (k, ch)
+            if state[ch] != UNKNOWN_CELL:
+                assert state[ch] == int(cells[ch]), (k, ch)
+            if ch % 8 == 0:
+                assert [[(b["crc_ok"], tuple(b["bits"])) for b in f["blocks"]] for f in res[ch]] == \
+                    [[(bool(ok), tuple(bits)) for _, bits, ok in dec] for _, _, dec in want], (k, ch)
+            if known_before[ch] or state[ch] != UNKNOWN_CELL:
+                for f in res[ch]:
+                    for b in f["blocks"]:
+                        nblk += 1
+                        nok += b["crc_ok"]
+    acquired = sum(int(v) != UNKNOWN_CELL for v in lm.cell_state)
+    assert acquired >= 0.85 * C, acquired
+    assert nok / nblk >= 0.97, (nok, nblk)
+
+
+def test_etsi_surface_methods():
+    """ETSI mode's component methods: demodulate_dqpsk = Table 5.1 decisions on given symbols
+    (ideal constellation walk decoded exactly; bit-identical to the oracle's eo_decide on the
+    receiver's symbols); filter_signal / extract_symbols = the channel filter and timing stages,
+    whose composition is process()."""
+    from tetraear.signal import SignalProcessor
+    from tetraear.signal.etsi import synth
+    p = SignalProcessor(2.4e6, mode="etsi")
+    rng = np.random.default_rng(4)
+    bits = rng.integers(0, 2, 2 * 999)
+    steps = np.where(bits[0::2] == 0, np.where(bits[1::2] == 0, 1, 3), np.where(bits[1::2] == 0, -1, -3))
+    x = np.exp(1j * (0.3 + np.pi / 4 * np.concatenate([[0], np.cumsum(steps)]))).astype(np.complex64)
+    want = (bits[0::2] * 2 + bits[1::2]).astype(np.uint8)
+    assert np.array_equal(p.demodulate_dqpsk(x), want)
+    assert np.array_equal(p.demodulate_dqpsk(x.astype(np.complex128)), want)
+    assert len(p.demodulate_dqpsk(x[:1])) == 0
+    iq = synth(1, 131072, seed=13, snr_db=15.0)[0][0]
+    hard = p.process(iq)
+    sym = p.symbols
+    assert np.array_equal(p.demodulate_dqpsk(sym), E.Receiver.decide(sym))
+    assert np.mean(p.demodulate_dqpsk(sym) == hard) > 0.9   # the fused decision also corrects the CFO
+    y = p.filter_signal(iq)
+    assert np.array_equal(y, E.Receiver().chanfilt(iq))
+    assert np.array_equal(p.extract_symbols(y), sym)
+    assert np.array_equal(p.extract_symbols(iq, sample_rate=2.4e6), sym)
+
+
+def test_env_selects_etsi_chain(monkeypatch):
+    """TETRAEAR_DEMOD=etsi: the reference's unchanged construction calls
+    (SignalProcessor(sample_rate=...), TetraDecoder(auto_decrypt=...), modern.py:1886-1887) run the
+    north-star chain."""
+    from tetraear.signal import SignalProcessor
+    from tetraear.core import TetraDecoder
+    from tetraear.signal.etsi import synth
+    monkeypatch.setenv("TETRAEAR_DEMOD", "etsi")
+    p = SignalProcessor(sample_rate=2.4e6)
+    d = TetraDecoder(auto_decrypt=False)
+    assert p.mode == "etsi" and d.mode == "etsi"
+    iq = synth(1, 131072, seed=11, snr_db=20.0, cfo_max=300.0)[0][0]
+    hard = p.process(iq)
+    assert hasattr(hard, "soft_bits") and len(hard.soft_bits) == 2 * len(hard)
+    frames = d.decode(hard)
+    assert all("blocks" in f for f in frames)
 
 
 def test_full_size_round_trip():
@@ -445,7 +564,7 @@ def test_c4_full_chain_4096_bursts():
     dev = torch.device("cuda", 0)
     c = _hip.ctx()
     C, N = 1536, 131072   # ~2.8 complete bursts per 131072-sample chunk
-    st = BenchStep(c, C, N, 2.4e6, seed=44, device=dev)
+    st = BenchStep(c, C, N, 2.4e6, seed=44, device=dev, cells="given")
     st()
     torch.cuda.synchronize(dev)
     nb = st.nburst.cpu().numpy()
@@ -483,3 +602,63 @@ def test_c4_full_chain_4096_bursts():
                 assert np.array_equal(t1[ch, k, :len(tb)], tb)
                 k += 1
         assert k == int(nk[ch])
+    # the same batch through the acquiring lower MAC (bench default): a channel acquires its cell
+    # from a sync burst in the chunk, and every block of a channel that did decodes as with the cell given
+    acq = BenchStep(c, C, N, 2.4e6, seed=44, device=dev, cells="acquire")
+    acq()
+    torch.cuda.synchronize(dev)
+    state = acq.cell_state.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+    ab, at1 = acq.blocks.cpu().numpy(), acq.type1.cpu().numpy()
+    bursts = st.bursts.cpu().numpy()
+    nacq = 0
+    for ch in range(C):
+        has_sb = any(int(bursts[ch, b, 1]) == 2 for b in range(int(nb[ch])))
+        sb_ok = False
+        q = 0
+        for b in range(int(nb[ch])):
+            if int(bursts[ch, b, 1]) == 2 and blocks[ch, q, 1]:
+                sb_ok = True
+            q += 1 if int(bursts[ch, b, 1]) == 0 else 2
+        assert (state[ch] == cells[ch]) == sb_ok or (not has_sb and state[ch] == 3), ch
+        if sb_ok:
+            nacq += 1
+            assert np.array_equal(ab[ch, :int(nk[ch])], blocks[ch, :int(nk[ch])]), ch
+            for j in range(int(nk[ch])):
+                n1j = n1[int(blocks[ch, j, 0])]
+                assert np.array_equal(at1[ch, j, :n1j], t1[ch, j, :n1j]), (ch, j)
+    assert nacq >= C // 3   # ~2.8 bursts per chunk, a quarter of them sync bursts
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_block_codec_vs_independent_spec(kind):
+    """The GPU encoder equals the independent spec restatement (oracle/etsi_spec.py, which shares
+    no code with etsi_oracle.c), and every CRC-good block the GPU decoder returns is a maximum-
+    likelihood codeword: its re-encoding correlates with the received soft bits at least as well as
+    the transmitted one (scored by the spec encoder)."""
+    import etsi_spec as S
+    from tetraear import _hip
+    rng = np.random.default_rng(30 + kind)
+    n1, K = S.KINDS[kind]["n1"], S.KINDS[kind]["K"]
+    F = 96
+    inits = ((rng.integers(0, 2 ** 30, F).astype(np.uint64) << 2) | 3).astype(np.uint32)
+    t1 = rng.integers(0, 2, (F, n1)).astype(np.uint8)
+    t5 = np.zeros((F, K), np.uint8)
+    c = _hip.ctx()
+    c.check(c.lib.tetra_etsi_encode_blocks(c.handle, _hip.ptr(t1), F, kind, _hip.ptr(inits), _hip.ptr(t5)))
+    for f in range(F):
+        assert np.array_equal(t5[f], S.encode(t1[f], kind, int(inits[f]))), f
+    sigma = np.where(np.arange(F) % 3 == 0, 55.0, 35.0)[:, None]
+    soft = np.clip(np.rint(np.where(t5 == 0, 32.0, -32.0) + rng.normal(0, 1, t5.shape) * sigma), -127, 127)
+    soft = soft.astype(np.int8)
+    dec = np.zeros((F, n1), np.uint8)
+    ok = np.zeros(F, np.uint8)
+    c.check(c.lib.tetra_etsi_decode_blocks(c.handle, _hip.ptr(soft), F, kind, _hip.ptr(inits), _hip.ptr(dec),
+                                           _hip.ptr(ok)))
+    ngood = 0
+    for f in range(F):
+        if ok[f]:   # a CRC-good block's path is type-1 + its CRC + zero tail
+            ngood += 1
+            m_dec = S.codeword_metric(soft[f], S.type2(dec[f]), kind, int(inits[f]))
+            m_tx = S.codeword_metric(soft[f], S.type2(t1[f]), kind, int(inits[f]))
+            assert m_dec >= m_tx, (f, m_dec, m_tx)
+    assert ngood >= F // 2

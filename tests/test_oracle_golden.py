@@ -3,7 +3,8 @@ import numpy as np
 import pytest
 
 import compat as O
-from conftest import iq_to_c64
+import mac as M
+from conftest import decoded_view, iq_to_c64
 
 
 def test_g1_process_bit_exact(g1):
@@ -64,6 +65,22 @@ def test_g2_sync_and_frames(g2):
                 assert {5: "Synchronization", 2: "NormalDownlink"}[f["burst_type"]] == g["burst_type"]
                 assert f["crc_ok"] == g["crc_ok"] and f["header"] == g["header"]
                 assert list(f["ts"]) == g["ts"] and list(f["data"]) == g["data"]
+
+
+def test_g2_decode_mac_stage(g2):
+    """decode() through decode_frame's MAC PDU stage (decoder.py:994-1100): the frames the
+    reference keeps and their mac_pdu / encrypted / encryption_algorithm, for all streams of g2
+    (including the round-3 MAC streams: CRC-good and -bad slots, sync bursts, fragment chains)."""
+    z, recs = g2
+    kept = dropped = 0
+    for i, r in enumerate(recs):
+        mp = M.MacParser()
+        got = O.decode_with_mac(z[f"s{i}_sym"], mp)
+        assert got == [decoded_view(d) for d in r["decoded"]], i
+        assert (mp.n_clear, mp.n_enc) == (r["stats"]["clear_mode_frames"], r["stats"]["encrypted_frames"]), i
+        kept += len(got)
+        dropped += sum(f["nbits"] >= 510 for f in r["frames"]) - len(got)
+    assert kept > 100 and dropped > 10
 
 
 def test_g3_crc_and_bursts(g3):

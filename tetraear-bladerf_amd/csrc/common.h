@@ -27,6 +27,7 @@ enum Slot {
     S_W11,                                                 // waterfall window + twiddles
     S_W12,                                                 // ETSI channel-filter tap image (kept)
     S_W13,                                                 // diagnostics (tetra_read_floor sink)
+    S_W14,                                                 // ETSI: scrambler inits the cell table holds
     S_COUNT
 };
 
@@ -84,6 +85,7 @@ struct Staging {
     explicit Staging(tetra_ctx *c) : ctx(c) {}
     const void *in(const void *p, size_t bytes);
     void *out(void *p, size_t bytes);
+    void *inout(void *p, size_t bytes);   // `in` + `out` on one buffer (host contents uploaded first)
     int finish();   // D2H copies (if any) + stream sync when host memory was involved
 };
 

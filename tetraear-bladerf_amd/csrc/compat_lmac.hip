@@ -339,21 +339,23 @@ __global__ __launch_bounds__(64) void k_mac_headers(const uint8_t *__restrict__ 
     if (f >= F) return;
     const uint8_t *b = bits + (size_t)f * stride;
     const long n = nbits[f];
+    // a bit is a nonzero byte, in the header fields as in the data bytes below (BitArray semantics)
+    auto bit = [&](long p) { return (int)(b[p] != 0); };
     auto uint_at = [&](long p, int w) {   // int(''.join(str(x) for x in bits[p:p+w]), 2)
         int v = 0;
-        for (int i = 0; i < w; ++i) v = (v << 1) | b[p + i];
+        for (int i = 0; i < w; ++i) v = (v << 1) | bit(p + i);
         return v;
     };
     // header (every lane computes it: the data range below depends on it)
     int status = 1, ptype = 0, mode = 0, fill = 0, addr = -1, length = 0, sys = 0, mcc = 0, mnc = 0, cc = 0;
     long dpos = 0, dbits = 0;
     if (n >= 8) {
-        const int pti = (b[0] << 1) | b[1];
+        const int pti = (bit(0) << 1) | bit(1);
         ptype = pti == 0 ? 0 : pti == 1 ? 1 : pti == 2 ? 3 : 2;
-        mode = (b[2] << 1) | b[3];
+        mode = (bit(2) << 1) | bit(3);
         status = 0;
         if (ptype == 0 || ptype == 2) {            // RESOURCE (:399-449) / END (:506-544)
-            fill = b[4];
+            fill = bit(4);
             long pos = 5;
             if (ptype == 0) {
                 if (n < pos + 24) status = 1;
@@ -368,7 +370,7 @@ __global__ __launch_bounds__(64) void k_mac_headers(const uint8_t *__restrict__ 
                 else { dpos = pos; dbits = (dl > 0 && n >= pos + dl) ? dl : n - pos; }
             }
         } else if (ptype == 1) {                   // FRAG (:451-469)
-            fill = b[4];
+            fill = bit(4);
             dpos = 5;
             dbits = n - 5;
         } else {                                   // BROADCAST (:471-504)

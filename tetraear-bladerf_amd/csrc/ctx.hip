@@ -75,6 +75,18 @@ void *Staging::out(void *p, size_t bytes) {
     return d;
 }
 
+void *Staging::inout(void *p, size_t bytes) {
+    if (failed) return nullptr;
+    if (is_device_ptr(p)) return p;
+    void *d = out(p, bytes);
+    if (d && hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) {
+        failed = true;
+        tetra_fail(ctx, TETRA_E_HIP, "H2D staging copy failed");
+        return nullptr;
+    }
+    return d;
+}
+
 int Staging::finish() {
     if (failed) return ctx->err.empty() ? tetra_fail(ctx, TETRA_E_HIP, "staging failed") : TETRA_E_HIP;
     hipError_t e = hipGetLastError();

@@ -920,10 +920,7 @@ __host__ __device__ inline size_t job_cap(int kind, size_t C) { return kind == 1
 // One wave per channel: pack hard bits, greedy burst scan, then allocate this channel's coded
 // blocks dense job indices in each kind's region (one atomic per kind per channel; outputs are
 // indexed by (channel, slot), so results do not depend on the allocation order).
-#ifndef SYNC_WAVES_N
-#define SYNC_WAVES_N 4
-#endif
-constexpr int SYNC_WAVES = SYNC_WAVES_N;   // channels per workgroup: one job-counter atomic per workgroup
+constexpr int SYNC_WAVES = 4;   // channels per workgroup: one job-counter atomic per workgroup
 
 struct SyncLds {
     uint64_t words_all[SYNC_WAVES][LMAC_MAXBITS / 64 + 2];
@@ -958,11 +955,7 @@ __device__ __forceinline__ void sync_group(SyncLds &L, int grp, const uint8_t *_
     // in the dependent loop cost one memory latency per 64 symbols
     constexpr int PK = 8;
     const int sl = lane >> 1, comp = lane & 1;
-#ifdef SYNC_SKIP_PACK   // timing-only variant: words left as they are
-    for (int s00 = 0; s00 < 0; s00 += 64 * PK) {
-#else
     for (int s00 = 0; s00 < nsy + 64; s00 += 64 * PK) {
-#endif
     uint32_t hA[PK], hB[PK];
 #pragma unroll
     for (int u = 0; u < PK; ++u) {
@@ -986,9 +979,6 @@ __device__ __forceinline__ void sync_group(SyncLds &L, int grp, const uint8_t *_
     }
     __syncthreads();
     int nb = 0;
-#ifdef SYNC_SKIP_SCAN   // timing-only variant: no burst scan
-    nbits = 0;
-#endif
     for (int cur = 0; cur + 510 <= nbits && nb < ETSI_MAXB;) {
         const int s = cur + lane;
         int kind = -1;
@@ -1063,16 +1053,13 @@ __device__ __forceinline__ void sync_group(SyncLds &L, int grp, const uint8_t *_
 }
 
 
-// Grid: one workgroup per SYNC_WAVES channels, walked with a grid stride (TETRA_SYNC_GRID caps it).
+// Grid: one workgroup per SYNC_WAVES channels (the loop is a grid stride).
 __global__ __launch_bounds__(64 * SYNC_WAVES) void k_etsi_sync(const uint8_t *__restrict__ hard, const int32_t *__restrict__ nsym,
                                                   int smax, int32_t *__restrict__ nburst, int32_t *__restrict__ bursts,
                                                   int32_t *__restrict__ nblock,
                                                   unsigned long long *__restrict__ jcount, Job *__restrict__ jobs,
                                                   int C) {
     __shared__ SyncLds L;
-#ifdef SYNC_NOOP   // timing-only variant: no bursts found (job counters stay 0), so no Viterbi work
-    return;
-#endif
     const int ng = (C + SYNC_WAVES - 1) / SYNC_WAVES;
     for (int g = blockIdx.x; g < ng; g += gridDim.x) {
         sync_group(L, g, hard, nsym, smax, nburst, bursts, nblock, jcount, jobs, C);
@@ -1201,7 +1188,6 @@ __device__ __forceinline__ void viterbi_wave(int8_t *rows, const Job *__restrict
     const size_t j = jbase + jl;
     const Job jb = act ? jobs[j] : Job{0, 0, 0, 0, KIND, 0};
     int8_t *row = rows + jw * VROW;
-#ifndef VIT_SKIP_GATHER   // timing-only variant (tools/build_variant.sh): rows left as they are
     if (act) {   // the quad loads the block's type-5 soft bits and scrambler bytes as dwords
         const int8_t *sb = softbits + (size_t)jb.ch * 2 * smax + jb.off;
         const uint8_t *scr = KIND == 2 ? bsch_scr : cell_scr + (size_t)jb.ch * 432;
@@ -1213,7 +1199,6 @@ __device__ __forceinline__ void viterbi_wave(int8_t *rows, const Job *__restrict
             load_seg<P.K / 4>(sb, sb_last, (const uint32_t *)scr, d32, q);
         }
     }
-#endif
     __syncthreads();   // the quad's row (one wave per workgroup)
     int32_t pm[4];
 #pragma unroll
@@ -1289,15 +1274,14 @@ __global__ __launch_bounds__(64) void k_etsi_viterbi(const Job *__restrict__ job
                                                      const int8_t *__restrict__ softbits, int smax,
                                                      const uint8_t *__restrict__ cell_scr,
                                                      const uint8_t *__restrict__ bsch_scr,
-                                                     uint32_t *__restrict__ surv) {
+                                                     uint32_t *__restrict__ surv, int kmask) {
     __shared__ __attribute__((aligned(16))) int8_t rows[16 * VROW];
-#ifdef VIT_NOOP   // timing-only variant: the lower MAC without its Viterbi
-    return;
-#endif
     const size_t ss = 32 * (size_t)C;
     const int8_t *sb_last = softbits + (size_t)C * 2 * smax - 1;   // the soft-bit buffer's last byte
     const unsigned long long cnt = *jcount;
-    const int n0 = (int)(cnt & 0x1FFFFFull), n1 = (int)((cnt >> 21) & 0x1FFFFFull), n2 = (int)(cnt >> 42);
+    // kinds outside kmask are left to another launch (cell acquisition decodes BSCH first)
+    const int n0 = kmask & 1 ? (int)(cnt & 0x1FFFFFull) : 0, n1 = kmask & 2 ? (int)((cnt >> 21) & 0x1FFFFFull) : 0,
+              n2 = kmask & 4 ? (int)(cnt >> 42) : 0;
     // the waves the job counts need (16 blocks each), walked with a grid stride: a grid smaller
     // than that keeps the lower MAC's LDS beside the demod's bounded when the two run side by side
     const int nb0 = (n0 + 15) / 16, nb1 = (n1 + 15) / 16, nb2 = (n2 + 15) / 16;
@@ -1318,10 +1302,12 @@ __global__ __launch_bounds__(64) void k_etsi_viterbi(const Job *__restrict__ job
 __global__ __launch_bounds__(64) void k_etsi_traceback(const Job *__restrict__ jobs,
                                                        const unsigned long long *__restrict__ jcount, int C,
                                                        const uint32_t *__restrict__ surv,
-                                                       int32_t *__restrict__ blocks, uint8_t *__restrict__ type1) {
+                                                       int32_t *__restrict__ blocks, uint8_t *__restrict__ type1,
+                                                       int kmask) {
     const size_t gstride = 4 * 32 * (size_t)C;   // dwords between survivor groups
     const unsigned long long cnt = *jcount;
-    const int n[3] = {(int)(cnt & 0x1FFFFFull), (int)((cnt >> 21) & 0x1FFFFFull), (int)(cnt >> 42)};
+    const int n[3] = {kmask & 1 ? (int)(cnt & 0x1FFFFFull) : 0, kmask & 2 ? (int)((cnt >> 21) & 0x1FFFFFull) : 0,
+                      kmask & 4 ? (int)(cnt >> 42) : 0};
     const int nb0 = (n[0] + 63) / 64, nb1 = (n[1] + 63) / 64, nb2 = (n[2] + 63) / 64;
     for (int b = blockIdx.x; b < nb0 + nb1 + nb2; b += gridDim.x) {
         const int kind = b < nb0 ? 0 : b < nb0 + nb1 ? 1 : 2;
@@ -1334,6 +1320,67 @@ __global__ __launch_bounds__(64) void k_etsi_traceback(const Job *__restrict__ j
         else if (kind == 1) traceback_lane<1>(jb, sv, gstride, blocks, type1);
         else traceback_lane<2>(jb, sv, gstride, blocks, type1);
     }
+}
+
+// --------------------------------------------------------------------------- cell acquisition
+// One lane per channel, after the BSCH blocks of the chunk are decoded (colour code 0): the last
+// CRC-good BSCH of the channel gives its extended colour code -- MAC-SYNC colour code at type-1
+// bits 4..9, D-MLE-SYNC MCC at 31..40 and MNC at 41..54 (EN 300 392-2 §21.4.4.2, §18.4.2.1) -- and
+// the scrambling init (ecc << 2) | 3 (§8.2.5.2).  Without one the channel keeps its init.  The
+// channel's 432 scrambler bytes (the table k_etsi_viterbi descrambles with) are regenerated only
+// when the init differs from the one the table was made for (tab_init; 0 = none yet).
+constexpr uint32_t SCR_TAPS = (1u << 0) | (1u << 6) | (1u << 9) | (1u << 10) | (1u << 16) | (1u << 20) | (1u << 21) |
+                              (1u << 22) | (1u << 24) | (1u << 25) | (1u << 27) | (1u << 28) | (1u << 30) | (1u << 31);
+
+__global__ __launch_bounds__(256) void k_cell_acquire(int C, const int32_t *__restrict__ nburst,
+                                                      const int32_t *__restrict__ bursts,
+                                                      const int32_t *__restrict__ blocks,
+                                                      const uint8_t *__restrict__ type1, uint32_t *__restrict__ cell_init,
+                                                      uint32_t *__restrict__ tab_init, uint8_t *__restrict__ cell_scr) {
+    const int ch = blockIdx.x * 256 + threadIdx.x;
+    if (ch >= C) return;
+    uint32_t init = cell_init[ch];
+    const int nb = min(nburst[ch], ETSI_MAXB);
+    int q = 0;   // block slot of burst b: the sync kernel's numbering (1 per NDB(n), 2 per NDB(p) / SB)
+    for (int b = 0; b < nb; ++b) {
+        const int k = bursts[((size_t)ch * ETSI_MAXB + b) * 2 + 1];
+        if (k == 2 && q < ETSI_MAXJ && blocks[((size_t)ch * ETSI_MAXJ + q) * 4 + 1]) {
+            const uint8_t *t = type1 + ((size_t)ch * ETSI_MAXJ + q) * 268;
+            uint32_t ecc = 0;
+            for (int i = 4; i < 10; ++i) ecc = (ecc << 1) | (t[i] & 1u);     // colour code (low 6)
+            uint32_t mm = 0;
+            for (int i = 31; i < 55; ++i) mm = (mm << 1) | (t[i] & 1u);     // MCC(10) MNC(14)
+            init = (((mm << 6) | ecc) << 2) | 3u;
+        }
+        q += k == 0 ? 1 : 2;
+    }
+    cell_init[ch] = init;
+    if (tab_init[ch] != init) {
+        tab_init[ch] = init;
+        uint32_t r = init;
+        uint32_t *o = reinterpret_cast<uint32_t *>(cell_scr + (size_t)ch * 432);
+        for (int w = 0; w < 108; ++w) {   // four scrambler bytes (0 / 1) per dword store
+            uint32_t v = 0;
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t bt = (uint32_t)__popc(r & SCR_TAPS) & 1u;
+                r = (r >> 1) | (bt << 31);
+                v |= bt << (8 * k);
+            }
+            o[w] = v;
+        }
+    }
+}
+
+// ETSI differential decision on given symbol-spaced samples (SignalProcessor(mode="etsi")
+// .demodulate_dqpsk): d = x[k] conj(x[k-1]), dibit = (Im d < 0, Re d < 0) -- EN 300 392-2 Table 5.1
+// (00 +pi/4, 01 +3pi/4, 11 -3pi/4, 10 -pi/4), the fused demod's decision without its CFO rotation.
+template <typename T>
+__global__ __launch_bounds__(256) void k_etsi_decide(const T *__restrict__ x, long n, uint8_t *__restrict__ hard) {
+    const long k = (long)blockIdx.x * 256 + threadIdx.x + 1;
+    if (k >= n) return;
+    const float ar = (float)x[k].x, ai = (float)x[k].y, br = (float)x[k - 1].x, bi = (float)x[k - 1].y;
+    const float dr = fmaf(ar, br, ai * bi), di = fmaf(ai, br, -(ar * bi));
+    hard[k - 1] = (uint8_t)(((di < 0.0f) << 1) | (dr < 0.0f));
 }
 
 // --------------------------------------------------------------------------- component kernels
@@ -1442,6 +1489,26 @@ static int etsi_check(tetra_ctx *ctx, const tetra_etsi_plan *P) {
     return TETRA_OK;
 }
 
+// Which channel-filter kernel a launch takes (launch_chanfilt, tetra_etsi_kernel_info).
+enum CfKernel { CF_W_FUSED, CF_W, CF_SC16_FUSED, CF_SC16, CF_F4_FUSED, CF_F4 };
+static CfKernel chanfilt_kernel(int fmt, int64_t M2, bool fused) {
+    if (fmt == TETRA_CF32 && M2 <= YLDS) return fused ? CF_W_FUSED : CF_W;
+    if (fmt == TETRA_SC16) return fused ? CF_SC16_FUSED : CF_SC16;
+    return fused ? CF_F4_FUSED : CF_F4;
+}
+static const void *chanfilt_fn(CfKernel k) {
+    switch (k) {
+    case CF_W_FUSED: return reinterpret_cast<const void *>(&k_chanfilt_w<true>);
+    case CF_W: return reinterpret_cast<const void *>(&k_chanfilt_w<false>);
+    case CF_SC16_FUSED: return reinterpret_cast<const void *>(&k_chanfilt<uint2, true>);
+    case CF_SC16: return reinterpret_cast<const void *>(&k_chanfilt<uint2, false>);
+    case CF_F4_FUSED: return reinterpret_cast<const void *>(&k_chanfilt<float4, true>);
+    default: return reinterpret_cast<const void *>(&k_chanfilt<float4, false>);
+    }
+}
+static const char *const CF_NAMES[] = {"k_chanfilt_w", "k_chanfilt_w", "k_chanfilt", "k_chanfilt", "k_chanfilt",
+                                       "k_chanfilt"};
+
 // Stage-1 taps and the per-branch stage-2 tap table (k_chanfilt), then the launch.
 static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *x, int fmt, size_t C, size_t N,
                            int64_t M1, int64_t M2, float2 *y, const TimingOut *fused = nullptr) {
@@ -1468,24 +1535,31 @@ static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void 
     PROF(ctx, fused ? "etsi_demod" : "etsi_chanfilt");
     const TimingOut to = fused ? *fused : TimingOut{};
     const dim3 g((unsigned)C), b(256);
-    if (fmt == TETRA_CF32 && M2 <= YLDS && fused)
+    switch (chanfilt_kernel(fmt, M2, fused != nullptr)) {
+    case CF_W_FUSED:
         hipLaunchKernelGGL((k_chanfilt_w<true>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1, (int)M2,
                            coef, coef + 64, y, to);
-    else if (fmt == TETRA_CF32 && M2 <= YLDS)
+        break;
+    case CF_W:
         hipLaunchKernelGGL((k_chanfilt_w<false>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1, (int)M2,
                            coef, coef + 64, y, to);
-    else if (fmt == TETRA_SC16 && fused)
+        break;
+    case CF_SC16_FUSED:
         hipLaunchKernelGGL((k_chanfilt<uint2, true>), g, b, 0, ctx->stream, (const uint2 *)x, (long)N, (int)M1, (int)M2,
                            coef, coef + 64, y, to);
-    else if (fmt == TETRA_SC16)
+        break;
+    case CF_SC16:
         hipLaunchKernelGGL((k_chanfilt<uint2, false>), g, b, 0, ctx->stream, (const uint2 *)x, (long)N, (int)M1,
                            (int)M2, coef, coef + 64, y, to);
-    else if (fused)
+        break;
+    case CF_F4_FUSED:
         hipLaunchKernelGGL((k_chanfilt<float4, true>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1,
                            (int)M2, coef, coef + 64, y, to);
-    else
+        break;
+    default:
         hipLaunchKernelGGL((k_chanfilt<float4, false>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1,
                            (int)M2, coef, coef + 64, y, to);
+    }
     HIP_TRY(ctx, hipGetLastError());
     return TETRA_OK;
 }
@@ -1502,6 +1576,21 @@ int tetra_etsi_lengths(const tetra_etsi_plan *P, size_t N, int64_t *M1, int64_t 
     return TETRA_OK;
 }
 
+int tetra_etsi_kernel_info(tetra_ctx *ctx, const tetra_etsi_plan *P, int fmt, size_t N, int fused, char *name,
+                           size_t name_len, int64_t *lds_bytes) {
+    if (!ctx || !P || (fmt != TETRA_CF32 && fmt != TETRA_SC16)) return TETRA_E_INVALID;
+    int64_t M1, M2, sm;
+    tetra_etsi_lengths(P, N, &M1, &M2, &sm);
+    if (fused)   // the fused form's own condition (tetra_demod_etsi_fmt)
+        fused = fmt == TETRA_SC16 ? M2 + sm <= CF_LDS2_SC16 : (M2 <= YLDS && sm <= 2 * 4 * WIMG4);
+    const CfKernel k = chanfilt_kernel(fmt, M2, fused != 0);
+    hipFuncAttributes a;
+    HIP_TRY(ctx, hipFuncGetAttributes(&a, chanfilt_fn(k)));
+    if (name && name_len) snprintf(name, name_len, "%s", CF_NAMES[k]);
+    if (lds_bytes) *lds_bytes = (int64_t)a.sharedSizeBytes;
+    return TETRA_OK;
+}
+
 int tetra_etsi_set_cells(tetra_ctx *ctx, const uint32_t *scramb_init, size_t C) {
     if (!ctx || !scramb_init || C == 0) return TETRA_E_INVALID;
     std::vector<uint32_t> init(C);
@@ -1510,8 +1599,10 @@ int tetra_etsi_set_cells(tetra_ctx *ctx, const uint32_t *scramb_init, size_t C) 
     for (size_t c = 0; c < C; ++c) scramble_seq(init[c], 432, tab.data() + c * 432);
     scramble_seq(3u, 432, tab.data() + C * 432);   // BSCH: colour code 0
     uint8_t *d = (uint8_t *)ws(ctx, S_W5, tab.size());
-    if (!d) return TETRA_E_NOMEM;
+    uint32_t *ti = (uint32_t *)ws(ctx, S_W14, C * 4);   // the inits the table holds (cell acquisition)
+    if (!d || !ti) return TETRA_E_NOMEM;
     HIP_TRY(ctx, hipMemcpyAsync(d, tab.data(), tab.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(ti, init.data(), C * 4, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     ctx->cells = C;
     return TETRA_OK;
@@ -1609,6 +1700,22 @@ int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *i
 }
 
 
+int tetra_etsi_decide(tetra_ctx *ctx, const void *x, int fmt, size_t n, uint8_t *hard) {
+    if (!ctx || (fmt != TETRA_CF32 && fmt != TETRA_CF64)) return TETRA_E_INVALID;
+    if (n < 2) return TETRA_OK;
+    Staging st(ctx);
+    const void *xd = st.in(x, n * (fmt == TETRA_CF64 ? 16 : 8));
+    uint8_t *h = (uint8_t *)st.out(hard, n - 1);
+    if (!xd || !h) return st.finish();
+    if (fmt == TETRA_CF32)
+        hipLaunchKernelGGL(k_etsi_decide<float2>, dim3(grid_for(n - 1, 256)), dim3(256), 0, ctx->stream,
+                           (const float2 *)xd, (long)n, h);
+    else
+        hipLaunchKernelGGL(k_etsi_decide<double2>, dim3(grid_for(n - 1, 256)), dim3(256), 0, ctx->stream,
+                           (const double2 *)xd, (long)n, h);
+    return st.finish();
+}
+
 int tetra_etsi_decode_blocks(tetra_ctx *ctx, const int8_t *soft5, size_t F, int kind, const uint32_t *scramb_init,
                              uint8_t *type1, uint8_t *crc_ok) {
     if (!ctx || kind < 0 || kind > 2) return TETRA_E_INVALID;
@@ -1651,12 +1758,16 @@ int tetra_etsi_encode_blocks(tetra_ctx *ctx, const uint8_t *type1, size_t F, int
     return st.finish();
 }
 
-int tetra_lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard, const int32_t *nsym, size_t C,
-                    size_t smax, int32_t *nburst, int32_t *bursts, int32_t *nblock, int32_t *blocks, uint8_t *type1) {
+// The lower MAC's launch sequence; cell_init (device) selects acquisition, else the configured cells.
+static int lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard, const int32_t *nsym, size_t C,
+                     size_t smax, uint32_t *cell_init, int32_t *nburst, int32_t *bursts, int32_t *nblock,
+                     int32_t *blocks, uint8_t *type1) {
     if (!ctx || C == 0) return TETRA_E_INVALID;
-    if (ctx->cells < C) return tetra_fail(ctx, TETRA_E_INVALID, "tetra_etsi_set_cells() for %zu channels first", C);
+    if (!cell_init && ctx->cells < C)
+        return tetra_fail(ctx, TETRA_E_INVALID, "tetra_etsi_set_cells() for %zu channels first", C);
     if (2 * smax > LMAC_MAXBITS + 4) return tetra_fail(ctx, TETRA_E_INVALID, "chunk too long for tetra_lmac_etsi");
     Staging st(ctx);
+    uint32_t *ci = cell_init ? (uint32_t *)st.inout(cell_init, C * 4) : nullptr;
     const int8_t *sb = (const int8_t *)st.in(softbits, C * smax * 2);
     const uint8_t *hd = (const uint8_t *)st.in(hard, C * smax);
     const int32_t *ns = (const int32_t *)st.in(nsym, C * 4);
@@ -1669,34 +1780,74 @@ int tetra_lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard,
     // workspace: [job counters per kind (16 B)] [jobs] [survivors: 36 groups x jtot x 4 lanes x 32 bits
     // (SCH/F: 288 steps / 8; allocated as 288 x jtot dwords)]
     char *w = (char *)ws(ctx, S_W7, 16 + jtot * sizeof(Job) + 288 * jtot * 4);
-    if (!sb || !hd || !ns || !nbo || !bo || !nko || !ko || !to || !w) return st.finish();
+    if ((cell_init && !ci) || !sb || !hd || !ns || !nbo || !bo || !nko || !ko || !to || !w) return st.finish();
     unsigned long long *jcount = (unsigned long long *)w;
     Job *jobs = (Job *)(w + 16);
     uint32_t *surv = (uint32_t *)(w + 16 + jtot * sizeof(Job));
-    const uint8_t *cells = (const uint8_t *)ctx->slot[S_W5].p;
+    if (cell_init && ctx->cells != C) {   // acquisition on a new channel count: an empty table
+        std::vector<uint8_t> bsch(432);
+        scramble_seq(3u, 432, bsch.data());
+        uint8_t *tab = (uint8_t *)ws(ctx, S_W5, C * 432 + 432);
+        uint32_t *ti = (uint32_t *)ws(ctx, S_W14, C * 4);
+        if (!tab || !ti) return TETRA_E_NOMEM;
+        HIP_TRY(ctx, hipMemcpyAsync(tab + C * 432, bsch.data(), 432, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemsetAsync(ti, 0, C * 4, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));   // bsch is a pageable host buffer
+        ctx->cells = C;
+    }
+    uint8_t *cells = (uint8_t *)ctx->slot[S_W5].p;
+    const uint8_t *bsch_scr = cells + ctx->cells * 432;
     {
         PROF(ctx, "etsi_sync");
         HIP_TRY(ctx, hipMemsetAsync(jcount, 0, 16, ctx->stream));
-        unsigned ngrp = (unsigned)((C + SYNC_WAVES - 1) / SYNC_WAVES);
-        static const long sgrid = [] { const char *e = getenv("TETRA_SYNC_GRID"); return e ? atol(e) : 0L; }();
-        if (sgrid > 0 && (unsigned long)sgrid < ngrp) ngrp = (unsigned)sgrid;
+        const unsigned ngrp = (unsigned)((C + SYNC_WAVES - 1) / SYNC_WAVES);
         hipLaunchKernelGGL(k_etsi_sync, dim3(ngrp), dim3(64 * SYNC_WAVES), 0,
                            ctx->stream, hd, ns, (int)smax, nbo, bo, nko, jcount, jobs, (int)C);
     }
+    // grids: the waves each kind's job capacity needs (16 blocks per trellis wave, 64 per traceback wave)
+    auto vgrid = [&](int m) {
+        size_t g = 0;
+        for (int k = 0; k < 3; ++k) g += (m >> k) & 1 ? (job_cap(k, C) + 15) / 16 : 0;
+        return dim3((unsigned)g);
+    };
+    auto tgrid = [&](int m) {
+        size_t g = 0;
+        for (int k = 0; k < 3; ++k) g += (m >> k) & 1 ? (job_cap(k, C) + 63) / 64 : 0;
+        return dim3((unsigned)g);
+    };
+    int mask = 7;
+    if (ci) {   // BSCH first (colour code 0), then the cell from it, then SCH/F + SCH/HD
+        PROF(ctx, "etsi_acquire");
+        hipLaunchKernelGGL(k_etsi_viterbi, vgrid(4), dim3(64), 0, ctx->stream, jobs, jcount, (int)C, sb, (int)smax,
+                           cells, bsch_scr, surv, 4);
+        hipLaunchKernelGGL(k_etsi_traceback, tgrid(4), dim3(64), 0, ctx->stream, jobs, jcount, (int)C, surv, ko, to, 4);
+        hipLaunchKernelGGL(k_cell_acquire, dim3(grid_for(C, 256)), dim3(256), 0, ctx->stream, (int)C, nbo, bo, ko, to,
+                           ci, (uint32_t *)ctx->slot[S_W14].p, cells);
+        mask = 3;
+    }
     {
         PROF(ctx, "etsi_viterbi");
-        unsigned nblk = (unsigned)((job_cap(0, C) + 15) / 16 + (job_cap(1, C) + 15) / 16 + (job_cap(2, C) + 15) / 16);
-        static const long vgrid = [] { const char *e = getenv("TETRA_VIT_GRID"); return e ? atol(e) : 0L; }();
-        if (vgrid > 0 && (unsigned long)vgrid < nblk) nblk = (unsigned)vgrid;
-        hipLaunchKernelGGL(k_etsi_viterbi, dim3(nblk), dim3(64), 0, ctx->stream, jobs, jcount, (int)C, sb, (int)smax,
-                           cells, cells + ctx->cells * 432, surv);
+        hipLaunchKernelGGL(k_etsi_viterbi, vgrid(mask), dim3(64), 0, ctx->stream, jobs, jcount, (int)C, sb, (int)smax,
+                           cells, bsch_scr, surv, mask);
     }
     {
         PROF(ctx, "etsi_traceback");
-        const unsigned ntb = (unsigned)((job_cap(0, C) + 63) / 64 + (job_cap(1, C) + 63) / 64 + (job_cap(2, C) + 63) / 64);
-        hipLaunchKernelGGL(k_etsi_traceback, dim3(ntb), dim3(64), 0, ctx->stream, jobs, jcount, (int)C, surv, ko, to);
+        hipLaunchKernelGGL(k_etsi_traceback, tgrid(mask), dim3(64), 0, ctx->stream, jobs, jcount, (int)C, surv, ko, to,
+                           mask);
     }
     return st.finish();
+}
+
+int tetra_lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard, const int32_t *nsym, size_t C,
+                    size_t smax, int32_t *nburst, int32_t *bursts, int32_t *nblock, int32_t *blocks, uint8_t *type1) {
+    return lmac_etsi(ctx, softbits, hard, nsym, C, smax, nullptr, nburst, bursts, nblock, blocks, type1);
+}
+
+int tetra_lmac_etsi_acquire(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard, const int32_t *nsym,
+                            size_t C, size_t smax, uint32_t *cell_init, int32_t *nburst, int32_t *bursts,
+                            int32_t *nblock, int32_t *blocks, uint8_t *type1) {
+    if (!cell_init) return tetra_fail(ctx, TETRA_E_INVALID, "cell_init is NULL");
+    return lmac_etsi(ctx, softbits, hard, nsym, C, smax, cell_init, nburst, bursts, nblock, blocks, type1);
 }
 
 }  // extern "C"

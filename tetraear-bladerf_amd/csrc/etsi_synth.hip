@@ -75,7 +75,8 @@ __device__ void encode_into(const uint8_t *t1, int kind, const uint8_t *scr, uin
 
 // One wave per (channel, burst).
 __global__ __launch_bounds__(64) void k_synth_bursts(uint64_t seed, int NBR, const uint8_t *__restrict__ cell_scr,
-                                                     const uint8_t *__restrict__ bsch_scr, uint8_t *__restrict__ bits,
+                                                     const uint8_t *__restrict__ bsch_scr,
+                                                     const uint32_t *__restrict__ cell_init, uint8_t *__restrict__ bits,
                                                      int32_t *__restrict__ kinds, uint8_t *__restrict__ payload) {
     const int ch = blockIdx.x / NBR, b = blockIdx.x % NBR, lane = threadIdx.x;
     __shared__ uint8_t t1[2][268];
@@ -94,8 +95,14 @@ __global__ __launch_bounds__(64) void k_synth_bursts(uint64_t seed, int NBR, con
             continue;
         }
         const int n1 = kp(kind).n1;
+        // BSCH: the SYNC PDU of the channel's cell -- MAC-SYNC colour code at bits 4..9 and
+        // D-MLE-SYNC MCC 31..40 / MNC 41..54 (EN 300 392-2 §21.4.4.2, §18.4.2.1), MSB first
+        const uint32_t ecc = cell_init[ch] >> 2;   // MCC(10) MNC(14) CC(6)
         for (int i = lane; i < 268; i += 64) {
-            const uint8_t v = i < n1 ? (uint8_t)(hkey(seed, ch, b * 2 + blk, i) & 1) : 0;
+            uint8_t v = i < n1 ? (uint8_t)(hkey(seed, ch, b * 2 + blk, i) & 1) : 0;
+            if (kind == 2 && i >= 4 && i < 10) v = (uint8_t)((ecc >> (9 - i)) & 1u);          // CC
+            if (kind == 2 && i >= 31 && i < 41) v = (uint8_t)((ecc >> (29 - (i - 31))) & 1u);  // MCC
+            if (kind == 2 && i >= 41 && i < 55) v = (uint8_t)((ecc >> (19 - (i - 41))) & 1u);  // MNC
             t1[blk][i] = v;
             pl[i] = v;
         }
@@ -254,7 +261,7 @@ int tetra_synth_etsi(tetra_ctx *ctx, size_t C, size_t N, double fs, uint64_t see
     const float sigma = snr_db > -100.f && snr_db < 200.f
                             ? amp * sqrtf((float)(fs / 18000.0) / powf(10.f, snr_db / 10.f) / 2.f) : 0.f;
     hipLaunchKernelGGL(k_synth_bursts, dim3((unsigned)(C * NBR)), dim3(64), 0, ctx->stream, seed, NBR, scr,
-                       scr + C * 432, bits, kd, pl);
+                       scr + C * 432, ci, bits, kd, pl);
     hipLaunchKernelGGL(k_synth_phase, dim3((unsigned)C), dim3(64), 0, ctx->stream, bits, nsym, ph, seed);
     hipLaunchKernelGGL(k_synth_iq, dim3(grid_for(C * N, 256)), dim3(256), 0, ctx->stream, ph, nsym, (long)N, fs, seed,
                        amp, sigma, cfo_max, tt, x);

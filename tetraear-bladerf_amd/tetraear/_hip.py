@@ -105,7 +105,10 @@ def _bind(L):
         "tetra_demod_etsi_fmt": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _i32, _sz, _sz, _vp, _vp, _vp, _vp, _sz,
                                         _vp]),
         "tetra_etsi_set_cells": (_i32, [_vp, _vp, _sz]),
+        "tetra_etsi_decide": (_i32, [_vp, _vp, _i32, _sz, _vp]),
+        "tetra_etsi_kernel_info": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _i32, _sz, _i32, ctypes.c_char_p, _sz, _vp]),
         "tetra_lmac_etsi": (_i32, [_vp, _vp, _vp, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp]),
+        "tetra_lmac_etsi_acquire": (_i32, [_vp, _vp, _vp, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp]),
         "tetra_etsi_decode_blocks": (_i32, [_vp, _vp, _sz, _i32, _vp, _vp, _vp]),
         "tetra_etsi_encode_blocks": (_i32, [_vp, _vp, _sz, _i32, _vp, _vp]),
         "tetra_wb_lengths": (_i32, [ctypes.POINTER(WbPlan), _sz, _vp, _vp]),

@@ -8,8 +8,10 @@ reference's float decisions (threshold comparisons, the adaptive re-search rule)
 frame dicts.  Upper-MAC parsing, SDS and decryption (decoder.py:994-1117) are not part of this
 hot-path build: they stay the reference's Python and attach through ``upper_mac``.
 
-``mode="etsi"`` decodes ETSI channel coding (descramble, deinterleave, RCPC Viterbi, CRC-16) on
-the soft bits of the ETSI demodulator instead; see tetraear.core.etsi.
+``mode="etsi"`` (or ``TETRAEAR_DEMOD=etsi`` for callers that construct ``TetraDecoder()``
+unchanged) decodes ETSI channel coding (cell acquisition from the BSCH, descramble, deinterleave,
+RCPC Viterbi, CRC-16) on the soft bits of the ETSI demodulator instead; see tetraear.core.etsi.
+Its frames carry the reference's frame-dict keys, built from the decoded type-1 bits.
 """
 import ctypes
 import functools
@@ -19,7 +21,7 @@ from typing import Optional
 import numpy as np
 
 from tetraear import _hip
-from tetraear.core.protocol import TetraProtocolParser, burst_from_bits
+from tetraear.core.protocol import TetraProtocolParser, burst_data_bits, burst_from_bits
 
 logger = logging.getLogger(__name__)
 
@@ -81,7 +83,7 @@ def _bits_u8(bits):
 class TetraDecoder:
     """Decodes TETRA frames from demodulated symbols (decoder.py:16)."""
 
-    def __init__(self, key_manager=None, auto_decrypt: bool = True, mode: str = "compat"):
+    def __init__(self, key_manager=None, auto_decrypt: bool = True, mode=None):
         self.SYNC_PATTERN = [0, 1, 0, 1, 1, 0, 0, 1, 1, 1, 0, 0, 0, 1, 0, 0,
                              1, 0, 1, 1, 0, 0, 1, 1, 1, 0, 0, 0, 1, 0, 0]
         self.FRAME_LENGTH = 510
@@ -90,9 +92,8 @@ class TetraDecoder:
         self.protocol_parser = TetraProtocolParser()
         self.sync_patterns = {'TS1': TS1.copy(), 'TS2': TS2.copy()}
         self.user_keys = []
-        if mode not in ("compat", "etsi"):
-            raise ValueError("mode must be 'compat' or 'etsi'")
-        self.mode = mode
+        from tetraear.signal.processor import demod_mode
+        self.mode = demod_mode(mode)
         self._etsi = None
 
     # ------------------------------------------------------------------ bits
@@ -139,11 +140,14 @@ class TetraDecoder:
     def decode(self, symbols):
         """Sync cascade, slot slicing and burst parsing of one symbol stream (decoder.py:835-888)."""
         if self.mode == "etsi":
-            return self._etsi_rx().decode(symbols)
+            return self._etsi_frames(self._etsi_rx().decode(symbols))
         return self.decode_batch([symbols])[0]
 
     def decode_batch(self, streams):
-        """decode() over many independent symbol streams with one device pass."""
+        """decode() over many independent symbol streams with one device pass per stage: sync,
+        slicing, burst typing and CRC in one tetra_lmac_compat launch, then the MAC PDU headers of
+        every slot in one tetra_mac_headers launch.  The parser state (statistics, fragment buffer,
+        SYSINFO) is applied in stream and frame order, as consecutive decode() calls would."""
         streams = [np.asarray(s) for s in streams]
         C = len(streams)
         stride = max([len(s) for s in streams] + [1])
@@ -160,20 +164,29 @@ class TetraDecoder:
         c.check(c.lib.tetra_lmac_compat(c.handle, _hip.ptr(sym), _hip.ptr(ns), C, stride, _hip.ptr(cascade_table()),
                                         _hip.ptr(nsync), _hip.ptr(rec), _hip.ptr(fbits), _hip.ptr(bbits)),
                 "tetra_lmac_compat")
-        out = []
+        slots = []   # (stream, record, frame bits, burst bits) of every slot decode_frame parses
         for i in range(C):
-            frames = []
             for f in range(int(nsync[i])):
                 r = rec[i, f]
-                if not r[_hip.F_VALID]:
-                    continue
-                nb = int(r[_hip.F_NBITS])
-                number = int(r[_hip.F_NUMBER])
-                frame = self._frame_from_device(fbits[i, f, :nb].astype(np.int64), number, r, bbits[i, f])
-                if frame:
-                    frames.append(frame)
-                    logger.info(f"Decoded frame {frame['number']} (type: {frame['type']})")
-            out.append(frames)
+                if r[_hip.F_VALID] and int(r[_hip.F_NBITS]) >= self.FRAME_LENGTH:
+                    slots.append((i, r, fbits[i, f, :int(r[_hip.F_NBITS])], bbits[i, f]))
+        # parse_mac_pdu(burst.data_bits) of every slot (decoder.py:996): device header fields
+        rows = [burst_data_bits(bb, int(r[_hip.F_BTYPE])) for _, r, _, bb in slots]
+        fields, data = self.protocol_parser.mac_fields(rows) if rows else (None, None)
+        out = [[] for _ in range(C)]
+        for k, (i, r, fb, bb) in enumerate(slots):
+            number = int(r[_hip.F_NUMBER])
+            frame = self._frame_dict(fb.astype(np.int64), 0, number)
+            crc_ok = bool(r[_hip.F_CRC])
+            self.protocol_parser.count_burst(crc_ok)
+            burst = burst_from_bits(bb, int(r[_hip.F_BTYPE]), crc_ok, number % 4,
+                                    self.protocol_parser.current_frame_number, self.protocol_parser.colour_code or 0)
+            frame['burst_crc'] = crc_ok
+            pdu = self.protocol_parser.mac_state(fields[k], data[k])
+            frame = self._mac_stage(frame, burst, pdu)
+            if frame:
+                out[i].append(frame)
+                logger.info(f"Decoded frame {frame['number']} (type: {frame['type']})")
         return out
 
     def _frame_dict(self, frame_bits, start_pos, frame_number):
@@ -198,19 +211,36 @@ class TetraDecoder:
             'additional_info': info,
         }
 
-    def _frame_from_device(self, frame_bits, number, rec, burst_bits):
-        if len(frame_bits) < self.FRAME_LENGTH:
-            return None
-        frame = self._frame_dict(frame_bits, 0, number)
-        crc_ok = bool(rec[_hip.F_CRC])
-        self.protocol_parser.count_burst(crc_ok)
-        burst = burst_from_bits(burst_bits, int(rec[_hip.F_BTYPE]), crc_ok, number % 4,
-                                self.protocol_parser.current_frame_number, self.protocol_parser.colour_code or 0)
-        frame['burst_crc'] = crc_ok
-        return self.upper_mac(frame, burst)
+    def _mac_stage(self, frame, burst, pdu):
+        """decode_frame's MAC PDU stage (decoder.py:994-1100) on the parsed PDU of the slot.
+
+        No PDU and a failed CRC drops the frame (decoder.py:1093-1095).  A PDU adds
+        frame['mac_pdu'] and settles 'encrypted' / 'encryption_algorithm': from the PDU's mode when
+        it is encrypted (decoder.py:1008-1035), otherwise by the data-entropy rule -- more than 8
+        bytes with a distinct-byte ratio above 0.7 count as encrypted (decoder.py:1036-1053).
+        Then upper_mac (call metadata / SDS, decoder.py:1055-1091) runs on the kept frame."""
+        if pdu is None:
+            return frame if burst.crc_ok else None
+        frame['mac_pdu'] = {'type': pdu.pdu_type.name, 'encrypted': pdu.encrypted, 'address': pdu.address,
+                            'length': pdu.length, 'data': pdu.data}
+        if pdu.encrypted:
+            frame['encrypted'] = True
+            mode = getattr(pdu, 'encryption_mode', 0)
+            if mode in ENC_MODES:
+                frame['encryption_algorithm'], frame['additional_info']['encryption_mode'] = ENC_MODES[mode]
+            elif not frame['encryption_algorithm']:
+                frame['encryption_algorithm'] = 'TEA1'
+        else:
+            n = len(pdu.data)
+            if n > 0 and len(set(pdu.data)) / max(n, 1) > 0.7 and n > 8:
+                frame['encrypted'] = True
+            else:
+                frame['encrypted'] = False
+                frame['encryption_algorithm'] = None
+        return self.upper_mac(frame, burst, pdu)
 
     def decode_frame(self, bits, start_pos, symbols=None, frame_number=0):
-        """Frame header + burst parse of one 510-bit slot (decoder.py:890-992)."""
+        """Frame header, burst parse and MAC PDU stage of one 510-bit slot (decoder.py:890-1100)."""
         if len(bits) < self.FRAME_LENGTH:
             return None
         fb = np.asarray(bits)
@@ -224,17 +254,54 @@ class TetraDecoder:
             burst = self.protocol_parser.parse_burst(np.asarray(symbols), slot_number=frame_number % 4)
             if burst:
                 frame['burst_crc'] = burst.crc_ok
-                return self.upper_mac(frame, burst)
+                return self._mac_stage(frame, burst, self.protocol_parser.parse_mac_pdu(burst.data_bits))
         except Exception as e:   # the reference logs and keeps the frame (decoder.py:1102-1103)
             logger.debug(f"Protocol parsing error: {e}")
         return frame
 
-    def upper_mac(self, frame, burst):
-        """Hook for the reference's upper MAC / SDS / decryption (decoder.py:994-1117).
+    def upper_mac(self, frame, burst, mac_pdu=None):
+        """Hook for the reference's call metadata / SDS / decryption (decoder.py:1055-1117), called
+        with every frame the MAC PDU stage keeps and its MacPDU (None when the slot has none).
 
-        This build stops at the lower MAC and returns the frame unchanged; INTEGRATION.md shows how
-        the reference's own Python parsers attach here."""
+        This build stops at the MAC PDU and returns the frame unchanged; INTEGRATION.md shows how
+        the reference's own Python parsers attach here.  They cannot change which frames are kept:
+        the reference drops a frame only on an exception inside its MAC stage, and call metadata
+        and SDS only index the PDU's bytes within the lengths they check first."""
         return frame
+
+    def _etsi_frames(self, raw):
+        """ETSI bursts as the reference's frame dicts (decoder.py:960-972 keys + the MAC PDU stage),
+        built from the channel-decoded type-1 bits: a burst's blocks in order (SCH/F 268 bits,
+        SCH/HD 2 x 124, BSCH 60 + SCH/HD 124), frame number start // 510, burst_crc = every block's
+        CRC-16.  The ETSI details stay on the frame: 'blocks', 'burst', 'burst_kind'.  The MAC PDU
+        stage (drop rule included) is the compat one, applied to the decoded bits."""
+        from tetraear.core.protocol import BurstType, TetraBurst
+        rows, items = [], []
+        for f in raw:
+            bits = np.concatenate([b["bits"] for b in f["blocks"]]).astype(np.int64)
+            if len(bits) < 8:
+                continue
+            rows.append(bits.astype(np.uint8))
+            items.append((f, bits))
+        if not rows:
+            return []
+        fields, data = self.protocol_parser.mac_fields(rows)
+        out = []
+        for k, (f, bits) in enumerate(items):
+            number = f["position"] // 510
+            frame = self._frame_dict(bits, f["position"], number)
+            crc_ok = bool(f["crc_ok"])
+            self.protocol_parser.count_burst(crc_ok)
+            frame.update(burst_crc=crc_ok, blocks=f["blocks"], burst=f["burst"], burst_kind=f["burst_kind"])
+            burst = TetraBurst(burst_type=BurstType.Synchronization if f["burst_kind"] == 2 else BurstType.NormalDownlink,
+                               slot_number=number % 4, frame_number=self.protocol_parser.current_frame_number,
+                               training_sequence=np.zeros(0, np.int64), data_bits=bits, crc_ok=crc_ok,
+                               colour_code=self._etsi.colour_code or 0)
+            pdu = self.protocol_parser.mac_state(fields[k], data[k])
+            frame = self._mac_stage(frame, burst, pdu)
+            if frame:
+                out.append(frame)
+        return out
 
     def _etsi_rx(self):
         if self._etsi is None:

@@ -22,27 +22,78 @@ def scrambling_init(mcc, mnc, colour_code):
     return ((((mcc & 0x3FF) << 20) | ((mnc & 0x3FFF) << 6) | (colour_code & 0x3F)) << 2) | 3
 
 
+def cell_of(init):
+    """(MCC, MNC, colour code) of a scrambling init."""
+    ecc = int(init) >> 2
+    return (ecc >> 20) & 0x3FF, (ecc >> 6) & 0x3FFF, ecc & 0x3F
+
+
+UNKNOWN_CELL = scrambling_init(0, 0, 0)   # colour code 0: what a receiver descrambles with before the BSCH
+
+
 class EtsiLowerMac:
-    def __init__(self, mcc=0, mnc=0, colour_code=0):
-        self.cell = scrambling_init(mcc, mnc, colour_code)
+    """Lower MAC of the ETSI chain.  With a cell (mcc, mnc, colour_code) every channel is
+    descrambled with it.  Without one the receiver acquires the cell itself: each chunk's BSCH
+    blocks are decoded first with colour code 0, and the SYNC PDU of the last CRC-good one gives the
+    channel's MCC / MNC / colour code (tetra_lmac_etsi_acquire).  The acquired cell persists across
+    calls per channel -- the state the reference parser keeps from a SYSINFO broadcast
+    (/root/reference/tetraear/core/protocol.py:479-485) -- and is exposed as ``cells`` /
+    ``mcc`` / ``mnc`` / ``colour_code``."""
+
+    def __init__(self, mcc=None, mnc=None, colour_code=None):
+        self.acquire = mcc is None and mnc is None and colour_code is None
+        self.cell = None if self.acquire else scrambling_init(mcc or 0, mnc or 0, colour_code or 0)
+        self.cell_state = None   # [C] scrambling inits of the acquired cells (acquisition mode)
+
+    @property
+    def cells(self):
+        """Per channel (MCC, MNC, colour code) acquired so far, None where no BSCH decoded yet."""
+        if self.cell_state is None:
+            return []
+        return [None if int(v) == UNKNOWN_CELL else cell_of(v) for v in self.cell_state]
+
+    @property
+    def mcc(self):
+        c = self.cells[0] if self.cells else None
+        return None if c is None else c[0]
+
+    @property
+    def mnc(self):
+        c = self.cells[0] if self.cells else None
+        return None if c is None else c[1]
+
+    @property
+    def colour_code(self):
+        c = self.cells[0] if self.cells else None
+        return None if c is None else c[2]
 
     def decode_batch(self, soft, hard, nsym, cells=None):
-        """soft [C, 2*smax] int8, hard [C, smax] uint8, nsym [C] -> per channel a list of frames."""
+        """soft [C, 2*smax] int8, hard [C, smax] uint8, nsym [C] -> per channel a list of frames.
+        ``cells`` ([C] scrambling inits) overrides the receiver's cell for this call."""
         soft = np.ascontiguousarray(soft, np.int8)
         hard = np.ascontiguousarray(hard, np.uint8)
         nsym = np.ascontiguousarray(nsym, np.int32)
         C, smax = hard.shape
-        cells = np.full(C, self.cell, np.uint32) if cells is None else np.ascontiguousarray(cells, np.uint32)
         nb = np.zeros(C, np.int32)
         bursts = np.zeros((C, _hip.ETSI_MAXB, 2), np.int32)
         nk = np.zeros(C, np.int32)
         blocks = np.zeros((C, _hip.ETSI_MAXJ, 4), np.int32)
         t1 = np.zeros((C, _hip.ETSI_MAXJ, 268), np.uint8)
         c = _hip.ctx()
-        c.check(c.lib.tetra_etsi_set_cells(c.handle, _hip.ptr(cells), C), "tetra_etsi_set_cells")
-        c.check(c.lib.tetra_lmac_etsi(c.handle, _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(nsym), C, smax, _hip.ptr(nb),
-                                      _hip.ptr(bursts), _hip.ptr(nk), _hip.ptr(blocks), _hip.ptr(t1)),
-                "tetra_lmac_etsi")
+        if self.acquire and cells is None:
+            if self.cell_state is None or len(self.cell_state) != C:
+                self.cell_state = np.full(C, UNKNOWN_CELL, np.uint32)
+            c.check(c.lib.tetra_lmac_etsi_acquire(c.handle, _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(nsym), C, smax,
+                                                  _hip.ptr(self.cell_state), _hip.ptr(nb), _hip.ptr(bursts),
+                                                  _hip.ptr(nk), _hip.ptr(blocks), _hip.ptr(t1)),
+                    "tetra_lmac_etsi_acquire")
+        else:
+            cells = np.full(C, self.cell if self.cell is not None else UNKNOWN_CELL, np.uint32) if cells is None \
+                else np.ascontiguousarray(cells, np.uint32)
+            c.check(c.lib.tetra_etsi_set_cells(c.handle, _hip.ptr(cells), C), "tetra_etsi_set_cells")
+            c.check(c.lib.tetra_lmac_etsi(c.handle, _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(nsym), C, smax,
+                                          _hip.ptr(nb), _hip.ptr(bursts), _hip.ptr(nk), _hip.ptr(blocks), _hip.ptr(t1)),
+                    "tetra_lmac_etsi")
         out = []
         for ch in range(C):
             frames = []

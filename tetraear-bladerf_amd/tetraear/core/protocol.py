@@ -98,13 +98,22 @@ def _bits_u8(bits):
     return np.ascontiguousarray(np.where((b == 0) | (b == 1), b, 2), dtype=np.uint8)
 
 
+def burst_data_bits(bits510, btype_value):
+    """_extract_data_bits (protocol.py:277-290): all 510 bits of a synchronisation burst, else
+    bits[0:108] + bits[122:230]."""
+    if btype_value == BurstType.Synchronization.value:
+        return bits510
+    return np.concatenate([bits510[0:108], bits510[122:230]])
+
+
 def burst_from_bits(bits510, btype_value, crc_ok, slot_number, frame_number, colour_code):
     """Assemble a TetraBurst from the device's burst bits (protocol.py:267-290 slices)."""
     bits = bits510.astype(np.int64)
+    data = burst_data_bits(bits, btype_value)
     if btype_value == BurstType.Synchronization.value:
-        ts, data = bits[108:130], bits
+        ts = bits[108:130]
     else:
-        ts, data = bits[108:122], np.concatenate([bits[0:108], bits[122:230]])
+        ts = bits[108:122]
     return TetraBurst(burst_type=BurstType(btype_value), slot_number=slot_number, frame_number=frame_number,
                       training_sequence=ts, data_bits=data, crc_ok=bool(crc_ok), colour_code=colour_code)
 
@@ -222,16 +231,23 @@ class TetraProtocolParser:
     def parse_mac_pdu_batch(self, frames) -> list:
         """parse_mac_pdu over many frames in order, one launch: [MacPDU or None].
 
-        Frames are 0/1 bit vectors, as parse_burst's data_bits.  (The reference would raise a
-        ValueError from int(..., 2) for other values inside a parsed numeric field and shift them
-        into the header fields; this build rejects them up front with a ValueError.)"""
+        Frames are 0/1 integer bit vectors, as parse_burst's data_bits.  The reference raises a
+        ValueError from int(..., 2) when a parsed header field holds anything else (bool arrays
+        included: int('TrueFalse', 2)).  This build checks every frame of 8 or more bits: at the
+        first bad frame, the frames before it are parsed (their fragment / SYSINFO / statistics
+        state applied, as the reference's sequential calls would have left it) and then the
+        ValueError is raised, so the batch returns nothing."""
         rows = [np.asarray(f).ravel() for f in frames]
+        for i, r in enumerate(rows):
+            if r.size >= 8 and (r.dtype == np.bool_ or not np.all((r == 0) | (r == 1))):
+                self._mac_batch(rows[:i])
+                raise ValueError(f"parse_mac_pdu: frame {i}: bits must be integer 0/1")
+        return self._mac_batch(rows)
+
+    def mac_fields(self, rows):
+        """The stateless device half of parse_mac_pdu for many 0/1 rows: (fields [F, MAC_FIELDS],
+        packed data bytes [F, stride/8]) from one tetra_mac_headers launch."""
         F = len(rows)
-        if F == 0:
-            return []
-        for r in rows:
-            if r.size and not np.all((r == 0) | (r == 1)):
-                raise ValueError("parse_mac_pdu: bits must be 0/1")
         stride = max(8, max(r.size for r in rows))
         bits = np.zeros((F, stride), np.uint8)
         nbits = np.zeros(F, np.int32)
@@ -244,10 +260,16 @@ class TetraProtocolParser:
         c = _hip.ctx()
         c.check(c.lib.tetra_mac_headers(c.handle, _hip.ptr(bits), _hip.ptr(nbits), F, stride, _hip.ptr(fields),
                                         _hip.ptr(data), dstride), "tetra_mac_headers")
-        return [self._mac_state(fields[i], data[i]) for i in range(F)]
+        return fields, data
 
-    def _mac_state(self, r, data):
-        """The stateful half of parse_mac_pdu for one frame's device fields, in order."""
+    def _mac_batch(self, rows):
+        if not rows:
+            return []
+        fields, data = self.mac_fields(rows)
+        return [self.mac_state(fields[i], data[i]) for i in range(len(rows))]
+
+    def mac_state(self, r, data):
+        """The stateful half of parse_mac_pdu for one frame's device fields, applied in frame order."""
         status = int(r[_hip.MAC_STATUS])
         if r[_hip.MAC_SYSINFO]:   # set before the sanity check (protocol.py:483-485)
             self.mcc, self.mnc, self.colour_code = int(r[_hip.MAC_MCC]), int(r[_hip.MAC_MNC]), int(r[_hip.MAC_CC])

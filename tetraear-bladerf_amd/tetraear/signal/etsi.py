@@ -126,7 +126,51 @@ class EtsiReceiver:
         return SoftSymbols(hard[0, :nd].copy(), soft[0, :2 * nd].copy()), sym[0, :n].copy()
 
     def decide(self, symbols):
-        raise NotImplementedError("the ETSI decision runs inside the fused demod (use process())")
+        """Table 5.1 differential decision on given symbol-spaced samples (tetra_etsi_decide):
+        uint8 dibits, one fewer than the symbols (the fused demod's decision without its CFO
+        rotation; ETSI-mode demodulate_dqpsk)."""
+        x = np.asarray(symbols)
+        if len(x) < 2:
+            return np.array([], dtype=np.uint8)
+        fmt = _hip.TETRA_CF32 if x.dtype in (np.complex64, np.float32) else _hip.TETRA_CF64
+        xc = np.ascontiguousarray(x, np.complex64 if fmt == _hip.TETRA_CF32 else np.complex128)
+        out = np.empty(len(x) - 1, np.uint8)
+        c = _hip.ctx()
+        c.check(c.lib.tetra_etsi_decide(c.handle, _hip.ptr(xc), fmt, len(xc), _hip.ptr(out)), "tetra_etsi_decide")
+        return out
+
+    def chanfilt(self, samples):
+        """Channel filter: 2.4 MSps samples -> the RRC-matched 72 kHz samples (4 per symbol) the
+        timing stage reads (tetra_etsi_chanfilt); ETSI-mode filter_signal."""
+        x = np.ascontiguousarray(samples, np.complex64)
+        x = x[:len(x) - len(x) % 2]
+        _, M2, _ = lengths(self.plan, len(x))
+        y = np.zeros(max(M2, 0), np.complex64)
+        if M2 <= 0:
+            return y
+        c = _hip.ctx()
+        c.check(c.lib.tetra_etsi_chanfilt(c.handle, self.plan, _hip.ptr(x), 1, len(x), _hip.ptr(y)),
+                "tetra_etsi_chanfilt")
+        return y
+
+    def timing(self, y):
+        """Timing recovery on 72 kHz samples: (SoftSymbols hard dibits, complex64 symbol-spaced
+        samples) (tetra_etsi_timing); ETSI-mode extract_symbols returns the samples."""
+        y = np.ascontiguousarray(y, np.complex64)
+        M2 = len(y)
+        smax = M2 // 4 + 2
+        if M2 < 16:
+            return SoftSymbols(np.zeros(0, np.uint8), np.zeros(0, np.int8)), np.zeros(0, np.complex64)
+        sym = np.zeros(smax, np.complex64)
+        soft = np.zeros(2 * smax, np.int8)
+        hard = np.zeros(smax, np.uint8)
+        ns = np.zeros(1, np.int32)
+        c = _hip.ctx()
+        c.check(c.lib.tetra_etsi_timing(c.handle, self.plan, _hip.ptr(y), 1, M2, _hip.ptr(sym), _hip.ptr(soft),
+                                        _hip.ptr(hard), _hip.ptr(ns), smax, None), "tetra_etsi_timing")
+        n = int(ns[0])
+        nd = max(0, n - 1)
+        return SoftSymbols(hard[:nd].copy(), soft[:2 * nd].copy()), sym[:n].copy()
 
 
 def synth(C, N, fs=2.4e6, seed=1, snr_db=None, cfo_max=600.0, device_arrays=None):
@@ -149,9 +193,13 @@ class BenchStep:
 
     dtype = "f32 (DSP), int8/int32 (Viterbi)"
 
-    def __init__(self, c, C, N, fs, seed, device, snr_db=18.0, iq_format="cf32", demod="fused"):
+    def __init__(self, c, C, N, fs, seed, device, snr_db=18.0, iq_format="cf32", demod="fused", cells="acquire"):
         import torch
         self.c, self.C, self.N, self.fs = c, C, N, fs
+        # "acquire": the lower MAC finds each channel's cell in its BSCH (tetra_lmac_etsi_acquire,
+        # per-channel state carried from step to step, as a receiver streaming chunks would);
+        # "given": the synthesised cells are configured up front (tetra_etsi_set_cells)
+        self.cells_mode = cells
         # "fused": k_chanfilt<.., true> (timing on the LDS-resident 72 kHz samples, wave 0 of the
         # workgroup); "split": k_chanfilt<.., false> writes y (0.24 B per input sample) and k_timing
         # runs as its own launch -- with the pipeline, beside the next batch's channel filter
@@ -167,6 +215,8 @@ class BenchStep:
         c.check(c.lib.tetra_synth_etsi(c.handle, C, N, fs, seed, snr_db, 600.0, _hip.ptr(self.iq), _hip.ptr(self.cells),
                                        _hip.ptr(self.kinds), _hip.ptr(self.payload), None), "synth")
         c.check(c.lib.tetra_etsi_set_cells(c.handle, _hip.ptr(self.cells), C), "set_cells")
+        from tetraear.core.etsi import UNKNOWN_CELL
+        self.cell_state = torch.full((C,), UNKNOWN_CELL, dtype=torch.int32, device=device)
         if self.fmt == _hip.TETRA_SC16:   # the synth output is on the SC16 grid: exact
             self.iq = torch.round(self.iq * 32768).clamp_(-32768, 32767).to(torch.int16)
         sm = self.smax
@@ -256,6 +306,12 @@ class BenchStep:
             ev.record(st)
 
     def _lmac(self, c, soft, hard, nsym):
+        if self.cells_mode == "acquire":
+            c.check(c.lib.tetra_lmac_etsi_acquire(c.handle, _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(nsym), self.C,
+                                                  self.smax, _hip.ptr(self.cell_state), _hip.ptr(self.nburst),
+                                                  _hip.ptr(self.bursts), _hip.ptr(self.nblock), _hip.ptr(self.blocks),
+                                                  _hip.ptr(self.type1)), "lmac_etsi_acquire")
+            return
         c.check(c.lib.tetra_lmac_etsi(c.handle, _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(nsym), self.C, self.smax,
                                       _hip.ptr(self.nburst), _hip.ptr(self.bursts), _hip.ptr(self.nblock),
                                       _hip.ptr(self.blocks), _hip.ptr(self.type1)), "lmac_etsi")
@@ -303,71 +359,42 @@ class BenchStep:
         self._lmac(self.back, soft, hard, nsym)
         self.ev_back[i].record(self.s_back)
 
+    def kernel_info(self):
+        """(symbol, static LDS bytes) of the channel-filter kernel this step's demod launches, asked
+        from the library (tetra_etsi_kernel_info), so the bench follows the kernels as they change."""
+        name = ctypes.create_string_buffer(64)
+        lds = ctypes.c_int64(0)
+        self.c.check(self.c.lib.tetra_etsi_kernel_info(self.c.handle, self.plan, self.fmt, self.N,
+                                                       int(self.demod_mode == "fused"), name, 64, ctypes.byref(lds)),
+                     "tetra_etsi_kernel_info")
+        return name.value.decode(), lds.value
+
     def dominant(self):
         # fused demod: reads 8 B (cf32) or 4 B (SC16) per input sample; writes per symbol (0.0075 per
         # input sample) 8 B cf32 symbol + 2 B soft bits + 1 B hard dibit.  split: the same reads,
-        # writes y (8 B per 72 kHz sample = 0.24 B per input sample).  Kernel: the per-wave
-        # k_chanfilt_w for cf32 chunks of up to YLDS = 3904 outputs (etsi_rx.hip), else k_chanfilt.
+        # writes y (8 B per 72 kHz sample = 0.24 B per input sample).
         rd = 4.0 if self.fmt == _hip.TETRA_SC16 else 8.0
-        sym = "k_chanfilt_w" if self.fmt == _hip.TETRA_CF32 and self.M2 <= 3904 else "k_chanfilt"
+        sym = self.kernel_info()[0]
         if self.demod_mode == "split":
             return ("etsi_chanfilt", rd + 8.0 * self.M2 / self.N, sym)
         return ("etsi_demod", rd + 11.0 * 18000.0 / self.fs, sym)
 
     def floor_args(self):
-        """bench.py's read floor over this batch: one row per channel at the demod kernel's LDS
-        footprint -- k_chanfilt_w's 74,336 B (two workgroups per CU) or SC16 k_chanfilt's 39,568 B
-        (four)."""
+        """bench.py's read floor over this batch: one row per channel at the demod kernel's own LDS
+        footprint (so as many workgroups per CU as the kernel gets)."""
         row = self.N * (4 if self.fmt == _hip.TETRA_SC16 else 8)
-        return _hip.ptr(self.iq), self.C, row, 39568 if self.fmt == _hip.TETRA_SC16 else 74336
+        return _hip.ptr(self.iq), self.C, row, self.kernel_info()[1]
 
     def quality(self):
-        """Decoded-block statistics of the last step (device results, checked on the host)."""
+        """Decoded-block statistics of the last step (device results, checked on the host); with
+        cell acquisition also how many channels hold the synthesised cell."""
         nb = self.nblock.cpu().numpy()
         blocks = self.blocks.cpu().numpy()
         ok = sum(int(blocks[i, :nb[i], 1].sum()) for i in range(self.C))
-        return dict(blocks=int(nb.sum()), crc_ok=ok, bursts=int(self.nburst.sum().item()))
-
-    def cpu_baseline(self, budget_s):
-        """The C oracle (demod + lower MAC) on the host: one thread for a third of the budget, then
-        every host thread this box grants (OMP_NUM_THREADS, 16 on a one-GPU box) in a thread pool --
-        the oracle's C calls release the GIL, so the pool scales; threads, not processes, because
-        this process has initialised the GPU."""
-        import concurrent.futures
-        import os
-        import sys
-        import time
-        repo = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
-        sys.path.insert(0, os.path.join(repo, "oracle"))
-        import etsi as oracle   # the CPU restatement (cpu_baseline leg only)
-        x = self.iq[:4].float().cpu().numpy()
-        if self.fmt == _hip.TETRA_SC16:
-            x = x / 32768   # the oracle filters cf32; SC16 -> cf32 is exact
-        x = np.ascontiguousarray(x, np.float32).view(np.complex64)[..., 0]
-        cells = self.cells[:4].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
-
-        def worker(deadline, k0):
-            rx = oracle.Receiver(self.fs)
-            n = 0
-            while time.perf_counter() < deadline:
-                sym, soft, hard, _ = rx.demod(x[(k0 + n) % 4])
-                rx.lower_mac(soft, hard, int(cells[(k0 + n) % 4]))
-                n += 1
-            return n
-
-        t0 = time.perf_counter()
-        n1 = worker(t0 + budget_s / 3, 0)
-        v1 = n1 * self.N / (time.perf_counter() - t0) / 1e6
-        threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16")), len(os.sched_getaffinity(0)), 64))
-        t1 = time.perf_counter()
-        deadline = t1 + 2 * budget_s / 3
-        with concurrent.futures.ThreadPoolExecutor(threads) as ex:
-            counts = list(ex.map(lambda k: worker(deadline, k), range(threads)))
-        vt = sum(counts) * self.N / (time.perf_counter() - t1) / 1e6
-        return dict(value=vt, unit="Msamples/s", cores=threads, kind="port", single_thread_value=v1,
-                    sample=f"{sum(counts)} channel chunks x {self.N} cf32 @2.4 MSps through the C oracle "
-                           f"(chanfilt+timing+sync+Viterbi) on {threads} threads in {2 * budget_s / 3:.0f} s; "
-                           f"single thread: {n1} chunks, {v1:.1f} Msamples/s")
+        q = dict(blocks=int(nb.sum()), crc_ok=ok, bursts=int(self.nburst.sum().item()))
+        if self.cells_mode == "acquire":
+            q["cells_acquired"] = int((self.cell_state == self.cells).sum().item())
+        return q
 
 
 def smoke_check():

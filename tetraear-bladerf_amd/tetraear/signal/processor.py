@@ -9,11 +9,15 @@ device, the first numeric call raises ``TetraHipError``.
 
 ``mode="etsi"`` selects the ETSI EN 300 392-2 receiver (polyphase RRC channel filter, Gardner
 timing recovery, correct pi/4-DQPSK decision with soft bits) instead of the reference-compatible
-("compat") chain; see tetraear.signal.etsi.
+("compat") chain; see tetraear.signal.etsi.  Callers that construct ``SignalProcessor(sample_rate)``
+unchanged (/root/reference/tetraear/ui/modern.py:1886, scanner.py:164) pick the chain with the
+environment: ``TETRAEAR_DEMOD=compat|etsi`` (default compat).  ``TETRAEAR_BACKEND`` may only be
+``hip`` (the default): this build has no CPU path.
 """
 import functools
 import logging
 import math
+import os
 
 import numpy as np
 from scipy import signal as _design   # filter DESIGN only (coefficients), as the reference does
@@ -26,6 +30,18 @@ SYMBOL_RATE = 18000
 TARGET_RATE = 240000
 # decision thresholds evaluated exactly as processor.py:152-158 writes them
 THRESHOLDS = (-5 * np.pi / 8, -3 * np.pi / 8, 3 * np.pi / 8, 5 * np.pi / 8)
+
+
+def demod_mode(mode=None):
+    """The chain a SignalProcessor / TetraDecoder runs: `mode`, else $TETRAEAR_DEMOD, else compat."""
+    m = mode if mode is not None else os.environ.get("TETRAEAR_DEMOD", "compat")
+    if m not in ("compat", "etsi"):
+        raise ValueError(f"mode / TETRAEAR_DEMOD must be 'compat' or 'etsi', not {m!r}")
+    backend = os.environ.get("TETRAEAR_BACKEND", "hip")
+    if backend != "hip":
+        raise _hip.TetraHipError(f"TETRAEAR_BACKEND={backend!r}: this build computes on the GPU only (hip); "
+                                 f"the CPU path is the reference itself")
+    return m
 
 
 def _fmt_of(x):
@@ -113,14 +129,12 @@ def mixer_coefficient(freq_offset):
 class SignalProcessor:
     """Processes raw IQ samples for TETRA demodulation (processor.py:18)."""
 
-    def __init__(self, sample_rate=2.4e6, mode="compat"):
+    def __init__(self, sample_rate=2.4e6, mode=None):
         self.sample_rate = sample_rate
         self.symbol_rate = SYMBOL_RATE
         self.samples_per_symbol = int(sample_rate / self.symbol_rate)
         self.symbols = None
-        if mode not in ("compat", "etsi"):
-            raise ValueError("mode must be 'compat' or 'etsi'")
-        self.mode = mode
+        self.mode = demod_mode(mode)
         self._etsi = None
 
     # --------------------------------------------------------------- component methods
@@ -146,7 +160,15 @@ class SignalProcessor:
         return y.real.copy() if real else y
 
     def filter_signal(self, samples, bandwidth=25000, sample_rate=None):
-        """Butterworth-4 filtfilt low-pass (processor.py:51-83), on the GPU."""
+        """Butterworth-4 filtfilt low-pass (processor.py:51-83), on the GPU.
+
+        ETSI mode: the receiver's channel filter instead -- 2.4 MSps in, the RRC(0.35)-matched
+        72 kHz samples (4 per symbol) out (`bandwidth` is fixed at the TETRA channel's)."""
+        if self.mode == "etsi":
+            fs = sample_rate if sample_rate is not None else self.sample_rate
+            if fs != self.sample_rate:
+                raise ValueError("ETSI mode filters the receiver's own input rate")
+            return self._etsi_rx().chanfilt(samples)
         if len(samples) == 0:
             return samples
         fs = sample_rate if sample_rate is not None else self.sample_rate
@@ -187,7 +209,10 @@ class SignalProcessor:
         return out
 
     def demodulate_dqpsk(self, samples):
-        """Differential decision with the reference's thresholds (processor.py:102-166)."""
+        """Differential decision with the reference's thresholds (processor.py:102-166).
+
+        ETSI mode: the Table 5.1 decision regions of the docstring at processor.py:106-110
+        (00 +pi/4, 01 +3pi/4, 11 -3pi/4, 10 -pi/4) on the given symbols (tetra_etsi_decide)."""
         if self.mode == "etsi":
             return self._etsi_rx().decide(samples)
         if len(samples) < 2:
@@ -203,7 +228,15 @@ class SignalProcessor:
         return out
 
     def extract_symbols(self, samples, sample_rate=None):
-        """Best integer sampling phase by mean power, then decimate (processor.py:168-219)."""
+        """Best integer sampling phase by mean power, then decimate (processor.py:168-219).
+
+        ETSI mode: timing recovery (Oerder-Meyr + block Gardner) on the channel filter's 72 kHz
+        samples (sample_rate 72000), or on raw input at the receiver's rate (filtered first)."""
+        if self.mode == "etsi":
+            fs = sample_rate if sample_rate is not None else 72000.0
+            x = np.asarray(samples)
+            y = x if fs == 72000.0 else self.filter_signal(x, sample_rate=fs)
+            return self._etsi_rx().timing(y)[1]
         if len(samples) == 0:
             return np.array([], dtype=complex)
         fs = sample_rate if sample_rate is not None else self.sample_rate

@@ -247,35 +247,6 @@ class BenchStep:
     def workload_key(self):
         return f"C3: {self.Nw} samples"   # a substring of config()["workload"]
 
-    def cpu_baseline(self, budget_s):
-        import os
-        import sys
-        import time
-        repo = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
-        sys.path.insert(0, os.path.join(repo, "oracle"))
-        import etsi as E   # the CPU restatements (cpu_baseline leg only)
-        import wideband as W
-        d = W.design(self.fs, self.plan.M)
-        nw = (self.m2 * DOWN) // UP * self.plan.D + self.plan.M * P_WB + 64 * self.plan.D   # one chunk per carrier
-        x = self.x[:nw].cpu().numpy().view(np.complex64)[:, 0]
-        t0 = time.perf_counter()
-        y = W.channelize(x.astype(np.complex128), d, self.m2).astype(np.complex64)
-        t_ch = time.perf_counter() - t0
-        cells = self.cells[::self.nchunk].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
-        rx = E.Receiver()
-        t1 = time.perf_counter()
-        k = 0
-        while k < self.plan.M and (k < 8 or time.perf_counter() - t0 < budget_s):
-            sym, soft, hard, _ = rx.timing(y[k])
-            rx.lower_mac(soft, hard, int(cells[k]))
-            k += 1
-        t_c = (time.perf_counter() - t1) / k
-        total = t_ch + self.plan.M * t_c
-        return dict(value=nw / total / 1e6, unit="Msamples/s", cores=1, kind="port",
-                    sample=f"{nw} samples @{self.fs / 1e6:g} MSps: numpy float64 channeliser ({t_ch:.2f} s) + C "
-                           f"oracle timing+lower MAC on {k} of {self.plan.M} carriers (x{self.plan.M / k:.1f} "
-                           f"extrapolated), 1 thread")
-
     def quality(self):
         nb = self.nblock.cpu().numpy()
         blocks = self.blocks.cpu().numpy()

@@ -1,13 +1,16 @@
 #!/bin/bash
-# GPU-box check: parity tests, smoke, default bench, wideband bench.  Every GPU step is time-limited
-# and the steps are chained (set -e), so a fault or timeout ends the call.
+# GPU-box check: parity tests, smoke, default bench, wideband bench; PROFILE=tag adds the rocprof
+# passes of the default bench (tools/profile_bench.sh).  Every GPU step is time-limited and the steps
+# are chained (set -e), so a fault or timeout ends the call.
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p $O
 cd $R
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 timeout -k 10 300 python -u bench.py > $O/bench_etsi.log 2>&1
-timeout -k 10 300 python -u bench.py --chain wideband --no-cpu "$@" > $O/bench_wb.log 2>&1
+timeout -k 10 300 python -u bench.py --no-cpu --cells given > $O/bench_etsi_given.log 2>&1
+timeout -k 10 300 python -u bench.py --chain wideband --no-cpu > $O/bench_wb.log 2>&1
+if [ -n "$PROFILE" ]; then bash tools/profile_bench.sh $PROFILE; fi
 echo done

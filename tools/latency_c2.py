@@ -48,7 +48,7 @@ def main():
 
     p = SignalProcessor(fs, mode="etsi")
     d = TetraDecoder(mode="etsi")
-    d._etsi_rx().cell = int(cells[0])
+    d._etsi_rx().cell_state = np.array([cells[0]], np.uint32)   # as if acquired from an earlier chunk
     x = np.ascontiguousarray(iq[0])
     out["etsi_process_ms"] = med_ms(lambda: p.process(x), a.reps)
     hard = p.process(x)
