@@ -499,21 +499,57 @@ __global__ __launch_bounds__(256, cf_waves<In>()) void k_chanfilt(const In *__re
         if (k >= 0 && k < M1) {
             const float4 *w = xin + 5 * tid + 4;
             pf2 a = {0.f, 0.f};
-            if constexpr (YL) {
+            if constexpr (YL) {   // three groups of 16 taps, the next group's reads in flight (k_chanfilt_w)
+                float4 ta[4], xa[8], tb[4], xb[8];
+                auto rd = [&](float4 (&T)[4], float4 (&X)[8], int g) __attribute__((always_inline)) {
 #pragma unroll
-                for (int q = 0; q < 12; ++q) {
-                    const float4 t4 = htap[q], x0 = w[2 * q], x1 = w[2 * q + 1];
-                    a = pfma(t4.x, pf2{x0.x, x0.y}, a);
-                    a = pfma(t4.y, pf2{x0.z, x0.w}, a);
-                    a = pfma(t4.z, pf2{x1.x, x1.y}, a);
-                    a = pfma(t4.w, pf2{x1.z, x1.w}, a);
-                }
-            } else {   // SC16 keeps the scalar taps (VGPR budget, below)
+                    for (int i = 0; i < 4; ++i) {
+                        T[i] = htap[4 * g + i];
+                        X[2 * i] = w[8 * g + 2 * i];
+                        X[2 * i + 1] = w[8 * g + 2 * i + 1];
+                    }
+                };
+                auto fm = [&](const float4 (&T)[4], const float4 (&X)[8]) __attribute__((always_inline)) {
 #pragma unroll
-                for (int jj = 0; jj < 24; ++jj) {
-                    const float4 v = w[jj];
-                    a = pfma(h1[2 * jj], pf2{v.x, v.y}, a);
-                    a = pfma(h1[2 * jj + 1], pf2{v.z, v.w}, a);
+                    for (int i = 0; i < 4; ++i) {
+                        const float4 t4 = T[i], x0 = X[2 * i], x1 = X[2 * i + 1];
+                        a = pfma(t4.x, pf2{x0.x, x0.y}, a);
+                        a = pfma(t4.y, pf2{x0.z, x0.w}, a);
+                        a = pfma(t4.z, pf2{x1.x, x1.y}, a);
+                        a = pfma(t4.w, pf2{x1.z, x1.w}, a);
+                    }
+                };
+                rd(ta, xa, 0);
+                rd(tb, xb, 1);
+                __builtin_amdgcn_sched_barrier(0);
+                fm(ta, xa);
+                __builtin_amdgcn_sched_barrier(0);
+                rd(ta, xa, 2);
+                __builtin_amdgcn_sched_barrier(0);
+                fm(tb, xb);
+                __builtin_amdgcn_sched_barrier(0);
+                fm(ta, xa);
+            } else {
+                // SC16 (128-VGPR budget): the taps from LDS too (scalar taps were re-loaded by an
+                // s_load with lgkmcnt(0) inside the chain), the next tap quad's reads in flight
+                float4 tq[2], x0[2], x1[2];
+                tq[0] = htap[0];
+                x0[0] = w[0];
+                x1[0] = w[1];
+#pragma unroll
+                for (int g = 0; g < 12; ++g) {
+                    if (g + 1 < 12) {
+                        tq[(g + 1) & 1] = htap[g + 1];
+                        x0[(g + 1) & 1] = w[2 * g + 2];
+                        x1[(g + 1) & 1] = w[2 * g + 3];
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    const float4 T = tq[g & 1], X0 = x0[g & 1], X1 = x1[g & 1];
+                    a = pfma(T.x, pf2{X0.x, X0.y}, a);
+                    a = pfma(T.y, pf2{X0.z, X0.w}, a);
+                    a = pfma(T.z, pf2{X1.x, X1.y}, a);
+                    a = pfma(T.w, pf2{X1.z, X1.w}, a);
+                    __builtin_amdgcn_sched_barrier(0);
                 }
             }
             lin[k - kbase] = make_float2(a.x, a.y);
@@ -777,14 +813,38 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_w(const float4 *__restrict_
         if (k >= K0 && k < K1) {
             const float4 *w = xw + 5 * lane + 4;
             pf2 a = {0.f, 0.f};
+            // the 48-tap chain in three groups of 16 taps (4 tap quads + 8 sample pairs each), the
+            // next group's LDS reads in flight during this group's FMAs: left to itself hipcc keeps
+            // two reads ahead of the chain, one LDS round trip per two FMAs (~24 per tile)
+            float4 ta[4], xa[8], tb[4], xb[8];
+            auto rd = [&](float4 (&T)[4], float4 (&X)[8], int g) __attribute__((always_inline)) {
 #pragma unroll
-            for (int q = 0; q < 12; ++q) {
-                const float4 t4 = htap[q], x0 = w[2 * q], x1 = w[2 * q + 1];
-                a = pfma(t4.x, pf2{x0.x, x0.y}, a);
-                a = pfma(t4.y, pf2{x0.z, x0.w}, a);
-                a = pfma(t4.z, pf2{x1.x, x1.y}, a);
-                a = pfma(t4.w, pf2{x1.z, x1.w}, a);
-            }
+                for (int i = 0; i < 4; ++i) {
+                    T[i] = htap[4 * g + i];
+                    X[2 * i] = w[8 * g + 2 * i];
+                    X[2 * i + 1] = w[8 * g + 2 * i + 1];
+                }
+            };
+            auto fm = [&](const float4 (&T)[4], const float4 (&X)[8]) __attribute__((always_inline)) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float4 t4 = T[i], x0 = X[2 * i], x1 = X[2 * i + 1];
+                    a = pfma(t4.x, pf2{x0.x, x0.y}, a);
+                    a = pfma(t4.y, pf2{x0.z, x0.w}, a);
+                    a = pfma(t4.z, pf2{x1.x, x1.y}, a);
+                    a = pfma(t4.w, pf2{x1.z, x1.w}, a);
+                }
+            };
+            rd(ta, xa, 0);
+            rd(tb, xb, 1);
+            __builtin_amdgcn_sched_barrier(0);
+            fm(ta, xa);
+            __builtin_amdgcn_sched_barrier(0);
+            rd(ta, xa, 2);
+            __builtin_amdgcn_sched_barrier(0);
+            fm(tb, xb);
+            __builtin_amdgcn_sched_barrier(0);
+            fm(ta, xa);
             lin[k - kbase] = make_float2(a.x, a.y);
             if (wv > 0 && k - K0 < SEAM) seam[(wv - 1) * SEAM + k - K0] = make_float2(a.x, a.y);
         }

@@ -13,4 +13,10 @@ timeout -k 10 300 python -u bench.py > $O/bench_etsi.log 2>&1
 timeout -k 10 300 python -u bench.py --no-cpu --cells given > $O/bench_etsi_given.log 2>&1
 timeout -k 10 300 python -u bench.py --chain wideband --no-cpu > $O/bench_wb.log 2>&1
 if [ -n "$PROFILE" ]; then bash tools/profile_bench.sh $PROFILE; fi
+# AB="libA.so libB.so": same-box A/B of library variants, pipelined and serial cf32, pipelined SC16
+if [ -n "$AB" ]; then
+  AB_ARGS=" " bash tools/ab_demod.sh $AB > $O/ab_pipe.txt 2>&1
+  AB_ARGS="--pipeline off" bash tools/ab_demod.sh $AB > $O/ab_serial.txt 2>&1
+  AB_ARGS="--iq sc16" bash tools/ab_demod.sh $AB > $O/ab_sc16.txt 2>&1
+fi
 echo done
