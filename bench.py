@@ -65,9 +65,11 @@ def parse():
     ap.add_argument("--host-input", action="store_true",
                     help="etsi: PCIe-inclusive mode -- each batch is copied from pinned host memory (double-buffered "
                          "copy stream); value is then the host-fed rate, never the HBM-resident headline")
-    ap.add_argument("--cells", choices=("acquire", "given"), default="acquire",
-                    help="etsi: the lower MAC acquires each channel's cell from its BSCH (colour code 0 first, "
-                         "state kept across steps) or is given the synthesised cells")
+    ap.add_argument("--cells", choices=("acquire", "given"), default="given",
+                    help="etsi: the lower MAC is given each channel's cell (as acquired by a streaming receiver "
+                         "from an earlier chunk), or acquires it from the batch's own BSCH (colour code 0 first, "
+                         "state kept across steps; channels whose chunk has no sync burst never acquire, "
+                         "because every step re-decodes the same batch)")
     ap.add_argument("--demod", choices=("fused", "split"), default="fused",
                     help="etsi: fused channel filter + timing in one launch, or split (y through HBM, timing "
                          "launched separately -- beside the next batch's channel filter when pipelined)")

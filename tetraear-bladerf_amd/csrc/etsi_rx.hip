@@ -85,26 +85,7 @@ __device__ __forceinline__ float pat2(float y, float x) {
     return r;
 }
 
-// Cubic Lagrange interpolation of y at t (y[n] at w[n - w0]).
-__device__ __forceinline__ float2 interp(const float2 *w, int w0, float t) {
-    const float K6 = 1.0f / 6.0f;
-    const float fi = floorf(t);
-    const int i = (int)fi;
-    const float f = t - fi;
-    const float fm1 = f - 1.0f, fm2 = f - 2.0f, fp1 = f + 1.0f;
-    const float cm = -(f * fm1 * fm2) * K6;
-    const float c0 = (fp1 * fm1 * fm2) * 0.5f;
-    const float c1 = -(fp1 * f * fm2) * 0.5f;
-    const float c2 = (fp1 * f * fm1) * K6;
-    const float2 a = w[i - 1 - w0], b = w[i - w0], c = w[i + 1 - w0], d = w[i + 2 - w0];
-    float r = cm * a.x, q = cm * a.y;
-    r = fmaf(c0, b.x, r); q = fmaf(c0, b.y, q);
-    r = fmaf(c1, c.x, r); q = fmaf(c1, c.y, q);
-    r = fmaf(c2, d.x, r); q = fmaf(c2, d.y, q);
-    return make_float2(r, q);
-}
-
-// interp(w, w0, t) and interp(w, w0, t - 2) together: t - 2 is exact here (t < 2^22), so both share
+// Cubic Lagrange interpolation of y (y[n] at w[n - w0]) at t and at t - 2 together: t - 2 is exact here (t < 2^22), so both share
 // the fraction f and the four Lagrange weights -- computed once, the same bits either way.
 __device__ __forceinline__ void interp_pair(const float2 *w, int w0, float t, float2 &on, float2 &mid) {
     const float K6 = 1.0f / 6.0f;
@@ -155,10 +136,19 @@ struct TrackOut {
 
 constexpr int CPOL_SC1 = 16;   // gfx940+ cache-policy bits: sc0 1, nt 2, sc1 16 (copy_out)
 
+// SPLIT: the CFO sums are left to a second wave (cfo_consumer) that follows the tracking through
+// the LDS progress word *prog (symbols done | PROG_DONE at the end): off the serial tracking chain.
+constexpr int PROG_DONE = 1 << 30;
+template <bool SPLIT = false>
 __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float gain, float soft_scale, float2 *sp,
-                                                 float2 *dp, int smax, int lane) {
+                                                 float2 *dp, int smax, int lane, int *prog = nullptr) {
     TrackOut o{0, 1.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-    if (M2 < 16) return o;
+    if (M2 < 16) {
+        if constexpr (SPLIT) {
+            if (lane == 0) __hip_atomic_store(prog, PROG_DONE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        return o;
+    }
     // Oerder-Meyr: class sums of |y|^2 over n mod 4 (loads issued 8 ahead; same summation order)
     float s = 0.f;
     for (int n0 = lane; n0 < M2; n0 += 8 * 64) {
@@ -201,12 +191,14 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
                 const int j = S + lane;
                 const float xr = fmaf(on.x, pv.x, on.y * pv.y), xi = fmaf(on.y, pv.x, -(on.x * pv.y));
                 dp[j - 1] = make_float2(xr, xi);
-                // CFO: 4th power and magnitude of d_j (j = lane mod 64, ascending: the oracle's order)
-                const float sr = fmaf(xr, xr, -(xi * xi)), si = (xr * xi) * 2.0f;
-                const float qr = fmaf(sr, sr, -(si * si)), qi = (sr * si) * 2.0f;
-                zr += qr;
-                zi += qi;
-                am += sqrtf(fmaf(xr, xr, xi * xi));
+                if constexpr (!SPLIT) {
+                    // CFO: 4th power and magnitude of d_j (j = lane mod 64, ascending: the oracle's order)
+                    const float sr = fmaf(xr, xr, -(xi * xi)), si = (xr * xi) * 2.0f;
+                    const float qr = fmaf(sr, sr, -(si * si)), qi = (sr * si) * 2.0f;
+                    zr += qr;
+                    zi += qi;
+                    am += sqrtf(fmaf(xr, xr, xi * xi));
+                }
             }
             sp[S + lane] = on;
         }
@@ -219,8 +211,16 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
             have_prev = true;
         }
         S += nv;
+        if constexpr (SPLIT) {   // d_j, j < S, are in dp: release them to the CFO wave
+            if (lane == 0)
+                __hip_atomic_store(prog, S | (nv < 64 ? PROG_DONE : 0), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         if (nv < 64) break;
     }
+    o.S = S;
+    o.base = base;
+    o.delta = delta;
+    if constexpr (SPLIT) return o;   // rr, ri, sc: cfo_consumer's
     // CFO rotation conj((-Z/|Z|)^(1/4)) and the soft scale from the mean |d|
     const float Zr = wave_sum(zr), Zi = wave_sum(zi), A = wave_sum(am);
     float rr = 1.0f, ri = 0.0f;
@@ -231,13 +231,51 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
         rr = w.x;
         ri = -w.y;
     }
-    o.S = S;
     o.rr = rr;
     o.ri = ri;
     o.sc = (S > 1 && A > 0.0f) ? soft_scale / (A / (float)(S - 1)) : 0.0f;
-    o.base = base;
-    o.delta = delta;
     return o;
+}
+
+// The CFO half of timing_track<false>, on a second wave while timing_track<true> tracks: lane l
+// sums the 4th powers and magnitudes of d_j, j = l mod 64, block after block as the progress word
+// releases them -- the same per-lane order, so the same bits -- then the rotation and the soft
+// scale into *o (rr, ri, sc).
+__device__ __forceinline__ void cfo_consumer(const float2 *dp, float soft_scale, int *prog, TrackOut *o, int lane) {
+    float zr = 0.f, zi = 0.f, am = 0.f;
+    int jb = 0, S = 0;
+    for (;;) {
+        const int v = __hip_atomic_load(prog, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        S = v & (PROG_DONE - 1);
+        for (; jb < S; jb += 64) {
+            const int j = jb + lane;
+            if (j >= 1 && j < S) {
+                const float2 d = dp[j - 1];
+                const float xr = d.x, xi = d.y;
+                const float sr = fmaf(xr, xr, -(xi * xi)), si = (xr * xi) * 2.0f;
+                const float qr = fmaf(sr, sr, -(si * si)), qi = (sr * si) * 2.0f;
+                zr += qr;
+                zi += qi;
+                am += sqrtf(fmaf(xr, xr, xi * xi));
+            }
+        }
+        if (v & PROG_DONE) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    const float Zr = wave_sum(zr), Zi = wave_sum(zi), A = wave_sum(am);
+    float rr = 1.0f, ri = 0.0f;
+    const float zm = sqrtf(fmaf(Zr, Zr, Zi * Zi));
+    if (zm > 0.0f) {
+        const float2 v = csqrt_p(-Zr / zm, -Zi / zm);
+        const float2 w = csqrt_p(v.x, v.y);
+        rr = w.x;
+        ri = -w.y;
+    }
+    if (lane == 0) {
+        o->rr = rr;
+        o->ri = ri;
+        o->sc = (S > 1 && A > 0.0f) ? soft_scale / (A / (float)(S - 1)) : 0.0f;
+    }
 }
 
 // Decision pass over d_j, j in [1, S): wave w of nw takes the 64-symbol blocks w, w + nw, ...
@@ -395,21 +433,27 @@ struct TailStage {
 // the tracking is the serial tail (wave 0, prioritised on its SIMD); the decision pass after it is
 // shared by all four waves (the rotation and scale go through LDS, *tro).
 __device__ __forceinline__ void timing_tail(const float2 *ly, float2 *scr, const TimingOut &to, int M2, int ch,
-                                            int tid, TrackOut *tro, const TailStage *stage = nullptr) {
+                                            int tid, TrackOut *tro, int *prog, const TailStage *stage = nullptr) {
     const size_t so = (size_t)ch * to.smax;
+    if (tid == 0) *prog = 0;
+    __syncthreads();
     if (tid < 64) {
         __builtin_amdgcn_s_setprio(3);
         // S <= M2 / 4 + 1 < the staging size either way: the bound only guards the LDS buffer
-        const TrackOut o = timing_track(ly, M2, to.gain, to.soft_scale, stage ? stage->sym : to.sym + so, scr,
-                                        stage ? min(to.smax, M2 / 4 + 2) : to.smax, tid);
+        const TrackOut o = timing_track<true>(ly, M2, to.gain, to.soft_scale, stage ? stage->sym : to.sym + so, scr,
+                                              stage ? min(to.smax, M2 / 4 + 2) : to.smax, tid, prog);
         if (tid == 0) {
-            *tro = o;
+            tro->S = o.S;
+            tro->base = o.base;
+            tro->delta = o.delta;
             to.nsym[ch] = o.S;
-            if (to.diag && M2 >= 16) to.diag[ch] = make_float4(o.base, o.delta, o.rr, o.ri);
         }
+    } else if (tid < 128) {
+        cfo_consumer(scr, to.soft_scale, prog, tro, tid & 63);
     }
     __syncthreads();
     const TrackOut o = *tro;
+    if (tid == 0 && to.diag && M2 >= 16) to.diag[ch] = make_float4(o.base, o.delta, o.rr, o.ri);
     if (!stage) {
         timing_decide(o, scr, to.softbits + 2 * so, to.hard + so, tid >> 6, 4, tid & 63);
         return;
@@ -529,27 +573,13 @@ __global__ __launch_bounds__(256, cf_waves<In>()) void k_chanfilt(const In *__re
                 fm(tb, xb);
                 __builtin_amdgcn_sched_barrier(0);
                 fm(ta, xa);
-            } else {
-                // SC16 (128-VGPR budget): the taps from LDS too (scalar taps were re-loaded by an
-                // s_load with lgkmcnt(0) inside the chain), the next tap quad's reads in flight
-                float4 tq[2], x0[2], x1[2];
-                tq[0] = htap[0];
-                x0[0] = w[0];
-                x1[0] = w[1];
+            } else {   // SC16 keeps the scalar taps (VGPR budget, below; LDS taps read two quads ahead
+                       // of the chain measured 3 % slower: 1.20 -> 1.24 ms per pipelined SC16 step)
 #pragma unroll
-                for (int g = 0; g < 12; ++g) {
-                    if (g + 1 < 12) {
-                        tq[(g + 1) & 1] = htap[g + 1];
-                        x0[(g + 1) & 1] = w[2 * g + 2];
-                        x1[(g + 1) & 1] = w[2 * g + 3];
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                    const float4 T = tq[g & 1], X0 = x0[g & 1], X1 = x1[g & 1];
-                    a = pfma(T.x, pf2{X0.x, X0.y}, a);
-                    a = pfma(T.y, pf2{X0.z, X0.w}, a);
-                    a = pfma(T.z, pf2{X1.x, X1.y}, a);
-                    a = pfma(T.w, pf2{X1.z, X1.w}, a);
-                    __builtin_amdgcn_sched_barrier(0);
+                for (int jj = 0; jj < 24; ++jj) {
+                    const float4 v = w[jj];
+                    a = pfma(h1[2 * jj], pf2{v.x, v.y}, a);
+                    a = pfma(h1[2 * jj + 1], pf2{v.z, v.w}, a);
                 }
             }
             lin[k - kbase] = make_float2(a.x, a.y);
@@ -676,7 +706,8 @@ __global__ __launch_bounds__(256, cf_waves<In>()) void k_chanfilt(const In *__re
             scr = yl + M2;
         }
         __shared__ TrackOut tro;
-        timing_tail(ly, scr, to, M2, ch, tid, &tro);
+        __shared__ int prog;
+        timing_tail(ly, scr, to, M2, ch, tid, &tro, &prog);
     } else if constexpr (YL) {
         flush(M2);
     }
@@ -706,7 +737,7 @@ constexpr int WSMEM4 = 14 + 4 * WIMG4 + (4 * WLR + 3 * SEAM + YLDS) / 2;   // fl
 // two workgroups per CU with >= 9.5 KB of the CU's LDS left for the lower MAC's kernels
 // (k_etsi_viterbi 7 KB, k_etsi_sync 2.4 KB), which the bench's pipeline runs beside the next demod
 static_assert(2 * WSMEM4 * 16 + 7 * 1024 + 2560 <= 160 * 1024, "per-wave demod LDS");
-static_assert(sizeof(TrackOut) <= 32 && (4 * WLR + 3 * SEAM) % 2 == 0, "per-wave demod LDS carving");
+static_assert(sizeof(TrackOut) + sizeof(int) <= 32 && (4 * WLR + 3 * SEAM) % 2 == 0, "per-wave demod LDS carving");
 // fused tail staging: sm symbols in the stage-1 buffers; 8 sm (d_j) + 2 sm + sm bytes in the images
 constexpr int WTAIL_SM = YLDS / 4 + 2;
 static_assert(WTAIL_SM * 8 <= 4 * WLR * 8 && 11 * WTAIL_SM + 32 <= 4 * WIMG4 * 16, "tail staging LDS");
@@ -901,7 +932,9 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_w(const float4 *__restrict_
         const int sm = M2 / 4 + 2;
         int8_t *ib = reinterpret_cast<int8_t *>(img);
         const TailStage st{lin_all, ib + ((8 * sm + 15) & ~15), reinterpret_cast<uint8_t *>(ib + ((10 * sm + 31) & ~15))};
-        timing_tail(reinterpret_cast<const float2 *>(yb), reinterpret_cast<float2 *>(img), to, M2, ch, tid, tro, &st);
+        int *prog = reinterpret_cast<int *>(tro + 1);   // the word after TrackOut in its 32-B slot
+        timing_tail(reinterpret_cast<const float2 *>(yb), reinterpret_cast<float2 *>(img), to, M2, ch, tid, tro, prog,
+                    &st);
     } else {
         copy_out(reinterpret_cast<uint8_t *>(y + (size_t)ch * M2), reinterpret_cast<const uint8_t *>(yb), 8 * M2, tid);
     }
@@ -922,13 +955,6 @@ constexpr int YB[38] = {1, 1, 0, 0, 0, 0, 0, 1, 1, 0, 0, 1, 1, 1, 0, 0, 1, 1, 1,
 constexpr uint64_t W_HEAD = packb(QB + 10, 12), W_TAIL = packb(QB, 10), W_N = packb(NB, 22), W_P = packb(PB, 22),
                    W_Y = packb(YB, 38);
 
-__device__ __forceinline__ uint64_t bits_at(const uint64_t *w, int pos, int len) {
-    // branch-free: (x << 1) << (63 - r) is x << (64 - r) for r > 0 and 0 for r = 0 (a per-lane
-    // `if (r)` here made every extraction a divergent branch in the burst scan)
-    const int q = pos >> 6, r = pos & 63;
-    const uint64_t v = (w[q] >> r) | ((w[q + 1] << 1) << (63 - r));
-    return len == 64 ? v : (v & ((1ull << len) - 1));
-}
 // up to 32 stream bits from pos, from the 32-bit view of the words: one funnel shift
 __device__ __forceinline__ uint32_t bits32_at(const uint32_t *w, int pos) {
     const int q = pos >> 5;
@@ -937,10 +963,6 @@ __device__ __forceinline__ uint32_t bits32_at(const uint32_t *w, int pos) {
 __device__ __forceinline__ int matches32(uint32_t v, uint32_t pat, int len) {
     return len - __popc((v ^ pat) & (len == 32 ? 0xFFFFFFFFu : ((1u << len) - 1)));
 }
-__device__ __forceinline__ int matches(uint64_t v, uint64_t pat, int len) {
-    return len - __popcll((v ^ pat) & ((1ull << len) - 1));
-}
-
 __device__ __forceinline__ int punct_index(int j1) {   // rate 2/3, t=3, P=(1,2,5); 1-based
     const int g = (j1 - 1) / 3;
     const int r = j1 - 3 * g;

@@ -193,7 +193,7 @@ class BenchStep:
 
     dtype = "f32 (DSP), int8/int32 (Viterbi)"
 
-    def __init__(self, c, C, N, fs, seed, device, snr_db=18.0, iq_format="cf32", demod="fused", cells="acquire"):
+    def __init__(self, c, C, N, fs, seed, device, snr_db=18.0, iq_format="cf32", demod="fused", cells="given"):
         import torch
         self.c, self.C, self.N, self.fs = c, C, N, fs
         # "acquire": the lower MAC finds each channel's cell in its BSCH (tetra_lmac_etsi_acquire,

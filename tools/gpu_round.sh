@@ -7,7 +7,10 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p $O
 cd $R
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
+# test failures (rc 1) do not stop the call; anything else (a fault, a timeout, a crash) does
+rc=0
+timeout -k 10 500 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || rc=$?
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 timeout -k 10 300 python -u bench.py > $O/bench_etsi.log 2>&1
 timeout -k 10 300 python -u bench.py --no-cpu --cells given > $O/bench_etsi_given.log 2>&1
@@ -16,7 +19,7 @@ if [ -n "$PROFILE" ]; then bash tools/profile_bench.sh $PROFILE; fi
 # AB="libA.so libB.so": same-box A/B of library variants, pipelined and serial cf32, pipelined SC16
 if [ -n "$AB" ]; then
   AB_ARGS=" " bash tools/ab_demod.sh $AB > $O/ab_pipe.txt 2>&1
-  AB_ARGS="--pipeline off" bash tools/ab_demod.sh $AB > $O/ab_serial.txt 2>&1
+  if [ -n "$AB_SERIAL" ]; then AB_ARGS="--pipeline off" bash tools/ab_demod.sh $AB > $O/ab_serial.txt 2>&1; fi
   AB_ARGS="--iq sc16" bash tools/ab_demod.sh $AB > $O/ab_sc16.txt 2>&1
 fi
 echo done
