@@ -68,6 +68,26 @@ __device__ __forceinline__ float bfly(float v) {
     return v;
 }
 __device__ __forceinline__ float wave_sum(float v) { return bfly<1>(v); }
+// two full butterflies level by level, interleaved: the Gardner block's error and power sums are
+// one dependent chain each, and issued one after the other they doubled the loop's reduction latency
+__device__ __forceinline__ void wave_sum2(float &u, float &v) {
+    const auto a0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(u), __float_as_uint(u), false, false);
+    const auto a1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    u = __uint_as_float(a0[0]) + __uint_as_float(a0[1]);
+    v = __uint_as_float(a1[0]) + __uint_as_float(a1[1]);
+    const auto b0 = __builtin_amdgcn_permlane16_swap(__float_as_uint(u), __float_as_uint(u), false, false);
+    const auto b1 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    u = __uint_as_float(b0[0]) + __uint_as_float(b0[1]);
+    v = __uint_as_float(b1[0]) + __uint_as_float(b1[1]);
+    u = u + dppf<0x128>(u);
+    v = v + dppf<0x128>(v);
+    u = u + dppf<0x124>(u);
+    v = v + dppf<0x124>(v);
+    u = u + dppf<0x4E>(u);
+    v = v + dppf<0x4E>(v);
+    u = u + dppf<0xB1>(u);
+    v = v + dppf<0xB1>(v);
+}
 __device__ __forceinline__ float lane_f(float v, int l) {   // wave-uniform l
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
@@ -203,7 +223,8 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
             sp[S + lane] = on;
         }
         if (nv > 0) {
-            const float E = wave_sum(ev), W = wave_sum(pw);
+            float E = ev, W = pw;
+            wave_sum2(E, W);
             if (W > 0.0f) delta = delta - gain * (E / W);
             if (delta > 1.5f) delta = 1.5f;
             if (delta < -1.5f) delta = -1.5f;
