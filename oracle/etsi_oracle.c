@@ -272,11 +272,22 @@ int eo_timing(const float *y, int M2, float gain, float soft_scale, float *soft_
               uint8_t *hard, int smax, float *diag)
 {
     if (M2 < 16) return 0;
-    /* Oerder-Meyr: lane l accumulates |y[n]|^2 for n = l, l+64, ... (class n mod 4 = l mod 4) */
+    /* Oerder-Meyr: lane l accumulates |y[n]|^2 for n = l, l+64, ... (class n mod 4 = l mod 4), as
+     * four partial sums over quarters of the 64-sample blocks (part w: blocks [w q4, (w+1) q4),
+     * q4 = ceil(nb / 4)) added in order -- the GPU computes the parts on four waves at once */
     float acc[64];
+    const int nb = (M2 + 63) / 64, q4 = (nb + 3) / 4;
     for (int l = 0; l < 64; ++l) {
         float s = 0.f;
-        for (int n = l; n < M2; n += 64) s += fmaf(y[2 * n], y[2 * n], y[2 * n + 1] * y[2 * n + 1]);
+        for (int w = 0; w < 4; ++w) {
+            float pw = 0.f;
+            int b1 = (w + 1) * q4 < nb ? (w + 1) * q4 : nb;
+            for (int b = w * q4; b < b1; ++b) {
+                int n = 64 * b + l;
+                if (n < M2) pw += fmaf(y[2 * n], y[2 * n], y[2 * n + 1] * y[2 * n + 1]);
+            }
+            s = w == 0 ? pw : s + pw;
+        }
         acc[l] = s;
     }
     /* class sums: butterfly over xor 32,16,8,4 */

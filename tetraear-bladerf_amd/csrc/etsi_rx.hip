@@ -105,8 +105,11 @@ __device__ __forceinline__ float pat2(float y, float x) {
     return r;
 }
 
-// Cubic Lagrange interpolation of y (y[n] at w[n - w0]) at t and at t - 2 together: t - 2 is exact here (t < 2^22), so both share
-// the fraction f and the four Lagrange weights -- computed once, the same bits either way.
+// Cubic Lagrange interpolation of y (y[n] at w[n - w0]) at t and at t - 2 together: t - 2 is exact
+// here (t < 2^22), so both share the fraction f and the four Lagrange weights -- computed once, the
+// same bits either way.  (Measured and rejected: prefetching the next block's window at the position
+// the current delta predicts, selected by the wave-uniform shift: 0.5 % slower -- the Gardner block is
+// bound by its instruction chain, not by this LDS read.)
 __device__ __forceinline__ void interp_pair(const float2 *w, int w0, float t, float2 &on, float2 &mid) {
     const float K6 = 1.0f / 6.0f;
     const float fi = floorf(t);
@@ -159,9 +162,27 @@ constexpr int CPOL_SC1 = 16;   // gfx940+ cache-policy bits: sc0 1, nt 2, sc1 16
 // SPLIT: the CFO sums are left to a second wave (cfo_consumer) that follows the tracking through
 // the LDS progress word *prog (symbols done | PROG_DONE at the end): off the serial tracking chain.
 constexpr int PROG_DONE = 1 << 30;
+// Oerder-Meyr part w for this lane: |y[n]|^2 summed over n = 64 b + lane, b in [w q4, (w + 1) q4),
+// q4 = ceil(nb / 4) (loads issued 8 ahead; ascending order)
+__device__ __forceinline__ float om_part(const float2 *y, int M2, int w, int lane) {
+    const int nb = (M2 + 63) / 64, q4 = (nb + 3) / 4;
+    const int n1 = min(64 * min((w + 1) * q4, nb), M2);
+    float s = 0.f;
+    for (int n0 = 64 * w * q4 + lane; n0 < n1; n0 += 8 * 64) {
+        float2 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = n0 + 64 * u < n1 ? y[n0 + 64 * u] : make_float2(0.f, 0.f);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (n0 + 64 * u < n1) s += fmaf(v[u].x, v[u].x, v[u].y * v[u].y);
+    }
+    return s;
+}
+
 template <bool SPLIT = false>
 __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float gain, float soft_scale, float2 *sp,
-                                                 float2 *dp, int smax, int lane, int *prog = nullptr) {
+                                                 float2 *dp, int smax, int lane, int *prog = nullptr,
+                                                 const float *om = nullptr) {
     TrackOut o{0, 1.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     if (M2 < 16) {
         if constexpr (SPLIT) {
@@ -169,15 +190,18 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
         }
         return o;
     }
-    // Oerder-Meyr: class sums of |y|^2 over n mod 4 (loads issued 8 ahead; same summation order)
-    float s = 0.f;
-    for (int n0 = lane; n0 < M2; n0 += 8 * 64) {
-        float2 v[8];
+    // Oerder-Meyr: class sums of |y|^2 over n mod 4, per lane as four partial sums over quarters of
+    // the blocks added in order (om_part; the oracle's order) -- precomputed by four waves (om)
+    // or computed here one after the other
+    float s;
+    if (om) {
+        s = om[lane];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = n0 + 64 * u < M2 ? y[n0 + 64 * u] : make_float2(0.f, 0.f);
+        for (int w = 1; w < 4; ++w) s = s + om[64 * w + lane];
+    } else {
+        s = om_part(y, M2, 0, lane);
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (n0 + 64 * u < M2) s += fmaf(v[u].x, v[u].x, v[u].y * v[u].y);
+        for (int w = 1; w < 4; ++w) s = s + om_part(y, M2, w, lane);
     }
     s = bfly<4>(s);
     const float A0 = lane_f(s, 0), A1 = lane_f(s, 1), A2 = lane_f(s, 2), A3 = lane_f(s, 3);
@@ -454,15 +478,17 @@ struct TailStage {
 // the tracking is the serial tail (wave 0, prioritised on its SIMD); the decision pass after it is
 // shared by all four waves (the rotation and scale go through LDS, *tro).
 __device__ __forceinline__ void timing_tail(const float2 *ly, float2 *scr, const TimingOut &to, int M2, int ch,
-                                            int tid, TrackOut *tro, int *prog, const TailStage *stage = nullptr) {
+                                            int tid, TrackOut *tro, int *prog, const TailStage *stage = nullptr,
+                                            float *om = nullptr) {
     const size_t so = (size_t)ch * to.smax;
+    if (om && M2 >= 16) om[tid] = om_part(ly, M2, tid >> 6, tid & 63);   // the four Oerder-Meyr parts at once
     if (tid == 0) *prog = 0;
     __syncthreads();
     if (tid < 64) {
         __builtin_amdgcn_s_setprio(3);
         // S <= M2 / 4 + 1 < the staging size either way: the bound only guards the LDS buffer
         const TrackOut o = timing_track<true>(ly, M2, to.gain, to.soft_scale, stage ? stage->sym : to.sym + so, scr,
-                                              stage ? min(to.smax, M2 / 4 + 2) : to.smax, tid, prog);
+                                              stage ? min(to.smax, M2 / 4 + 2) : to.smax, tid, prog, om);
         if (tid == 0) {
             tro->S = o.S;
             tro->base = o.base;
@@ -761,7 +787,7 @@ static_assert(2 * WSMEM4 * 16 + 7 * 1024 + 2560 <= 160 * 1024, "per-wave demod L
 static_assert(sizeof(TrackOut) + sizeof(int) <= 32 && (4 * WLR + 3 * SEAM) % 2 == 0, "per-wave demod LDS carving");
 // fused tail staging: sm symbols in the stage-1 buffers; 8 sm (d_j) + 2 sm + sm bytes in the images
 constexpr int WTAIL_SM = YLDS / 4 + 2;
-static_assert(WTAIL_SM * 8 <= 4 * WLR * 8 && 11 * WTAIL_SM + 32 <= 4 * WIMG4 * 16, "tail staging LDS");
+static_assert(WTAIL_SM * 8 <= 4 * WLR * 8 && 11 * WTAIL_SM + 32 + 1024 <= 4 * WIMG4 * 16, "tail staging LDS");
 
 // cross-lane LDS hand-off inside one wave: a wave's LDS instructions execute in order, so only the
 // compiler has to be kept from moving accesses across this point (no s_waitcnt, no s_barrier)
@@ -954,8 +980,10 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_w(const float4 *__restrict_
         int8_t *ib = reinterpret_cast<int8_t *>(img);
         const TailStage st{lin_all, ib + ((8 * sm + 15) & ~15), reinterpret_cast<uint8_t *>(ib + ((10 * sm + 31) & ~15))};
         int *prog = reinterpret_cast<int *>(tro + 1);   // the word after TrackOut in its 32-B slot
+        // the Oerder-Meyr parts (1 KB) at the images' end, past the tail staging (<= 10.8 KB)
+        float *om = reinterpret_cast<float *>(reinterpret_cast<uint8_t *>(img) + 4 * WIMG4 * 16 - 1024);
         timing_tail(reinterpret_cast<const float2 *>(yb), reinterpret_cast<float2 *>(img), to, M2, ch, tid, tro, prog,
-                    &st);
+                    &st, om);
     } else {
         copy_out(reinterpret_cast<uint8_t *>(y + (size_t)ch * M2), reinterpret_cast<const uint8_t *>(yb), 8 * M2, tid);
     }

@@ -1,0 +1,9 @@
+# the fused per-wave tail without its output stores (copy_out), everything else computed (timing only)
+import sys
+s = sys.stdin.read()
+a = "    copy_out(reinterpret_cast<uint8_t *>(to.sym + so), reinterpret_cast<const uint8_t *>(stage->sym), 8 * o.S, tid);"
+assert s.count(a) == 1
+s = s.replace(a, "    if (M2 > (1 << 30)) {   // timing variant\n" + a)
+b = "    copy_out(to.hard + so, stage->hard, nd, tid);"
+assert s.count(b) == 1
+sys.stdout.write(s.replace(b, b + "\n    }"))
