@@ -382,8 +382,10 @@ template <typename In> struct CfCfg;
 template <> struct CfCfg<float4> { static constexpr int s2_every = 8, lr = 2312; };
 template <> struct CfCfg<uint2> { static constexpr int s2_every = 8, lr = 2312; };
 constexpr int TPP = 107;        // RRC taps per polyphase branch (Lp = 321 = 3 x 107)
-constexpr int PFD = 2;          // input tiles in flight per workgroup (register prefetch depth, pa/pb;
-                                // 3 and 4 measured no faster)
+constexpr int PFD = 2;          // k_chanfilt: input tiles in flight per workgroup (register prefetch
+                                // depth, pa/pb; 3 and 4 measured no faster)
+constexpr int PFDW = 4;         // k_chanfilt_w: input tiles in flight per wave (pa/pb/pc/pd, 254 VGPRs,
+                                // no spill; same box: 2 -> 3 -1.5 %, 3 -> 4 -0.6 % serial demod)
 constexpr int YLDS = 3904;      // cf32: stage-2 outputs held in LDS (a 131072-sample chunk has 3899)
 // Stage 2 on the matrix cores (v_mfma_f32_16x16x4_f32: bit-for-bit a k-ordered fmaf chain).  One
 // MFMA tile: 16 columns = 8 segments x (re, im), each segment S2Q consecutive triples; row
@@ -764,7 +766,7 @@ __global__ __launch_bounds__(256, cf_waves<In>()) void k_chanfilt(const In *__re
 // cf32 with y in LDS (M2 <= YLDS): the workgroup's waves stream the channel's quarters
 // independently.  Wave w owns the stage-2 triples [U_w, U_w+1) and the stage-1 outputs
 // [K_w, K_w+1), K_w = 10 U_w (the last wave's end is M1), in 640-sample wave tiles (one stage-1
-// output per lane, five 16-B loads per lane, two tiles in flight) with its own LDS image and
+// output per lane, five 16-B loads per lane, four tiles in flight) with its own LDS image and
 // stage-1 buffer, and runs a one-MFMA-tile stage-2 burst (40 triples: one dependent chain of 39
 // MFMAs) whenever 40 triples have their windows.  So the stream has no workgroup barrier until the
 // channel ends, and a burst stalls one wave's quarter of the loads in flight instead of the whole
@@ -885,7 +887,7 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_w(const float4 *__restrict_
 #pragma unroll
         for (int r = 0; r < 5; ++r) xw[HALO / 2 + r * 64 + lane] = pf[r];
         __builtin_amdgcn_sched_barrier(0);
-        load_tile(pf, t + PFD);
+        load_tile(pf, t + PFDW);
         wave_sync();
         const int k = K0 + 64 * t - 4 + lane;
         if (k >= K0 && k < K1) {
@@ -952,18 +954,26 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_w(const float4 *__restrict_
         wave_sync();
     };
     __syncthreads();   // htap
-    static_assert(PFD == 2, "pa / pb below");
-    float4 pa[5], pb[5];
+    // four register sets, explicitly (an array over them costs VGPRs, round 2); the deeper prefetch
+    // keeps a workgroup's stream fed while its CU neighbour runs its timing tail
+    static_assert(PFDW == 4, "pa / pb / pc / pd below");
+    float4 pa[5], pb[5], pc[5], pd[5];
     if (ntile > 0) {
         load_tile(pa, 0);
         load_tile(pb, 1);
+        load_tile(pc, 2);
+        load_tile(pd, 3);
     }
     int t = 0;
-    for (; t + 1 < ntile; t += 2) {
+    for (; t + 3 < ntile; t += 4) {
         tile(t, pa);
         tile(t + 1, pb);
+        tile(t + 2, pc);
+        tile(t + 3, pd);
     }
     if (t < ntile) tile(t, pa);
+    if (t + 1 < ntile) tile(t + 1, pb);
+    if (t + 2 < ntile) tile(t + 2, pc);
     __syncthreads();   // every wave's seam and in-loop bursts
     if (active && u_done < u_end) {
         if (has_right) {   // x240[K1, K1 + SEAM) from wave wv + 1 (K1 - kbase <= 120)
