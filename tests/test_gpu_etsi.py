@@ -316,6 +316,28 @@ def test_bench_pipeline_matches_serial():
                 assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("N", [131072, 70002, 20000, 3000])
+def test_sc16_chanfilt_component_vs_oracle(N):
+    """tetra_etsi_chanfilt_fmt on SC16 (y written to HBM: k_chanfilt_r<.., false>, or k_chanfilt<uint2>
+    for rows that are not a multiple of four samples) equals the oracle's channel filter on the
+    1/32768-scaled samples, bit for bit."""
+    from tetraear import _hip
+    from tetraear.signal.etsi import synth, EtsiReceiver, lengths
+    C = 3
+    iq = synth(C, N, seed=21, snr_db=20.0)[0]
+    q = np.stack([np.round(iq.real * 32768), np.round(iq.imag * 32768)], -1).clip(-32768, 32767).astype(np.int16)
+    x = (q[..., 0].astype(np.float32) / 32768 + 1j * (q[..., 1].astype(np.float32) / 32768)).astype(np.complex64)
+    rx = EtsiReceiver()
+    _, M2, _ = lengths(rx.plan, N)
+    y = np.zeros((C, M2), np.complex64)
+    c = _hip.ctx()
+    c.check(c.lib.tetra_etsi_chanfilt_fmt(c.handle, rx.plan, _hip.ptr(np.ascontiguousarray(q)), _hip.TETRA_SC16, C, N,
+                                          _hip.ptr(y)), "chanfilt_fmt")
+    o = E.Receiver()
+    for ch in range(C):
+        assert np.array_equal(y[ch], o.chanfilt(x[ch])), ch
+
+
 def test_sc16_ingest_matches_cf32(synth_small):
     """SC16 (int16 I/Q, the BladeRF wire format) filtered straight from 4 B/sample equals the
     cf32 path on the same samples scaled by 1/32768 (capture.py:241-269), bit for bit."""
@@ -336,11 +358,12 @@ def test_sc16_ingest_matches_cf32(synth_small):
 
 
 @pytest.mark.parametrize("fmt", ["cf32", "sc16"])
-@pytest.mark.parametrize("N", [262144, 134408, 131072, 70001, 40000, 23408, 20000, 9001, 3000])
+@pytest.mark.parametrize("N", [262144, 134408, 131072, 70002, 70001, 40000, 23408, 20000, 9001, 3000])
 def test_demod_lengths_vs_oracle(N, fmt):
     """Chunk lengths around the kernels' structure: longer than the fused path's LDS output buffer
-    (component path; 134408 gives 4000 outputs, just past YLDS = 3904), the 128 Ki design point (fused; SC16 re-stages y into the freed image and
-    stage-1 buffer), mid lengths on the per-wave cf32 filter (odd wave-tile counts, quarters that
+    (component path; 134408 gives 4000 outputs, just past YLDS = 3904), the 128 Ki design point (fused; SC16 on
+    k_chanfilt_r, register stage 1; 70002, a row of SC16 not a multiple of four samples, on k_chanfilt<uint2>,
+    which re-stages y into the freed image and stage-1 buffer), mid lengths on the per-wave cf32 filter (odd wave-tile counts, quarters that
     end mid-tile), short (the per-wave filter on fewer than four waves), odd (trimmed to even like
     demod_batch does), and barely long enough -- for both input formats (SC16 against the oracle on
     its 1/32768-scaled samples)."""

@@ -47,7 +47,7 @@ struct tetra_ctx {
     std::string err;
     DevBuf slot[S_COUNT];
     char arch[64] = {0};
-    float coef_etsi[64 + 39 * 64];     // host image of the channel-filter tap tables (h1, stage-2 MFMA A)
+    float coef_etsi[128 + 39 * 64];    // host image of the channel-filter tap tables (h1, h1 / 32768, stage-2 MFMA A)
     const void *coef_etsi_dev = nullptr;   // workspace the tap image was last uploaded to
     std::vector<float> taps_wb;        // host image of the wideband prototype + resampler taps
     std::vector<float> taps_wb_up;     // ... as last uploaded to taps_wb_dev (slot S_W9)

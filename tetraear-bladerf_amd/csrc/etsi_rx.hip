@@ -8,12 +8,15 @@
 //                (alpha 0.35, 321 taps at 720 kHz) resampler x3/10 -> 72 kHz = 4 samples/symbol,
 //                then the timing stage (fused).  cf32 chunks up to YLDS outputs: the workgroup's
 //                four waves stream the channel's quarters independently (640-sample wave tiles,
-//                register prefetch two tiles deep, private LDS image and stage-1 buffer, stage 2 in
+//                register prefetch four tiles deep, private LDS image and stage-1 buffer, stage 2 in
 //                one-MFMA-tile bursts on v_mfma_f32_16x16x4_f32 -- exact f32: banded tap matrix x 16
 //                columns of 5 output triples), y held in LDS.  8 B read per input sample.
+//   k_chanfilt_r the per-wave filter for SC16 (4 B/sample in) with stage 1 in registers: a lane's
+//                10-sample block from the wave's LDS image, the next four blocks from its row
+//                neighbours by DPP (v_fmac_f32_dpp), 48-output wave tiles, y in LDS.
 //   k_chanfilt   the same filter with workgroup-wide 2560-sample tiles (barrier per tile, stage 2
-//                every 8 tiles): the SC16 form (4 B/sample in, y round-tripped through L2, four
-//                workgroups per CU) and chunks longer than YLDS outputs.
+//                every 8 tiles): SC16 rows that are not a multiple of four samples (y round-tripped
+//                through L2, four workgroups per CU) and chunks longer than YLDS outputs.
 //   k_timing     one wave per channel: Oerder-Meyr timing phase (wave reduction), block Gardner
 //                tracking (64 symbols per block = one per lane; error summed by xor-butterfly),
 //                cubic interpolation, differential decision, 4th-power CFO estimate, int8 soft bits.
@@ -402,7 +405,7 @@ template <typename In> constexpr int cf_lds4() { return XIN4 + cf_lr<In>() / 2; 
 constexpr int CF_LDS2_SC16 = 2 * (XIN4 + CfCfg<uint2>::lr / 2);   // SC16 fused: y + timing scratch (float2)
 static_assert(XIN4 + CfCfg<uint2>::lr / 2 == 2460, "SC16 LDS: 39,360 B, four workgroups per CU");
 static_assert((XIN4 + CfCfg<float4>::lr / 2 + 12) * 16 + 4096 * 8 <= 72 * 1024, "cf32 LDS: two workgroups per CU + 16 KB");
-constexpr int CF_COEF = 64 + S2K * 64;       // device tap image: h1 (64) + A fragments [S2K][64 lanes]
+constexpr int CF_COEF = 128 + S2K * 64;      // device tap image: h1 (64), h1 * 2^-15 (64, SC16) + A fragments [S2K][64 lanes]
 
 // Packed fp32 (v_pk_fma_f32): one real tap times a complex sample, each half a correctly rounded
 // fma -- the same per-component arithmetic as two fmaf calls.
@@ -994,6 +997,306 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_w(const float4 *__restrict_
         float *om = reinterpret_cast<float *>(reinterpret_cast<uint8_t *>(img) + 4 * WIMG4 * 16 - 1024);
         timing_tail(reinterpret_cast<const float2 *>(yb), reinterpret_cast<float2 *>(img), to, M2, ch, tid, tro, prog,
                     &st, om);
+    } else {
+        copy_out(reinterpret_cast<uint8_t *>(y + (size_t)ch * M2), reinterpret_cast<const uint8_t *>(yb), 8 * M2, tid);
+    }
+}
+
+// --------------------------------------------------------------------------- register stage 1
+// k_chanfilt_r: the per-wave channel filter with stage 1 out of LDS.  In k_chanfilt_w every lane
+// reads its 48-sample window (24 float4) and the 48 taps (12 broadcast float4) from LDS for one
+// output, ~5 LDS cycles per output of the CU's 128 B/cycle, and that is what bounds the filter once
+// the input needs no HBM (timing builds: the input L2-resident, 0.93 ms per 8192 x 131072 batch; its
+// stage-1 chain cut to a third, 0.66).  Here a lane reads only its own 10-sample block from the
+// image (5 loads of 2 samples) and takes the next four blocks from its row neighbours with DPP
+// (row_shl:p reads lane + p of the same 16-lane row): a row of 16 lanes holds 16 consecutive blocks
+// and computes the outputs of its first 12, so a wave tile is 48 outputs (480 new samples, a 40-sample
+// halo).  The taps sit in registers.  Each output is still the oracle's ascending-j fma chain
+// (x[10 k + j] is sample j mod 10 of lane + j / 10's block), bit-identical to k_chanfilt_w.
+// SC16 keeps its samples as raw dwords in the image (re low 16 bits, im high) and folds the 2^-15
+// scale into the taps (an exact power of two: fma(h 2^-15, x, a) == fma(h, x 2^-15, a)).
+// Everything after stage 1 -- the wave partition, seams, MFMA bursts, the fused timing tail -- is
+// k_chanfilt_w's.
+constexpr int RT_K = 48;            // stage-1 outputs per wave tile (4 rows x 12)
+constexpr int RT_IN = 10 * RT_K;    // new input samples per wave tile
+constexpr int RHALO = 40;           // image samples carried over from the previous tile
+template <typename In> struct RCfg;
+// SC16: a 16-B load = 4 samples; 4 tiles in flight per wave (same box, serial: 6 -> 4 -1 %, 3 = 4)
+template <> struct RCfg<uint4> { static constexpr int bps = 4, pf = 4; };
+template <typename In> constexpr int r_chunks() { return RT_IN * RCfg<In>::bps / 16; }   // 16-B loads per tile
+template <typename In> constexpr int r_img16() { return (RHALO + RT_IN) * RCfg<In>::bps / 16; }
+template <typename In> constexpr int r_smem4() { return 2 + 4 * r_img16<In>() + (4 * WLR + 3 * SEAM + YLDS) / 2; }
+// tail staging over the freed images + stage-1 buffers: d_j, soft bits, hard dibits, O-M parts, symbols
+template <typename In> constexpr int r_tail_bytes() { return 19 * WTAIL_SM + 48 + 1024; }
+static_assert(r_tail_bytes<uint4>() <= 4 * r_img16<uint4>() * 16 + 4 * WLR * 8, "k_chanfilt_r tail staging");
+static_assert(2 * r_smem4<uint4>() * 16 + 7 * 1024 + 2560 <= 160 * 1024, "k_chanfilt_r LDS");
+
+// ar += h[q] * x_re[q], ai += h[q] * x_im[q] for q < N in order, x taken from lane + P of this
+// lane's 16-lane row (row_shl:P; a lane past the row's end reads 0 -- only lanes 12..15 do, and
+// their outputs are not kept): one v_fmac_f32_dpp per product, the DPP folded into the fma (hipcc
+// emits a v_mov_b32_dpp per operand instead and keeps ~76 of them live).  Five products per asm:
+// the hazard recognizer puts a wait state after every asm statement.  The samples' producer (their
+// conversion) precedes this lane's own P = 0 use of them, >= 9 chain steps earlier, so the DPP
+// reads need no wait states of their own.
+template <int P, int N>
+__device__ __forceinline__ void fmac_rows(float &ar, float &ai, const float *xr, const float *xi, const float *h) {
+    if constexpr (P == 0) {
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+            ar = fmaf(h[q], xr[q], ar);
+            ai = fmaf(h[q], xi[q], ai);
+        }
+    }
+    else if constexpr (P == 1 && N == 5) {
+        asm("v_fmac_f32_dpp %0, %2, %12 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %7, %12 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %3, %13 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %8, %13 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %4, %14 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %9, %14 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %5, %15 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %10, %15 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %6, %16 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %11, %16 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            : "+v"(ar), "+v"(ai)
+            : "v"(xr[0]), "v"(xr[1]), "v"(xr[2]), "v"(xr[3]), "v"(xr[4]), "v"(xi[0]), "v"(xi[1]), "v"(xi[2]), "v"(xi[3]), "v"(xi[4]), "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]), "v"(h[4]));
+    }
+    else if constexpr (P == 2 && N == 5) {
+        asm("v_fmac_f32_dpp %0, %2, %12 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %7, %12 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %3, %13 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %8, %13 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %4, %14 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %9, %14 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %5, %15 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %10, %15 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %6, %16 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %11, %16 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            : "+v"(ar), "+v"(ai)
+            : "v"(xr[0]), "v"(xr[1]), "v"(xr[2]), "v"(xr[3]), "v"(xr[4]), "v"(xi[0]), "v"(xi[1]), "v"(xi[2]), "v"(xi[3]), "v"(xi[4]), "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]), "v"(h[4]));
+    }
+    else if constexpr (P == 3 && N == 5) {
+        asm("v_fmac_f32_dpp %0, %2, %12 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %7, %12 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %3, %13 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %8, %13 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %4, %14 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %9, %14 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %5, %15 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %10, %15 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %6, %16 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %11, %16 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            : "+v"(ar), "+v"(ai)
+            : "v"(xr[0]), "v"(xr[1]), "v"(xr[2]), "v"(xr[3]), "v"(xr[4]), "v"(xi[0]), "v"(xi[1]), "v"(xi[2]), "v"(xi[3]), "v"(xi[4]), "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]), "v"(h[4]));
+    }
+    else if constexpr (P == 4 && N == 5) {
+        asm("v_fmac_f32_dpp %0, %2, %12 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %7, %12 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %3, %13 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %8, %13 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %4, %14 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %9, %14 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %5, %15 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %10, %15 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %6, %16 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %11, %16 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            : "+v"(ar), "+v"(ai)
+            : "v"(xr[0]), "v"(xr[1]), "v"(xr[2]), "v"(xr[3]), "v"(xr[4]), "v"(xi[0]), "v"(xi[1]), "v"(xi[2]), "v"(xi[3]), "v"(xi[4]), "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]), "v"(h[4]));
+    }
+    else if constexpr (P == 4 && N == 3) {
+        asm("v_fmac_f32_dpp %0, %2, %8 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %5, %8 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %3, %9 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %6, %9 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %4, %10 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %7, %10 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            : "+v"(ar), "+v"(ai)
+            : "v"(xr[0]), "v"(xr[1]), "v"(xr[2]), "v"(xi[0]), "v"(xi[1]), "v"(xi[2]), "v"(h[0]), "v"(h[1]), "v"(h[2]));
+    }
+    else {
+        static_assert(P == 0, "fmac_rows: no such form");
+    }
+}
+
+template <typename In, bool FUSE>
+__global__ __launch_bounds__(256, 2) void k_chanfilt_r(const In *__restrict__ iq, long N, int M1, int M2,
+                                                       const float *__restrict__ h1, const float *__restrict__ afrag,
+                                                       float2 *__restrict__ y, TimingOut to) {
+    constexpr bool SC16 = std::is_same<In, uint4>::value;
+    constexpr int BPS = RCfg<In>::bps, PF = RCfg<In>::pf, NCH = r_chunks<In>(), NL = (NCH + 63) / 64;
+    constexpr int IMGB = r_img16<In>() * 16;   // image bytes per wave
+    using Pair = typename std::conditional<SC16, uint2, float4>::type;   // two samples
+    __shared__ float4 smem[r_smem4<In>()];
+    TrackOut *tro = reinterpret_cast<TrackOut *>(smem);                        // + prog: 2 float4
+    uint8_t *img_all = reinterpret_cast<uint8_t *>(smem + 2);                  // 4 wave images
+    float2 *lin_all = reinterpret_cast<float2 *>(img_all + 4 * IMGB);          // 4 stage-1 buffers
+    float2 *seam = lin_all + 4 * WLR;
+    float *yb = reinterpret_cast<float *>(seam + 3 * SEAM);
+    const int ch = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    uint8_t *img = img_all + wv * IMGB;
+    float2 *lin = lin_all + wv * WLR;
+    for (int i = lane; i < WLR; i += 64) lin[i] = make_float2(0.f, 0.f);
+    float at[S2K];
+#pragma unroll
+    for (int k = 0; k < S2K; ++k) at[k] = afrag[64 * k + lane];
+    float hv[48];
+#pragma unroll
+    for (int j = 0; j < 48; ++j) {
+        hv[j] = h1[j];   // SC16: the launch passes the taps pre-scaled by 2^-15
+        asm volatile("" : "+v"(hv[j]));   // held in VGPRs (v_fmac_f32_dpp's src1; as SGPRs hipcc copies them per tile)
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): landed before the stream starts
+    // the partition (k_chanfilt_w's)
+    const int UT = (M2 + 2) / 3;
+    const int nw = min(4, max(1, UT / UMIN));
+    const int UQ = (UT + nw - 1) / nw;
+    const bool active = wv < nw;
+    const bool has_right = wv + 1 < nw;
+    const int u_beg = min(wv * UQ, UT), u_end = has_right ? (wv + 1) * UQ : UT;
+    const int K0 = 10 * u_beg, K1 = has_right ? 10 * u_end : M1;
+    const int ntile = active ? (K1 - K0 + 4 + RT_K - 1) / RT_K : 0;   // wave tiles with kfirst < K1
+    // tile t: lane (row ro, i) holds the block of x240[K0 + 48 t - 4 + 12 ro + i], samples
+    // 10 (K0 + 48 t) - 40 + 10 (12 ro + i) + [0, 10) = image samples 10 (12 ro + i) + [0, 10); the
+    // tile's new samples 10 (K0 + 48 t) + [0, 480) land at image sample 40.  A buffer resource over the
+    // wave's samples [10 K0, last needed]: loads past it return 0 without touching memory.
+    const long s0 = 10L * K0;
+    const long slast = active ? min(10L * (K1 - 1) + 47, N - 1) : s0;
+    const uint8_t *xp = reinterpret_cast<const uint8_t *>(iq) + ((size_t)ch * N + s0) * BPS;
+    const int nbytes = active ? (int)(((slast - s0 + 1) * BPS + 15) & ~15L) : 0;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(xp), 0, nbytes, 0x00020000);
+    const int ro = lane >> 4, li = lane & 15;
+    const int blk = 12 * ro + li;
+    auto load_tile = [&](In (&pf)[NL], int t) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < NL; ++r) {
+            const int c = min(64 * r + lane, NCH - 1);   // unconditional (a branch makes hipcc wait at the join)
+            const nt_f4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * c, t * RT_IN * BPS, 2 /* nt */);
+            pf[r] = *reinterpret_cast<const In *>(&v);
+        }
+    };
+    int kbase = K0;      // x240 index of lin[0]
+    int u_done = u_beg;  // triples [u_beg, u_done) are in yb
+    const int kg = lane >> 4, seg = (lane & 15) >> 1, comp = lane & 1;
+    const float *lf = reinterpret_cast<const float *>(lin);
+    auto burst = [&](int u_lim) __attribute__((always_inline)) {   // k_chanfilt_w's
+        const int U0 = u_done + S2Q * seg;
+        const int b0 = U0 < u_lim ? 2 * (10 * U0 - kbase + kg) + comp : 2 * kg + comp;
+        float bv[S2K];
+        f4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s2 = 0; s2 < 13; ++s2) bv[s2] = lf[b0 + 8 * s2];
+#pragma unroll
+        for (int s3 = 0; s3 < 3; ++s3) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (s3 < 2) {
+#pragma unroll
+                for (int s2 = 13 * s3 + 13; s2 < 13 * s3 + 26; ++s2) bv[s2] = lf[b0 + 8 * s2];
+            }
+#pragma unroll
+            for (int s2 = 13 * s3; s2 < 13 * s3 + 13; ++s2)
+                c = __builtin_amdgcn_mfma_f32_16x16x4f32(at[s2], bv[s2], c, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = 4 * kg + r, q = i / 3, m = 3 * U0 + i;
+            if (i < 15 && U0 + q < u_lim && m < M2) yb[2 * m + comp] = c[r];
+        }
+    };
+    auto tile = [&](int t, In (&pf)[NL]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < NL; ++r)
+            if (64 * r + lane < NCH) *reinterpret_cast<In *>(img + RHALO * BPS + 16 * (64 * r + lane)) = pf[r];
+        __builtin_amdgcn_sched_barrier(0);
+        load_tile(pf, t + PF);
+        wave_sync();
+        // this lane's block: 10 samples as five pairs
+        float xre[10], xim[10];
+#pragma unroll
+        for (int m = 0; m < 5; ++m) {
+            const Pair v = *reinterpret_cast<const Pair *>(img + (10 * blk + 2 * m) * BPS);
+            if constexpr (SC16) {
+                xre[2 * m] = (float)(int16_t)(v.x & 0xFFFFu);
+                xim[2 * m] = (float)(int16_t)(v.x >> 16);
+                xre[2 * m + 1] = (float)(int16_t)(v.y & 0xFFFFu);
+                xim[2 * m + 1] = (float)(int16_t)(v.y >> 16);
+            } else {
+                xre[2 * m] = v.x;
+                xim[2 * m] = v.y;
+                xre[2 * m + 1] = v.z;
+                xim[2 * m + 1] = v.w;
+            }
+        }
+        // x240[k] = sum_j h1[j] x[10 k + j], j ascending: sample j % 10 of the block j / 10 lanes on
+        float ar = 0.f, ai = 0.f;
+        fmac_rows<0, 10>(ar, ai, xre, xim, hv);
+        fmac_rows<1, 5>(ar, ai, xre, xim, hv + 10);
+        fmac_rows<1, 5>(ar, ai, xre + 5, xim + 5, hv + 15);
+        fmac_rows<2, 5>(ar, ai, xre, xim, hv + 20);
+        fmac_rows<2, 5>(ar, ai, xre + 5, xim + 5, hv + 25);
+        fmac_rows<3, 5>(ar, ai, xre, xim, hv + 30);
+        fmac_rows<3, 5>(ar, ai, xre + 5, xim + 5, hv + 35);
+        fmac_rows<4, 5>(ar, ai, xre, xim, hv + 40);
+        fmac_rows<4, 3>(ar, ai, xre + 5, xim + 5, hv + 45);
+        const int k = K0 + RT_K * t - 4 + blk;
+        if (li < 12 && k >= K0 && k < K1) {
+            lin[k - kbase] = make_float2(ar, ai);
+            if (wv > 0 && k - K0 < SEAM) seam[(wv - 1) * SEAM + k - K0] = make_float2(ar, ai);
+        }
+        wave_sync();
+        // halo for the next tile: image samples [0, 40) = this tile's [480, 520)
+        if (lane < RHALO * BPS / 16)
+            reinterpret_cast<uint4 *>(img)[lane] = reinterpret_cast<const uint4 *>(img)[RT_IN * BPS / 16 + lane];
+        const int kav = min(K0 + RT_K * t + RT_K - 5, K1 - 1);   // the tile's last output
+        const int u_rdy = kav >= 113 ? min((kav - 113) / 10 + 1, u_end) : 0;
+        while (u_rdy - u_done >= S2T || (t == ntile - 1 && u_rdy > u_done)) {
+            const int ul = min(u_done + S2T, u_rdy);
+            burst(ul);
+            u_done = ul;
+            const int from = 10 * u_done - kbase, cnt = kav + 1 - 10 * u_done;
+            float2 v[3];
+#pragma unroll
+            for (int e = 0; e < 3; ++e) v[e] = lane + 64 * e < cnt ? lin[from + lane + 64 * e] : make_float2(0.f, 0.f);
+            wave_sync();
+#pragma unroll
+            for (int e = 0; e < 3; ++e)
+                if (lane + 64 * e < cnt) lin[lane + 64 * e] = v[e];
+            kbase = 10 * u_done;
+        }
+        wave_sync();
+    };
+    In pf[PF][NL];
+    if (ntile > 0) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) load_tile(pf[u], u);
+    }
+    int t = 0;
+    for (; t + PF <= ntile; t += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) tile(t + u, pf[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < PF - 1; ++u)
+        if (t + u < ntile) tile(t + u, pf[u]);
+    __syncthreads();   // every wave's seam and in-loop bursts
+    if (active && u_done < u_end) {
+        if (has_right) {
+            for (int i = lane; i < SEAM; i += 64) lin[K1 - kbase + i] = seam[wv * SEAM + i];
+            wave_sync();
+        }
+        burst(u_end);
+    }
+    __syncthreads();
+    if constexpr (FUSE) {
+        // the tail's LDS over the freed images and stage-1 buffers (the launch guarantees
+        // sm <= WTAIL_SM): d_j scratch, soft bits, hard dibits, the O-M parts, then the symbols
+        const int sm = M2 / 4 + 2;
+        uint8_t *R = img_all;
+        const int o_sb = (8 * sm + 15) & ~15, o_hd = o_sb + ((2 * sm + 15) & ~15), o_om = o_hd + ((sm + 15) & ~15);
+        const TailStage st{reinterpret_cast<float2 *>(R + o_om + 1024), reinterpret_cast<int8_t *>(R + o_sb), R + o_hd};
+        int *prog = reinterpret_cast<int *>(tro + 1);
+        timing_tail(reinterpret_cast<const float2 *>(yb), reinterpret_cast<float2 *>(R), to, M2, ch, tid, tro, prog,
+                    &st, reinterpret_cast<float *>(R + o_om));
     } else {
         copy_out(reinterpret_cast<uint8_t *>(y + (size_t)ch * M2), reinterpret_cast<const uint8_t *>(yb), 8 * M2, tid);
     }
@@ -1631,9 +1934,17 @@ static int etsi_check(tetra_ctx *ctx, const tetra_etsi_plan *P) {
 }
 
 // Which channel-filter kernel a launch takes (launch_chanfilt, tetra_etsi_kernel_info).
-enum CfKernel { CF_W_FUSED, CF_W, CF_SC16_FUSED, CF_SC16, CF_F4_FUSED, CF_F4 };
-static CfKernel chanfilt_kernel(int fmt, int64_t M2, bool fused) {
+enum CfKernel { CF_W_FUSED, CF_W, CF_SC16_FUSED, CF_SC16, CF_F4_FUSED, CF_F4, CF_R_FUSED, CF_R };
+// SC16 on the register-stage-1 per-wave filter: y in LDS (M2 <= YLDS) and rows of whole 16-B loads
+static bool sc16_r(int fmt, int64_t M2, size_t N) { return fmt == TETRA_SC16 && M2 <= YLDS && N % 4 == 0; }
+// the fused demod's condition: y (and the tail's staging) fit the kernel's LDS
+static bool fused_fits(int fmt, int64_t M2, int64_t sm, size_t N) {
+    if (fmt == TETRA_SC16 && !sc16_r(fmt, M2, N)) return M2 + sm <= CF_LDS2_SC16;
+    return M2 <= YLDS && sm <= WTAIL_SM;
+}
+static CfKernel chanfilt_kernel(int fmt, int64_t M2, size_t N, bool fused) {
     if (fmt == TETRA_CF32 && M2 <= YLDS) return fused ? CF_W_FUSED : CF_W;
+    if (sc16_r(fmt, M2, N)) return fused ? CF_R_FUSED : CF_R;
     if (fmt == TETRA_SC16) return fused ? CF_SC16_FUSED : CF_SC16;
     return fused ? CF_F4_FUSED : CF_F4;
 }
@@ -1644,11 +1955,13 @@ static const void *chanfilt_fn(CfKernel k) {
     case CF_SC16_FUSED: return reinterpret_cast<const void *>(&k_chanfilt<uint2, true>);
     case CF_SC16: return reinterpret_cast<const void *>(&k_chanfilt<uint2, false>);
     case CF_F4_FUSED: return reinterpret_cast<const void *>(&k_chanfilt<float4, true>);
+    case CF_R_FUSED: return reinterpret_cast<const void *>(&k_chanfilt_r<uint4, true>);
+    case CF_R: return reinterpret_cast<const void *>(&k_chanfilt_r<uint4, false>);
     default: return reinterpret_cast<const void *>(&k_chanfilt<float4, false>);
     }
 }
 static const char *const CF_NAMES[] = {"k_chanfilt_w", "k_chanfilt_w", "k_chanfilt", "k_chanfilt", "k_chanfilt",
-                                       "k_chanfilt"};
+                                       "k_chanfilt", "k_chanfilt_r", "k_chanfilt_r"};
 
 // Stage-1 taps and the per-branch stage-2 tap table (k_chanfilt), then the launch.
 static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *x, int fmt, size_t C, size_t N,
@@ -1658,13 +1971,16 @@ static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void 
     if (!coef) return TETRA_E_NOMEM;
     float hc[CF_COEF];
     static const int i0[3] = {320, 318, 319}, off[3] = {0, 4, 7};
-    for (int j = 0; j < 64; ++j) hc[j] = j < 48 ? P->h1[j] : 0.f;
+    for (int j = 0; j < 64; ++j) {
+        hc[j] = j < 48 ? P->h1[j] : 0.f;
+        hc[64 + j] = hc[j] * (1.0f / 32768.0f);   // k_chanfilt_r's SC16 taps: the sample scale folded in (exact)
+    }
     // A fragment of k-step ks for lane l: A[i = l & 15][s = 4 ks + (l >> 4)], row i = 3q + c
     for (int ks = 0; ks < S2K; ++ks)
         for (int l = 0; l < 64; ++l) {
             const int i = l & 15, sidx = 4 * ks + (l >> 4), q = i / 3, c = i % 3;
             const int j = sidx - 10 * q - off[c];
-            hc[64 + 64 * ks + l] = i < 15 && j >= 0 && j < TPP ? P->hp[i0[c] - 3 * j] : 0.f;
+            hc[128 + 64 * ks + l] = i < 15 && j >= 0 && j < TPP ? P->hp[i0[c] - 3 * j] : 0.f;
         }
     // upload only when the taps or the workspace changed: a per-call pageable copy would sit on the
     // stream in front of every launch
@@ -1676,30 +1992,38 @@ static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void 
     PROF(ctx, fused ? "etsi_demod" : "etsi_chanfilt");
     const TimingOut to = fused ? *fused : TimingOut{};
     const dim3 g((unsigned)C), b(256);
-    switch (chanfilt_kernel(fmt, M2, fused != nullptr)) {
+    switch (chanfilt_kernel(fmt, M2, N, fused != nullptr)) {
+    case CF_R_FUSED:
+        hipLaunchKernelGGL((k_chanfilt_r<uint4, true>), g, b, 0, ctx->stream, (const uint4 *)x, (long)N, (int)M1,
+                           (int)M2, coef + 64, coef + 128, y, to);
+        break;
+    case CF_R:
+        hipLaunchKernelGGL((k_chanfilt_r<uint4, false>), g, b, 0, ctx->stream, (const uint4 *)x, (long)N, (int)M1,
+                           (int)M2, coef + 64, coef + 128, y, to);
+        break;
     case CF_W_FUSED:
         hipLaunchKernelGGL((k_chanfilt_w<true>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1, (int)M2,
-                           coef, coef + 64, y, to);
+                           coef, coef + 128, y, to);
         break;
     case CF_W:
         hipLaunchKernelGGL((k_chanfilt_w<false>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1, (int)M2,
-                           coef, coef + 64, y, to);
+                           coef, coef + 128, y, to);
         break;
     case CF_SC16_FUSED:
         hipLaunchKernelGGL((k_chanfilt<uint2, true>), g, b, 0, ctx->stream, (const uint2 *)x, (long)N, (int)M1, (int)M2,
-                           coef, coef + 64, y, to);
+                           coef, coef + 128, y, to);
         break;
     case CF_SC16:
         hipLaunchKernelGGL((k_chanfilt<uint2, false>), g, b, 0, ctx->stream, (const uint2 *)x, (long)N, (int)M1,
-                           (int)M2, coef, coef + 64, y, to);
+                           (int)M2, coef, coef + 128, y, to);
         break;
     case CF_F4_FUSED:
         hipLaunchKernelGGL((k_chanfilt<float4, true>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1,
-                           (int)M2, coef, coef + 64, y, to);
+                           (int)M2, coef, coef + 128, y, to);
         break;
     default:
         hipLaunchKernelGGL((k_chanfilt<float4, false>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1,
-                           (int)M2, coef, coef + 64, y, to);
+                           (int)M2, coef, coef + 128, y, to);
     }
     HIP_TRY(ctx, hipGetLastError());
     return TETRA_OK;
@@ -1722,9 +2046,8 @@ int tetra_etsi_kernel_info(tetra_ctx *ctx, const tetra_etsi_plan *P, int fmt, si
     if (!ctx || !P || (fmt != TETRA_CF32 && fmt != TETRA_SC16)) return TETRA_E_INVALID;
     int64_t M1, M2, sm;
     tetra_etsi_lengths(P, N, &M1, &M2, &sm);
-    if (fused)   // the fused form's own condition (tetra_demod_etsi_fmt)
-        fused = fmt == TETRA_SC16 ? M2 + sm <= CF_LDS2_SC16 : (M2 <= YLDS && sm <= 2 * 4 * WIMG4);
-    const CfKernel k = chanfilt_kernel(fmt, M2, fused != 0);
+    if (fused) fused = fused_fits(fmt, M2, sm, N);   // the fused form's own condition (tetra_demod_etsi_fmt)
+    const CfKernel k = chanfilt_kernel(fmt, M2, N, fused != 0);
     hipFuncAttributes a;
     HIP_TRY(ctx, hipFuncGetAttributes(&a, chanfilt_fn(k)));
     if (name && name_len) snprintf(name, name_len, "%s", CF_NAMES[k]);
@@ -1818,10 +2141,11 @@ int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *i
     // fused: timing runs in the channel filter's workgroup on y in LDS (cf32: y never leaves LDS;
     // SC16: y round-trips through a C x M2 scratch and is re-staged into the freed image/ring)
     // (measured: cf32 with y through L2 at four workgroups per CU, as SC16 does, is 2.5 % slower)
-    const bool fuse = fmt == TETRA_SC16 ? M2 + sm <= CF_LDS2_SC16 : (M2 <= YLDS && sm <= 2 * 4 * WIMG4);
+    const bool fuse = fused_fits(fmt, M2, sm, N);
     if (fuse) {
-        float2 *ys = nullptr;
-        if (fmt == TETRA_SC16 && !(ys = (float2 *)ws(ctx, S_W3, C * (size_t)M2 * 8))) return st.finish();
+        float2 *ys = nullptr;   // k_chanfilt<uint2>: y's round trip
+        if (fmt == TETRA_SC16 && !sc16_r(fmt, M2, N) && !(ys = (float2 *)ws(ctx, S_W3, C * (size_t)M2 * 8)))
+            return st.finish();
         const TimingOut to{P->gain, P->soft_scale, (float2 *)so, sbo, ho, no, (float4 *)dg, (int)smax};
         rc = launch_chanfilt(ctx, P, x, fmt, C, N, M1, M2, ys, &to);
         if (rc) return rc;
