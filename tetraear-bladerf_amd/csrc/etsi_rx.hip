@@ -4,16 +4,15 @@
 // north_star asks for, restating oracle/etsi_oracle.c operation for operation (explicit fmaf,
 // emulated 64-lane reductions, a libm-free atan2), so GPU and oracle results are bit-identical.
 //
-//   k_chanfilt_w stage 1: 48-tap decimate-by-10 FIR (2.4 MSps -> 240 kHz), stage 2: polyphase RRC
+//   k_chanfilt_r stage 1: 48-tap decimate-by-10 FIR (2.4 MSps -> 240 kHz), stage 2: polyphase RRC
 //                (alpha 0.35, 321 taps at 720 kHz) resampler x3/10 -> 72 kHz = 4 samples/symbol,
-//                then the timing stage (fused).  cf32 chunks up to YLDS outputs: the workgroup's
-//                four waves stream the channel's quarters independently (640-sample wave tiles,
-//                register prefetch four tiles deep, private LDS image and stage-1 buffer, stage 2 in
-//                one-MFMA-tile bursts on v_mfma_f32_16x16x4_f32 -- exact f32: banded tap matrix x 16
-//                columns of 5 output triples), y held in LDS.  8 B read per input sample.
-//   k_chanfilt_r the per-wave filter for SC16 (4 B/sample in) with stage 1 in registers: a lane's
-//                10-sample block from the wave's LDS image, the next four blocks from its row
-//                neighbours by DPP (v_fmac_f32_dpp), 48-output wave tiles, y in LDS.
+//                then the timing stage (fused).  cf32 (8 B/sample) and SC16 (4 B/sample) chunks up
+//                to YLDS outputs: the workgroup's four waves stream the channel's quarters
+//                independently (480-sample wave tiles, register prefetch, private LDS image and
+//                stage-1 buffer; stage 1 in registers: a lane's 10-sample block from the image, the
+//                next four blocks from its row neighbours by DPP folded into v_fmac_f32_dpp; stage 2
+//                in one-MFMA-tile bursts on v_mfma_f32_16x16x4_f32 -- exact f32: banded tap matrix x
+//                16 columns of 5 output triples), y held in LDS.
 //   k_chanfilt   the same filter with workgroup-wide 2560-sample tiles (barrier per tile, stage 2
 //                every 8 tiles): SC16 rows that are not a multiple of four samples (y round-tripped
 //                through L2, four workgroups per CU) and chunks longer than YLDS outputs.
@@ -387,8 +386,6 @@ template <> struct CfCfg<uint2> { static constexpr int s2_every = 8, lr = 2312; 
 constexpr int TPP = 107;        // RRC taps per polyphase branch (Lp = 321 = 3 x 107)
 constexpr int PFD = 2;          // k_chanfilt: input tiles in flight per workgroup (register prefetch
                                 // depth, pa/pb; 3 and 4 measured no faster)
-constexpr int PFDW = 4;         // k_chanfilt_w: input tiles in flight per wave (pa/pb/pc/pd, 254 VGPRs,
-                                // no spill; same box: 2 -> 3 -1.5 %, 3 -> 4 -0.6 % serial demod)
 constexpr int YLDS = 3904;      // cf32: stage-2 outputs held in LDS (a 131072-sample chunk has 3899)
 // Stage 2 on the matrix cores (v_mfma_f32_16x16x4_f32: bit-for-bit a k-ordered fmaf chain).  One
 // MFMA tile: 16 columns = 8 segments x (re, im), each segment S2Q consecutive triples; row
@@ -595,7 +592,7 @@ __global__ __launch_bounds__(256, cf_waves<In>()) void k_chanfilt(const In *__re
         if (k >= 0 && k < M1) {
             const float4 *w = xin + 5 * tid + 4;
             pf2 a = {0.f, 0.f};
-            if constexpr (YL) {   // three groups of 16 taps, the next group's reads in flight (k_chanfilt_w)
+            if constexpr (YL) {   // three groups of 16 taps, the next group's reads in flight
                 float4 ta[4], xa[8], tb[4], xb[8];
                 auto rd = [&](float4 (&T)[4], float4 (&X)[8], int g) __attribute__((always_inline)) {
 #pragma unroll
@@ -766,10 +763,9 @@ __global__ __launch_bounds__(256, cf_waves<In>()) void k_chanfilt(const In *__re
 }
 
 // --------------------------------------------------------------------------- per-wave channel filter
-// cf32 with y in LDS (M2 <= YLDS): the workgroup's waves stream the channel's quarters
+// cf32 and SC16 with y in LDS (M2 <= YLDS): the workgroup's waves stream the channel's quarters
 // independently.  Wave w owns the stage-2 triples [U_w, U_w+1) and the stage-1 outputs
-// [K_w, K_w+1), K_w = 10 U_w (the last wave's end is M1), in 640-sample wave tiles (one stage-1
-// output per lane, five 16-B loads per lane, four tiles in flight) with its own LDS image and
+// [K_w, K_w+1), K_w = 10 U_w (the last wave's end is M1), in wave tiles with its own LDS image and
 // stage-1 buffer, and runs a one-MFMA-tile stage-2 burst (40 triples: one dependent chain of 39
 // MFMAs) whenever 40 triples have their windows.  So the stream has no workgroup barrier until the
 // channel ends, and a burst stalls one wave's quarter of the loads in flight instead of the whole
@@ -778,21 +774,15 @@ __global__ __launch_bounds__(256, cf_waves<In>()) void k_chanfilt(const In *__re
 // ones of wave w + 1, which that wave also copies into a seam buffer.  A wave bursts every ready
 // triple at its last tile, so after the one barrier at the channel's end it appends its seam and
 // runs one burst of the <= 12 triples left, then the timing tail as in k_chanfilt.  Every output is
-// the same fma chain as in k_chanfilt (bit-identical to the oracle).
-constexpr int WT_IN4 = 320;                 // sample pairs per wave tile (640 samples)
-constexpr int WIMG4 = HALO / 2 + WT_IN4;    // wave image (float4): 48-sample halo + the tile
+// the same fma chain as in k_chanfilt (bit-identical to the oracle).  (Round 3 ran cf32 on
+// k_chanfilt_w, the same structure with each lane reading its whole 48-sample window and the taps
+// from LDS; k_chanfilt_r below replaced it)
 constexpr int WLR = 568;                    // wave stage-1 buffer (float2): < 567 entries in the stream,
                                             // <= 265 in the channel's last (seam) burst
 constexpr int SEAM = 112;                   // >= the 104 outputs a left neighbour's last triples need
 constexpr int UMIN = 16;                    // triples per wave at least (10 UMIN >= SEAM)
-constexpr int WSMEM4 = 14 + 4 * WIMG4 + (4 * WLR + 3 * SEAM + YLDS) / 2;   // float4
-// two workgroups per CU with >= 9.5 KB of the CU's LDS left for the lower MAC's kernels
-// (k_etsi_viterbi 7 KB, k_etsi_sync 2.4 KB), which the bench's pipeline runs beside the next demod
-static_assert(2 * WSMEM4 * 16 + 7 * 1024 + 2560 <= 160 * 1024, "per-wave demod LDS");
 static_assert(sizeof(TrackOut) + sizeof(int) <= 32 && (4 * WLR + 3 * SEAM) % 2 == 0, "per-wave demod LDS carving");
-// fused tail staging: sm symbols in the stage-1 buffers; 8 sm (d_j) + 2 sm + sm bytes in the images
-constexpr int WTAIL_SM = YLDS / 4 + 2;
-static_assert(WTAIL_SM * 8 <= 4 * WLR * 8 && 11 * WTAIL_SM + 32 + 1024 <= 4 * WIMG4 * 16, "tail staging LDS");
+constexpr int WTAIL_SM = YLDS / 4 + 2;      // the fused tail's symbols per channel at most
 
 // cross-lane LDS hand-off inside one wave: a wave's LDS instructions execute in order, so only the
 // compiler has to be kept from moving accesses across this point (no s_waitcnt, no s_barrier)
@@ -801,235 +791,36 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-template <bool FUSE>
-__global__ __launch_bounds__(256, 2) void k_chanfilt_w(const float4 *__restrict__ iq, long N, int M1, int M2,
-                                                       const float *__restrict__ h1, const float *__restrict__ afrag,
-                                                       float2 *__restrict__ y, TimingOut to) {
-    // one LDS array, carved by hand: the taps first, so their broadcast reads address them with the
-    // instruction's 16-bit offset from one zero register (past 64 KiB each needs an address VGPR)
-    __shared__ float4 smem[WSMEM4];
-    float4 *htap = smem;                                                      // 12 stage-1 tap quads
-    TrackOut *tro = reinterpret_cast<TrackOut *>(smem + 12);                  // 2 float4
-    float4 *img = smem + 14;                                                  // 4 wave images
-    float2 *lin_all = reinterpret_cast<float2 *>(img + 4 * WIMG4);            // 4 stage-1 buffers
-    float2 *seam = lin_all + 4 * WLR;   // seam[w - 1]: wave w's first SEAM stage-1 outputs
-    float *yb = reinterpret_cast<float *>(seam + 3 * SEAM);                   // y as (re, im) floats
-    const int ch = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: the partition below is scalar
-    if (tid < 12)
-        htap[tid] = make_float4(h1[4 * tid], h1[4 * tid + 1], h1[4 * tid + 2], h1[4 * tid + 3]);
-    float4 *xw = img + wv * WIMG4;
-    float2 *lin = lin_all + wv * WLR;
-    // stage 2 reads whole windows, zero taps included: every entry must be finite
-    for (int i = lane; i < WLR; i += 64) lin[i] = make_float2(0.f, 0.f);
-    float at[S2K];
-#pragma unroll
-    for (int k = 0; k < S2K; ++k) at[k] = afrag[64 * k + lane];
-    // landed before the stream starts (else hipcc re-waits for them inside the loop, behind the
-    // prefetch loads)
-    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) (gfx9 encoding: expcnt 7, lgkmcnt 15 = no wait)
-    // the partition: nw waves of UQ triples (fewer waves for short chunks, so that every wave but
-    // the last owns >= SEAM stage-1 outputs)
-    const int UT = (M2 + 2) / 3;
-    const int nw = min(4, max(1, UT / UMIN));
-    const int UQ = (UT + nw - 1) / nw;
-    const bool active = wv < nw;
-    const bool has_right = wv + 1 < nw;
-    const int u_beg = min(wv * UQ, UT), u_end = has_right ? (wv + 1) * UQ : UT;
-    const int K0 = 10 * u_beg, K1 = has_right ? 10 * u_end : M1;
-    const int ntile = active ? (K1 - K0 + 4 + 63) / 64 : 0;   // wave tiles with kfirst < K1
-    // tile t: lane l computes x240[K0 + 64 t - 4 + l] from samples 10 K0 + 640 t - 40 + 10 l + [0, 48),
-    // image float4 4 + 5 l + [0, 24); loads past the wave's last needed pair re-read that pair
-    const float4 *xp = iq + (size_t)ch * (N / 2) + 5L * K0;
-    const int qlast = active ? (int)(min(5L * (K1 - 1) + 23, N / 2 - 1) - 5L * K0) : 0;
-    // a buffer resource over the wave's pairs [0, qlast]: loads past it return 0 without touching
-    // memory (those samples only feed outputs >= K1, never computed), and the offsets are 32-bit
-    // (lane part + instruction offset + the tile's scalar offset), so a load costs no address VALU
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float4 *>(xp), 0,
-                                                                        (qlast + 1) * 16, 0x00020000);
-    auto load_tile = [&](float4 (&pf)[5], int t) __attribute__((always_inline)) {
-#pragma unroll
-        for (int r = 0; r < 5; ++r) {
-            const nt_f4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, (r * 64 + lane) * 16, t * WT_IN4 * 16, 2 /* nt */);
-            pf[r] = make_float4(v.x, v.y, v.z, v.w);
-        }
-    };
-    int kbase = K0;      // x240 index of lin[0]
-    int u_done = u_beg;  // triples [u_beg, u_done) are in yb
-    const int kg = lane >> 4, seg = (lane & 15) >> 1, comp = lane & 1;
-    const float *lf = reinterpret_cast<const float *>(lin);
-    // one MFMA tile: triples [u_done, u_done + 40) as 8 segments x 5 (columns = 2 seg + comp), only
-    // triples < u_lim stored; a column past u_lim reads the buffer's start (finite, never stored)
-    auto burst = [&](int u_lim) __attribute__((always_inline)) {
-        const int U0 = u_done + S2Q * seg;
-        const int b0 = U0 < u_lim ? 2 * (10 * U0 - kbase + kg) + comp : 2 * kg + comp;
-        // B operands one 13-step chunk ahead of the MFMAs that use them (hipcc otherwise waits one
-        // LDS round trip before every MFMA pair of the dependent chain)
-        float bv[S2K];
-        f4 c = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s2 = 0; s2 < 13; ++s2) bv[s2] = lf[b0 + 8 * s2];
-#pragma unroll
-        for (int s3 = 0; s3 < 3; ++s3) {
-            __builtin_amdgcn_sched_barrier(0);
-            if (s3 < 2) {
-#pragma unroll
-                for (int s2 = 13 * s3 + 13; s2 < 13 * s3 + 26; ++s2) bv[s2] = lf[b0 + 8 * s2];
-            }
-#pragma unroll
-            for (int s2 = 13 * s3; s2 < 13 * s3 + 13; ++s2)
-                c = __builtin_amdgcn_mfma_f32_16x16x4f32(at[s2], bv[s2], c, 0, 0, 0);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = 4 * kg + r, q = i / 3, m = 3 * U0 + i;
-            if (i < 15 && U0 + q < u_lim && m < M2) yb[2 * m + comp] = c[r];
-        }
-    };
-    auto tile = [&](int t, float4 (&pf)[5]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int r = 0; r < 5; ++r) xw[HALO / 2 + r * 64 + lane] = pf[r];
-        __builtin_amdgcn_sched_barrier(0);
-        load_tile(pf, t + PFDW);
-        wave_sync();
-        const int k = K0 + 64 * t - 4 + lane;
-        if (k >= K0 && k < K1) {
-            const float4 *w = xw + 5 * lane + 4;
-            pf2 a = {0.f, 0.f};
-            // the 48-tap chain in three groups of 16 taps (4 tap quads + 8 sample pairs each), the
-            // next group's LDS reads in flight during this group's FMAs: left to itself hipcc keeps
-            // two reads ahead of the chain, one LDS round trip per two FMAs (~24 per tile)
-            float4 ta[4], xa[8], tb[4], xb[8];
-            auto rd = [&](float4 (&T)[4], float4 (&X)[8], int g) __attribute__((always_inline)) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    T[i] = htap[4 * g + i];
-                    X[2 * i] = w[8 * g + 2 * i];
-                    X[2 * i + 1] = w[8 * g + 2 * i + 1];
-                }
-            };
-            auto fm = [&](const float4 (&T)[4], const float4 (&X)[8]) __attribute__((always_inline)) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float4 t4 = T[i], x0 = X[2 * i], x1 = X[2 * i + 1];
-                    a = pfma(t4.x, pf2{x0.x, x0.y}, a);
-                    a = pfma(t4.y, pf2{x0.z, x0.w}, a);
-                    a = pfma(t4.z, pf2{x1.x, x1.y}, a);
-                    a = pfma(t4.w, pf2{x1.z, x1.w}, a);
-                }
-            };
-            rd(ta, xa, 0);
-            rd(tb, xb, 1);
-            __builtin_amdgcn_sched_barrier(0);
-            fm(ta, xa);
-            __builtin_amdgcn_sched_barrier(0);
-            rd(ta, xa, 2);
-            __builtin_amdgcn_sched_barrier(0);
-            fm(tb, xb);
-            __builtin_amdgcn_sched_barrier(0);
-            fm(ta, xa);
-            lin[k - kbase] = make_float2(a.x, a.y);
-            if (wv > 0 && k - K0 < SEAM) seam[(wv - 1) * SEAM + k - K0] = make_float2(a.x, a.y);
-        }
-        wave_sync();
-        // halo for the next tile: image samples [0, 48) = this tile's [640, 688)
-        if (lane < HALO / 2) xw[lane] = xw[WT_IN4 + lane];
-        // triple u has its window once 10 u + 113 <= kav
-        const int kav = min(K0 + 64 * t + 59, K1 - 1);
-        const int u_rdy = kav >= 113 ? min((kav - 113) / 10 + 1, u_end) : 0;
-        // bursts of 40; at the wave's last tile also the rest of the ready triples, so that only
-        // the seam's (<= 12) remain for after the barrier
-        while (u_rdy - u_done >= S2T || (t == ntile - 1 && u_rdy > u_done)) {
-            const int ul = min(u_done + S2T, u_rdy);
-            burst(ul);
-            u_done = ul;
-            // keep x240[10 u_done, kav] (<= 167 entries) at the buffer's front
-            const int from = 10 * u_done - kbase, cnt = kav + 1 - 10 * u_done;
-            float2 v[3];
-#pragma unroll
-            for (int e = 0; e < 3; ++e) v[e] = lane + 64 * e < cnt ? lin[from + lane + 64 * e] : make_float2(0.f, 0.f);
-            wave_sync();
-#pragma unroll
-            for (int e = 0; e < 3; ++e)
-                if (lane + 64 * e < cnt) lin[lane + 64 * e] = v[e];
-            kbase = 10 * u_done;
-        }
-        wave_sync();
-    };
-    __syncthreads();   // htap
-    // four register sets, explicitly (an array over them costs VGPRs, round 2); the deeper prefetch
-    // keeps a workgroup's stream fed while its CU neighbour runs its timing tail
-    static_assert(PFDW == 4, "pa / pb / pc / pd below");
-    float4 pa[5], pb[5], pc[5], pd[5];
-    if (ntile > 0) {
-        load_tile(pa, 0);
-        load_tile(pb, 1);
-        load_tile(pc, 2);
-        load_tile(pd, 3);
-    }
-    int t = 0;
-    for (; t + 3 < ntile; t += 4) {
-        tile(t, pa);
-        tile(t + 1, pb);
-        tile(t + 2, pc);
-        tile(t + 3, pd);
-    }
-    if (t < ntile) tile(t, pa);
-    if (t + 1 < ntile) tile(t + 1, pb);
-    if (t + 2 < ntile) tile(t + 2, pc);
-    __syncthreads();   // every wave's seam and in-loop bursts
-    if (active && u_done < u_end) {
-        if (has_right) {   // x240[K1, K1 + SEAM) from wave wv + 1 (K1 - kbase <= 120)
-            for (int i = lane; i < SEAM; i += 64) lin[K1 - kbase + i] = seam[wv * SEAM + i];
-            wave_sync();
-        }
-        burst(u_end);   // <= 12 triples
-    }
-    __syncthreads();
-    if constexpr (FUSE) {
-        // the tail's LDS: d_j scratch, soft bits and hard dibits in the freed wave images, the
-        // symbols in the freed stage-1 buffers (the launch guarantees sm <= WTAIL_SM)
-        const int sm = M2 / 4 + 2;
-        int8_t *ib = reinterpret_cast<int8_t *>(img);
-        const TailStage st{lin_all, ib + ((8 * sm + 15) & ~15), reinterpret_cast<uint8_t *>(ib + ((10 * sm + 31) & ~15))};
-        int *prog = reinterpret_cast<int *>(tro + 1);   // the word after TrackOut in its 32-B slot
-        // the Oerder-Meyr parts (1 KB) at the images' end, past the tail staging (<= 10.8 KB)
-        float *om = reinterpret_cast<float *>(reinterpret_cast<uint8_t *>(img) + 4 * WIMG4 * 16 - 1024);
-        timing_tail(reinterpret_cast<const float2 *>(yb), reinterpret_cast<float2 *>(img), to, M2, ch, tid, tro, prog,
-                    &st, om);
-    } else {
-        copy_out(reinterpret_cast<uint8_t *>(y + (size_t)ch * M2), reinterpret_cast<const uint8_t *>(yb), 8 * M2, tid);
-    }
-}
-
 // --------------------------------------------------------------------------- register stage 1
-// k_chanfilt_r: the per-wave channel filter with stage 1 out of LDS.  In k_chanfilt_w every lane
-// reads its 48-sample window (24 float4) and the 48 taps (12 broadcast float4) from LDS for one
-// output, ~5 LDS cycles per output of the CU's 128 B/cycle, and that is what bounds the filter once
-// the input needs no HBM (timing builds: the input L2-resident, 0.93 ms per 8192 x 131072 batch; its
-// stage-1 chain cut to a third, 0.66).  Here a lane reads only its own 10-sample block from the
-// image (5 loads of 2 samples) and takes the next four blocks from its row neighbours with DPP
-// (row_shl:p reads lane + p of the same 16-lane row): a row of 16 lanes holds 16 consecutive blocks
-// and computes the outputs of its first 12, so a wave tile is 48 outputs (480 new samples, a 40-sample
-// halo).  The taps sit in registers.  Each output is still the oracle's ascending-j fma chain
-// (x[10 k + j] is sample j mod 10 of lane + j / 10's block), bit-identical to k_chanfilt_w.
-// SC16 keeps its samples as raw dwords in the image (re low 16 bits, im high) and folds the 2^-15
-// scale into the taps (an exact power of two: fma(h 2^-15, x, a) == fma(h, x 2^-15, a)).
-// Everything after stage 1 -- the wave partition, seams, MFMA bursts, the fused timing tail -- is
-// k_chanfilt_w's.
+// k_chanfilt_r: the per-wave channel filter with stage 1 out of LDS.  With each lane reading its
+// whole 48-sample window (24 float4) and the 48 taps (12 broadcast float4) from LDS for one output
+// (round 3's k_chanfilt_w), stage 1 costs ~5 LDS cycles per output of the CU's 128 B/cycle, and
+// that bounds the filter once the input needs no HBM (timing builds, input L2-resident: 0.93 ms per
+// 8192 x 131072 batch without the tail; with stage 1's chain cut to a third, 0.66).  Here a lane reads
+// only its own 10-sample block from the image (5 loads of 2 samples) and takes the next four blocks
+// from its row neighbours with DPP (row_shl:p reads lane + p of the same 16-lane row): a row of 16
+// lanes holds 16 consecutive blocks and computes the outputs of its first 12, so a wave tile is 48
+// outputs (480 new samples, a 40-sample halo).  The taps sit in registers.  Each output is still the
+// oracle's ascending-j fma chain (x[10 k + j] is sample j mod 10 of lane + j / 10's block),
+// bit-identical.  SC16 keeps its samples as raw dwords in the image (re low 16 bits, im high) and
+// folds the 2^-15 scale into the taps (an exact power of two: fma(h 2^-15, x, a) == fma(h, x 2^-15, a)).
 constexpr int RT_K = 48;            // stage-1 outputs per wave tile (4 rows x 12)
 constexpr int RT_IN = 10 * RT_K;    // new input samples per wave tile
 constexpr int RHALO = 40;           // image samples carried over from the previous tile
 template <typename In> struct RCfg;
-// SC16: a 16-B load = 4 samples; 4 tiles in flight per wave (same box, serial: 6 -> 4 -1 %, 3 = 4)
+// input tiles in flight per wave (register prefetch).  SC16: a 16-B load = 4 samples (same box,
+// serial: 6 -> 4 tiles -1 %, 3 = 4); cf32: 2 samples, 3 tiles (4: 252 VGPRs, no faster)
 template <> struct RCfg<uint4> { static constexpr int bps = 4, pf = 4; };
+template <> struct RCfg<float4> { static constexpr int bps = 8, pf = 3; };
 template <typename In> constexpr int r_chunks() { return RT_IN * RCfg<In>::bps / 16; }   // 16-B loads per tile
 template <typename In> constexpr int r_img16() { return (RHALO + RT_IN) * RCfg<In>::bps / 16; }
 template <typename In> constexpr int r_smem4() { return 2 + 4 * r_img16<In>() + (4 * WLR + 3 * SEAM + YLDS) / 2; }
 // tail staging over the freed images + stage-1 buffers: d_j, soft bits, hard dibits, O-M parts, symbols
 template <typename In> constexpr int r_tail_bytes() { return 19 * WTAIL_SM + 48 + 1024; }
 static_assert(r_tail_bytes<uint4>() <= 4 * r_img16<uint4>() * 16 + 4 * WLR * 8, "k_chanfilt_r tail staging");
-static_assert(2 * r_smem4<uint4>() * 16 + 7 * 1024 + 2560 <= 160 * 1024, "k_chanfilt_r LDS");
+// two workgroups per CU with >= 9.5 KB of the CU's LDS left for the lower MAC's kernels
+// (k_etsi_viterbi 7 KB, k_etsi_sync 2.4 KB), which the bench's pipeline runs beside the next demod
+static_assert(2 * r_smem4<float4>() * 16 + 7 * 1024 + 2560 <= 160 * 1024, "k_chanfilt_r LDS");
 
 // ar += h[q] * x_re[q], ai += h[q] * x_im[q] for q < N in order, x taken from lane + P of this
 // lane's 16-lane row (row_shl:P; a lane past the row's end reads 0 -- only lanes 12..15 do, and
@@ -1140,14 +931,17 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_r(const In *__restrict__ iq
     float at[S2K];
 #pragma unroll
     for (int k = 0; k < S2K; ++k) at[k] = afrag[64 * k + lane];
+    // SC16: the launch passes the taps pre-scaled by 2^-15.  Taps 10..47 are v_fmac_f32_dpp's src1 and
+    // must be VGPRs (left as SGPRs hipcc copies them into VGPRs every tile); taps 0..9 (the in-lane
+    // products) stay scalar operands
     float hv[48];
 #pragma unroll
     for (int j = 0; j < 48; ++j) {
-        hv[j] = h1[j];   // SC16: the launch passes the taps pre-scaled by 2^-15
-        asm volatile("" : "+v"(hv[j]));   // held in VGPRs (v_fmac_f32_dpp's src1; as SGPRs hipcc copies them per tile)
+        hv[j] = h1[j];
+        if (j >= 10) asm volatile("" : "+v"(hv[j]));
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): landed before the stream starts
-    // the partition (k_chanfilt_w's)
+    // the partition
     const int UT = (M2 + 2) / 3;
     const int nw = min(4, max(1, UT / UMIN));
     const int UQ = (UT + nw - 1) / nw;
@@ -1179,7 +973,11 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_r(const In *__restrict__ iq
     int u_done = u_beg;  // triples [u_beg, u_done) are in yb
     const int kg = lane >> 4, seg = (lane & 15) >> 1, comp = lane & 1;
     const float *lf = reinterpret_cast<const float *>(lin);
-    auto burst = [&](int u_lim) __attribute__((always_inline)) {   // k_chanfilt_w's
+    // one MFMA tile: triples [u_done, u_done + 40) as 8 segments x 5 (columns = 2 seg + comp), only
+    // triples < u_lim stored; a column past u_lim reads the buffer's start (finite, never stored).
+    // B operands one 13-step chunk ahead of the MFMAs that use them (hipcc otherwise waits one LDS
+    // round trip before every MFMA pair of the dependent chain)
+    auto burst = [&](int u_lim) __attribute__((always_inline)) {
         const int U0 = u_done + S2Q * seg;
         const int b0 = U0 < u_lim ? 2 * (10 * U0 - kbase + kg) + comp : 2 * kg + comp;
         float bv[S2K];
@@ -1934,34 +1732,36 @@ static int etsi_check(tetra_ctx *ctx, const tetra_etsi_plan *P) {
 }
 
 // Which channel-filter kernel a launch takes (launch_chanfilt, tetra_etsi_kernel_info).
-enum CfKernel { CF_W_FUSED, CF_W, CF_SC16_FUSED, CF_SC16, CF_F4_FUSED, CF_F4, CF_R_FUSED, CF_R };
-// SC16 on the register-stage-1 per-wave filter: y in LDS (M2 <= YLDS) and rows of whole 16-B loads
-static bool sc16_r(int fmt, int64_t M2, size_t N) { return fmt == TETRA_SC16 && M2 <= YLDS && N % 4 == 0; }
+enum CfKernel { CF_R_FUSED, CF_R, CF_SC16_FUSED, CF_SC16, CF_F4_FUSED, CF_F4 };
+// the per-wave filter (k_chanfilt_r): y in LDS (M2 <= YLDS); SC16 rows of whole 16-B loads
+static bool per_wave(int fmt, int64_t M2, size_t N) { return M2 <= YLDS && (fmt == TETRA_CF32 || N % 4 == 0); }
 // the fused demod's condition: y (and the tail's staging) fit the kernel's LDS
 static bool fused_fits(int fmt, int64_t M2, int64_t sm, size_t N) {
-    if (fmt == TETRA_SC16 && !sc16_r(fmt, M2, N)) return M2 + sm <= CF_LDS2_SC16;
-    return M2 <= YLDS && sm <= WTAIL_SM;
+    if (!per_wave(fmt, M2, N)) return fmt == TETRA_SC16 && M2 + sm <= CF_LDS2_SC16;
+    return sm <= WTAIL_SM;
 }
 static CfKernel chanfilt_kernel(int fmt, int64_t M2, size_t N, bool fused) {
-    if (fmt == TETRA_CF32 && M2 <= YLDS) return fused ? CF_W_FUSED : CF_W;
-    if (sc16_r(fmt, M2, N)) return fused ? CF_R_FUSED : CF_R;
+    if (per_wave(fmt, M2, N)) return fused ? CF_R_FUSED : CF_R;
     if (fmt == TETRA_SC16) return fused ? CF_SC16_FUSED : CF_SC16;
     return fused ? CF_F4_FUSED : CF_F4;
 }
-static const void *chanfilt_fn(CfKernel k) {
+static const void *chanfilt_fn(CfKernel k, int fmt) {
+    const bool cf = fmt == TETRA_CF32;
     switch (k) {
-    case CF_W_FUSED: return reinterpret_cast<const void *>(&k_chanfilt_w<true>);
-    case CF_W: return reinterpret_cast<const void *>(&k_chanfilt_w<false>);
+    case CF_R_FUSED:
+        return cf ? reinterpret_cast<const void *>(&k_chanfilt_r<float4, true>)
+                  : reinterpret_cast<const void *>(&k_chanfilt_r<uint4, true>);
+    case CF_R:
+        return cf ? reinterpret_cast<const void *>(&k_chanfilt_r<float4, false>)
+                  : reinterpret_cast<const void *>(&k_chanfilt_r<uint4, false>);
     case CF_SC16_FUSED: return reinterpret_cast<const void *>(&k_chanfilt<uint2, true>);
     case CF_SC16: return reinterpret_cast<const void *>(&k_chanfilt<uint2, false>);
     case CF_F4_FUSED: return reinterpret_cast<const void *>(&k_chanfilt<float4, true>);
-    case CF_R_FUSED: return reinterpret_cast<const void *>(&k_chanfilt_r<uint4, true>);
-    case CF_R: return reinterpret_cast<const void *>(&k_chanfilt_r<uint4, false>);
     default: return reinterpret_cast<const void *>(&k_chanfilt<float4, false>);
     }
 }
-static const char *const CF_NAMES[] = {"k_chanfilt_w", "k_chanfilt_w", "k_chanfilt", "k_chanfilt", "k_chanfilt",
-                                       "k_chanfilt", "k_chanfilt_r", "k_chanfilt_r"};
+static const char *const CF_NAMES[] = {"k_chanfilt_r", "k_chanfilt_r", "k_chanfilt", "k_chanfilt", "k_chanfilt",
+                                       "k_chanfilt"};
 
 // Stage-1 taps and the per-branch stage-2 tap table (k_chanfilt), then the launch.
 static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *x, int fmt, size_t C, size_t N,
@@ -1994,20 +1794,20 @@ static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void 
     const dim3 g((unsigned)C), b(256);
     switch (chanfilt_kernel(fmt, M2, N, fused != nullptr)) {
     case CF_R_FUSED:
-        hipLaunchKernelGGL((k_chanfilt_r<uint4, true>), g, b, 0, ctx->stream, (const uint4 *)x, (long)N, (int)M1,
-                           (int)M2, coef + 64, coef + 128, y, to);
+        if (fmt == TETRA_CF32)
+            hipLaunchKernelGGL((k_chanfilt_r<float4, true>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1,
+                               (int)M2, coef, coef + 128, y, to);
+        else
+            hipLaunchKernelGGL((k_chanfilt_r<uint4, true>), g, b, 0, ctx->stream, (const uint4 *)x, (long)N, (int)M1,
+                               (int)M2, coef + 64, coef + 128, y, to);
         break;
     case CF_R:
-        hipLaunchKernelGGL((k_chanfilt_r<uint4, false>), g, b, 0, ctx->stream, (const uint4 *)x, (long)N, (int)M1,
-                           (int)M2, coef + 64, coef + 128, y, to);
-        break;
-    case CF_W_FUSED:
-        hipLaunchKernelGGL((k_chanfilt_w<true>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1, (int)M2,
-                           coef, coef + 128, y, to);
-        break;
-    case CF_W:
-        hipLaunchKernelGGL((k_chanfilt_w<false>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1, (int)M2,
-                           coef, coef + 128, y, to);
+        if (fmt == TETRA_CF32)
+            hipLaunchKernelGGL((k_chanfilt_r<float4, false>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1,
+                               (int)M2, coef, coef + 128, y, to);
+        else
+            hipLaunchKernelGGL((k_chanfilt_r<uint4, false>), g, b, 0, ctx->stream, (const uint4 *)x, (long)N, (int)M1,
+                               (int)M2, coef + 64, coef + 128, y, to);
         break;
     case CF_SC16_FUSED:
         hipLaunchKernelGGL((k_chanfilt<uint2, true>), g, b, 0, ctx->stream, (const uint2 *)x, (long)N, (int)M1, (int)M2,
@@ -2049,7 +1849,7 @@ int tetra_etsi_kernel_info(tetra_ctx *ctx, const tetra_etsi_plan *P, int fmt, si
     if (fused) fused = fused_fits(fmt, M2, sm, N);   // the fused form's own condition (tetra_demod_etsi_fmt)
     const CfKernel k = chanfilt_kernel(fmt, M2, N, fused != 0);
     hipFuncAttributes a;
-    HIP_TRY(ctx, hipFuncGetAttributes(&a, chanfilt_fn(k)));
+    HIP_TRY(ctx, hipFuncGetAttributes(&a, chanfilt_fn(k, fmt)));
     if (name && name_len) snprintf(name, name_len, "%s", CF_NAMES[k]);
     if (lds_bytes) *lds_bytes = (int64_t)a.sharedSizeBytes;
     return TETRA_OK;
@@ -2138,13 +1938,13 @@ int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *i
     int32_t *no = (int32_t *)st.out(nsym, C * 4);
     float *dg = diag ? (float *)st.out(diag, C * 16) : nullptr;
     if (!x || !so || !sbo || !ho || !no) return st.finish();
-    // fused: timing runs in the channel filter's workgroup on y in LDS (cf32: y never leaves LDS;
-    // SC16: y round-trips through a C x M2 scratch and is re-staged into the freed image/ring)
-    // (measured: cf32 with y through L2 at four workgroups per CU, as SC16 does, is 2.5 % slower)
+    // fused: timing runs in the channel filter's workgroup on y in LDS (k_chanfilt_r: y never leaves
+    // LDS; k_chanfilt<uint2>: y round-trips through a C x M2 scratch and is re-staged into the freed
+    // image) (measured: cf32 with y through L2 at four workgroups per CU is 2.5 % slower)
     const bool fuse = fused_fits(fmt, M2, sm, N);
     if (fuse) {
         float2 *ys = nullptr;   // k_chanfilt<uint2>: y's round trip
-        if (fmt == TETRA_SC16 && !sc16_r(fmt, M2, N) && !(ys = (float2 *)ws(ctx, S_W3, C * (size_t)M2 * 8)))
+        if (fmt == TETRA_SC16 && !per_wave(fmt, M2, N) && !(ys = (float2 *)ws(ctx, S_W3, C * (size_t)M2 * 8)))
             return st.finish();
         const TimingOut to{P->gain, P->soft_scale, (float2 *)so, sbo, ho, no, (float4 *)dg, (int)smax};
         rc = launch_chanfilt(ctx, P, x, fmt, C, N, M1, M2, ys, &to);

@@ -29,7 +29,7 @@ def main():
             m["lds_conflict_frac"] = m["SQ_LDS_BANK_CONFLICT"] / m["SQ_LDS_IDX_ACTIVE"]
         res[k] = m
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
-    for k in ("k_chanfilt_w", "k_chanfilt_r", "k_chanfilt", "k_etsi_viterbi"):
+    for k in ("k_chanfilt_r", "k_chanfilt", "k_etsi_viterbi"):
         if k in res:
             print(k, {c: round(v, 3) for c, v in res[k].items() if c.endswith("_frac")})
 

@@ -1,7 +1,7 @@
 # SC16 back on k_chanfilt<uint2> (the barrier-per-tile kernel, y through L2): the "before" side of
-# the k_chanfilt_r A/B
+# the k_chanfilt_r SC16 A/B
 import sys
 s = sys.stdin.read()
-a = "static bool sc16_r(int fmt, int64_t M2, size_t N) { return fmt == TETRA_SC16 && M2 <= YLDS && N % 4 == 0; }"
+a = "static bool per_wave(int fmt, int64_t M2, size_t N) { return M2 <= YLDS && (fmt == TETRA_CF32 || N % 4 == 0); }"
 assert s.count(a) == 1
-sys.stdout.write(s.replace(a, "static bool sc16_r(int, int64_t, size_t) { return false; }"))
+sys.stdout.write(s.replace(a, "static bool per_wave(int fmt, int64_t M2, size_t) { return M2 <= YLDS && fmt == TETRA_CF32; }"))

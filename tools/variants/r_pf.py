@@ -2,6 +2,6 @@
 import os
 import sys
 s = sys.stdin.read()
-a = "struct RCfg<uint4> { static constexpr int bps = 4, pf = 6; }"
+a = "struct RCfg<uint4> { static constexpr int bps = 4, pf = 4; }"
 assert s.count(a) == 1
 sys.stdout.write(s.replace(a, "struct RCfg<uint4> { static constexpr int bps = 4, pf = %d; }" % int(os.environ["RPF"])))

@@ -4,7 +4,7 @@
 import os
 import sys
 s = sys.stdin.read()
-k = s.index("void k_chanfilt_w(")
+k = s.index("void k_chanfilt_r(")
 a = "    const int ch = blockIdx.x, tid = threadIdx.x, lane = tid & 63;\n"
 i = s.index(a, k) + len(a)
 us = int(os.environ["STAGGER_US"])
