@@ -804,32 +804,40 @@ __device__ __forceinline__ void wave_sync() {
 // oracle's ascending-j fma chain (x[10 k + j] is sample j mod 10 of lane + j / 10's block),
 // bit-identical.  SC16 keeps its samples as raw dwords in the image (re low 16 bits, im high) and
 // folds the 2^-15 scale into the taps (an exact power of two: fma(h 2^-15, x, a) == fma(h, x 2^-15, a)).
-constexpr int RT_K = 48;            // stage-1 outputs per wave tile (4 rows x 12)
-constexpr int RT_IN = 10 * RT_K;    // new input samples per wave tile
 constexpr int RHALO = 40;           // image samples carried over from the previous tile
 template <typename In> struct RCfg;
-// input tiles in flight per wave (register prefetch).  SC16: a 16-B load = 4 samples (same box,
-// serial: 6 -> 4 tiles -1 %, 3 = 4); cf32: 2 samples, 3 tiles (4: 252 VGPRs, no faster)
-template <> struct RCfg<uint4> { static constexpr int bps = 4, pf = 4; };
-template <> struct RCfg<float4> { static constexpr int bps = 8, pf = 3; };
-template <typename In> constexpr int r_chunks() { return RT_IN * RCfg<In>::bps / 16; }   // 16-B loads per tile
-template <typename In> constexpr int r_img16() { return (RHALO + RT_IN) * RCfg<In>::bps / 16; }
-template <typename In> constexpr int r_smem4() { return 2 + 4 * r_img16<In>() + (4 * WLR + 3 * SEAM + YLDS) / 2; }
+// nb: 10-sample blocks per lane.  nb = 1: a row's 16 lanes hold 16 blocks and compute the outputs
+// of the first 12 (DPP shifts of 1..4 lanes); nb = 2: lane i holds blocks 2i, 2i + 1, a row 32
+// blocks, outputs of the first 28 (shifts of 1..2 lanes) -- 14 of 16 lanes' work kept instead of 12
+// and the per-tile work (loads, image, halo, burst test) spread over 112 outputs instead of 48.
+// cf32 keeps nb = 1: its 9.3 KB nb = 2 image would not fit two workgroups per CU.
+// pf: input tiles in flight per wave (register prefetch).
+template <> struct RCfg<uint4> { static constexpr int bps = 4, pf = 2, nb = 2, wlr = 632; };   // SC16: 16-B load = 4 samples
+template <> struct RCfg<float4> { static constexpr int bps = 8, pf = 3, nb = 1, wlr = WLR; };  // cf32: 2 samples (4 tiles: spills)
+template <typename In> constexpr int r_tk() { return RCfg<In>::nb == 1 ? 48 : 112; }   // stage-1 outputs per wave tile
+template <typename In> constexpr int r_chunks() { return 10 * r_tk<In>() * RCfg<In>::bps / 16; }   // 16-B loads per tile
+template <typename In> constexpr int r_img16() { return (RHALO + 10 * r_tk<In>()) * RCfg<In>::bps / 16; }
+template <typename In> constexpr int r_smem4() {
+    return 2 + 4 * r_img16<In>() + (4 * RCfg<In>::wlr + 3 * SEAM + YLDS) / 2;
+}
 // tail staging over the freed images + stage-1 buffers: d_j, soft bits, hard dibits, O-M parts, symbols
-template <typename In> constexpr int r_tail_bytes() { return 19 * WTAIL_SM + 48 + 1024; }
-static_assert(r_tail_bytes<uint4>() <= 4 * r_img16<uint4>() * 16 + 4 * WLR * 8, "k_chanfilt_r tail staging");
+constexpr int r_tail_bytes() { return 19 * WTAIL_SM + 48 + 1024; }
+static_assert(r_tail_bytes() <= 4 * r_img16<float4>() * 16 + 4 * WLR * 8, "k_chanfilt_r tail staging");
 // two workgroups per CU with >= 9.5 KB of the CU's LDS left for the lower MAC's kernels
 // (k_etsi_viterbi 7 KB, k_etsi_sync 2.4 KB), which the bench's pipeline runs beside the next demod
-static_assert(2 * r_smem4<float4>() * 16 + 7 * 1024 + 2560 <= 160 * 1024, "k_chanfilt_r LDS");
+static_assert(2 * r_smem4<float4>() * 16 + 7 * 1024 + 2560 <= 160 * 1024, "k_chanfilt_r LDS (cf32)");
+static_assert(2 * r_smem4<uint4>() * 16 + 7 * 1024 + 2560 <= 160 * 1024, "k_chanfilt_r LDS (SC16)");
+// a stage-1 buffer holds < 10 x 39 + 123 + one tile's outputs (the burst test runs once per tile)
+static_assert(RCfg<uint4>::wlr >= 513 + 112 && WLR >= 513 + 48, "stage-1 buffer");
 
 // ar += h[q] * x_re[q], ai += h[q] * x_im[q] for q < N in order, x taken from lane + P of this
-// lane's 16-lane row (row_shl:P; a lane past the row's end reads 0 -- only lanes 12..15 do, and
-// their outputs are not kept): one v_fmac_f32_dpp per product, the DPP folded into the fma (hipcc
-// emits a v_mov_b32_dpp per operand instead and keeps ~76 of them live).  Five products per asm:
-// the hazard recognizer puts a wait state after every asm statement.  The samples' producer (their
-// conversion) precedes this lane's own P = 0 use of them, >= 9 chain steps earlier, so the DPP
-// reads need no wait states of their own.
-template <int P, int N>
+// lane's 16-lane row (row_shl:P; a lane past the row's end reads 0 -- only lanes whose outputs are
+// not kept do): one v_fmac_f32_dpp per product, the DPP folded into the fma (hipcc emits a
+// v_mov_b32_dpp per operand instead and keeps ~76 of them live).  Five products per asm: the hazard
+// recognizer puts a wait state after every asm statement.  A DPP read needs two wait states after
+// the VALU write of its source: where the chain's order does not already put this lane's own use
+// of x (and so its conversion) >= 9 steps earlier, NOP = true opens the block with s_nop 1.
+template <int P, int N, bool NOP = false>
 __device__ __forceinline__ void fmac_rows(float &ar, float &ai, const float *xr, const float *xi, const float *h) {
     if constexpr (P == 0) {
 #pragma unroll
@@ -838,7 +846,7 @@ __device__ __forceinline__ void fmac_rows(float &ar, float &ai, const float *xr,
             ai = fmaf(h[q], xi[q], ai);
         }
     }
-    else if constexpr (P == 1 && N == 5) {
+    else if constexpr (P == 1 && N == 5 && !NOP) {
         asm("v_fmac_f32_dpp %0, %2, %12 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
             "v_fmac_f32_dpp %1, %7, %12 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
             "v_fmac_f32_dpp %0, %3, %13 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
@@ -852,7 +860,43 @@ __device__ __forceinline__ void fmac_rows(float &ar, float &ai, const float *xr,
             : "+v"(ar), "+v"(ai)
             : "v"(xr[0]), "v"(xr[1]), "v"(xr[2]), "v"(xr[3]), "v"(xr[4]), "v"(xi[0]), "v"(xi[1]), "v"(xi[2]), "v"(xi[3]), "v"(xi[4]), "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]), "v"(h[4]));
     }
-    else if constexpr (P == 2 && N == 5) {
+    else if constexpr (P == 1 && N == 5 && NOP) {
+        asm("s_nop 1\n\t"
+            "v_fmac_f32_dpp %0, %2, %12 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %7, %12 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %3, %13 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %8, %13 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %4, %14 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %9, %14 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %5, %15 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %10, %15 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %6, %16 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %11, %16 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            : "+v"(ar), "+v"(ai)
+            : "v"(xr[0]), "v"(xr[1]), "v"(xr[2]), "v"(xr[3]), "v"(xr[4]), "v"(xi[0]), "v"(xi[1]), "v"(xi[2]), "v"(xi[3]), "v"(xi[4]), "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]), "v"(h[4]));
+    }
+    else if constexpr (P == 1 && N == 3 && !NOP) {
+        asm("v_fmac_f32_dpp %0, %2, %8 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %5, %8 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %3, %9 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %6, %9 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %4, %10 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %7, %10 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            : "+v"(ar), "+v"(ai)
+            : "v"(xr[0]), "v"(xr[1]), "v"(xr[2]), "v"(xi[0]), "v"(xi[1]), "v"(xi[2]), "v"(h[0]), "v"(h[1]), "v"(h[2]));
+    }
+    else if constexpr (P == 1 && N == 3 && NOP) {
+        asm("s_nop 1\n\t"
+            "v_fmac_f32_dpp %0, %2, %8 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %5, %8 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %3, %9 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %6, %9 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %4, %10 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %7, %10 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            : "+v"(ar), "+v"(ai)
+            : "v"(xr[0]), "v"(xr[1]), "v"(xr[2]), "v"(xi[0]), "v"(xi[1]), "v"(xi[2]), "v"(h[0]), "v"(h[1]), "v"(h[2]));
+    }
+    else if constexpr (P == 2 && N == 5 && !NOP) {
         asm("v_fmac_f32_dpp %0, %2, %12 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
             "v_fmac_f32_dpp %1, %7, %12 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
             "v_fmac_f32_dpp %0, %3, %13 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
@@ -866,7 +910,43 @@ __device__ __forceinline__ void fmac_rows(float &ar, float &ai, const float *xr,
             : "+v"(ar), "+v"(ai)
             : "v"(xr[0]), "v"(xr[1]), "v"(xr[2]), "v"(xr[3]), "v"(xr[4]), "v"(xi[0]), "v"(xi[1]), "v"(xi[2]), "v"(xi[3]), "v"(xi[4]), "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]), "v"(h[4]));
     }
-    else if constexpr (P == 3 && N == 5) {
+    else if constexpr (P == 2 && N == 5 && NOP) {
+        asm("s_nop 1\n\t"
+            "v_fmac_f32_dpp %0, %2, %12 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %7, %12 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %3, %13 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %8, %13 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %4, %14 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %9, %14 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %5, %15 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %10, %15 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %6, %16 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %11, %16 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            : "+v"(ar), "+v"(ai)
+            : "v"(xr[0]), "v"(xr[1]), "v"(xr[2]), "v"(xr[3]), "v"(xr[4]), "v"(xi[0]), "v"(xi[1]), "v"(xi[2]), "v"(xi[3]), "v"(xi[4]), "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]), "v"(h[4]));
+    }
+    else if constexpr (P == 2 && N == 3 && !NOP) {
+        asm("v_fmac_f32_dpp %0, %2, %8 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %5, %8 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %3, %9 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %6, %9 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %4, %10 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %7, %10 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            : "+v"(ar), "+v"(ai)
+            : "v"(xr[0]), "v"(xr[1]), "v"(xr[2]), "v"(xi[0]), "v"(xi[1]), "v"(xi[2]), "v"(h[0]), "v"(h[1]), "v"(h[2]));
+    }
+    else if constexpr (P == 2 && N == 3 && NOP) {
+        asm("s_nop 1\n\t"
+            "v_fmac_f32_dpp %0, %2, %8 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %5, %8 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %3, %9 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %6, %9 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %4, %10 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %7, %10 row_shl:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            : "+v"(ar), "+v"(ai)
+            : "v"(xr[0]), "v"(xr[1]), "v"(xr[2]), "v"(xi[0]), "v"(xi[1]), "v"(xi[2]), "v"(h[0]), "v"(h[1]), "v"(h[2]));
+    }
+    else if constexpr (P == 3 && N == 5 && !NOP) {
         asm("v_fmac_f32_dpp %0, %2, %12 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
             "v_fmac_f32_dpp %1, %7, %12 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
             "v_fmac_f32_dpp %0, %3, %13 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
@@ -880,7 +960,43 @@ __device__ __forceinline__ void fmac_rows(float &ar, float &ai, const float *xr,
             : "+v"(ar), "+v"(ai)
             : "v"(xr[0]), "v"(xr[1]), "v"(xr[2]), "v"(xr[3]), "v"(xr[4]), "v"(xi[0]), "v"(xi[1]), "v"(xi[2]), "v"(xi[3]), "v"(xi[4]), "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]), "v"(h[4]));
     }
-    else if constexpr (P == 4 && N == 5) {
+    else if constexpr (P == 3 && N == 5 && NOP) {
+        asm("s_nop 1\n\t"
+            "v_fmac_f32_dpp %0, %2, %12 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %7, %12 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %3, %13 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %8, %13 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %4, %14 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %9, %14 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %5, %15 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %10, %15 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %6, %16 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %11, %16 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            : "+v"(ar), "+v"(ai)
+            : "v"(xr[0]), "v"(xr[1]), "v"(xr[2]), "v"(xr[3]), "v"(xr[4]), "v"(xi[0]), "v"(xi[1]), "v"(xi[2]), "v"(xi[3]), "v"(xi[4]), "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]), "v"(h[4]));
+    }
+    else if constexpr (P == 3 && N == 3 && !NOP) {
+        asm("v_fmac_f32_dpp %0, %2, %8 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %5, %8 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %3, %9 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %6, %9 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %4, %10 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %7, %10 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            : "+v"(ar), "+v"(ai)
+            : "v"(xr[0]), "v"(xr[1]), "v"(xr[2]), "v"(xi[0]), "v"(xi[1]), "v"(xi[2]), "v"(h[0]), "v"(h[1]), "v"(h[2]));
+    }
+    else if constexpr (P == 3 && N == 3 && NOP) {
+        asm("s_nop 1\n\t"
+            "v_fmac_f32_dpp %0, %2, %8 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %5, %8 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %3, %9 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %6, %9 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %4, %10 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %7, %10 row_shl:3 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            : "+v"(ar), "+v"(ai)
+            : "v"(xr[0]), "v"(xr[1]), "v"(xr[2]), "v"(xi[0]), "v"(xi[1]), "v"(xi[2]), "v"(h[0]), "v"(h[1]), "v"(h[2]));
+    }
+    else if constexpr (P == 4 && N == 5 && !NOP) {
         asm("v_fmac_f32_dpp %0, %2, %12 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
             "v_fmac_f32_dpp %1, %7, %12 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
             "v_fmac_f32_dpp %0, %3, %13 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
@@ -894,8 +1010,34 @@ __device__ __forceinline__ void fmac_rows(float &ar, float &ai, const float *xr,
             : "+v"(ar), "+v"(ai)
             : "v"(xr[0]), "v"(xr[1]), "v"(xr[2]), "v"(xr[3]), "v"(xr[4]), "v"(xi[0]), "v"(xi[1]), "v"(xi[2]), "v"(xi[3]), "v"(xi[4]), "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]), "v"(h[4]));
     }
-    else if constexpr (P == 4 && N == 3) {
+    else if constexpr (P == 4 && N == 5 && NOP) {
+        asm("s_nop 1\n\t"
+            "v_fmac_f32_dpp %0, %2, %12 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %7, %12 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %3, %13 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %8, %13 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %4, %14 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %9, %14 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %5, %15 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %10, %15 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %6, %16 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %11, %16 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            : "+v"(ar), "+v"(ai)
+            : "v"(xr[0]), "v"(xr[1]), "v"(xr[2]), "v"(xr[3]), "v"(xr[4]), "v"(xi[0]), "v"(xi[1]), "v"(xi[2]), "v"(xi[3]), "v"(xi[4]), "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]), "v"(h[4]));
+    }
+    else if constexpr (P == 4 && N == 3 && !NOP) {
         asm("v_fmac_f32_dpp %0, %2, %8 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %5, %8 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %3, %9 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %6, %9 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %0, %4, %10 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            "v_fmac_f32_dpp %1, %7, %10 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+            : "+v"(ar), "+v"(ai)
+            : "v"(xr[0]), "v"(xr[1]), "v"(xr[2]), "v"(xi[0]), "v"(xi[1]), "v"(xi[2]), "v"(h[0]), "v"(h[1]), "v"(h[2]));
+    }
+    else if constexpr (P == 4 && N == 3 && NOP) {
+        asm("s_nop 1\n\t"
+            "v_fmac_f32_dpp %0, %2, %8 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
             "v_fmac_f32_dpp %1, %5, %8 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
             "v_fmac_f32_dpp %0, %3, %9 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
             "v_fmac_f32_dpp %1, %6, %9 row_shl:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
@@ -915,19 +1057,21 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_r(const In *__restrict__ iq
                                                        float2 *__restrict__ y, TimingOut to) {
     constexpr bool SC16 = std::is_same<In, uint4>::value;
     constexpr int BPS = RCfg<In>::bps, PF = RCfg<In>::pf, NCH = r_chunks<In>(), NL = (NCH + 63) / 64;
+    constexpr int NB = RCfg<In>::nb, TK = r_tk<In>(), TIN = 10 * TK, LR = RCfg<In>::wlr;
+    constexpr int ROWK = NB == 1 ? 12 : 28;    // outputs per 16-lane row
     constexpr int IMGB = r_img16<In>() * 16;   // image bytes per wave
     using Pair = typename std::conditional<SC16, uint2, float4>::type;   // two samples
     __shared__ float4 smem[r_smem4<In>()];
     TrackOut *tro = reinterpret_cast<TrackOut *>(smem);                        // + prog: 2 float4
     uint8_t *img_all = reinterpret_cast<uint8_t *>(smem + 2);                  // 4 wave images
     float2 *lin_all = reinterpret_cast<float2 *>(img_all + 4 * IMGB);          // 4 stage-1 buffers
-    float2 *seam = lin_all + 4 * WLR;
+    float2 *seam = lin_all + 4 * LR;
     float *yb = reinterpret_cast<float *>(seam + 3 * SEAM);
     const int ch = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     uint8_t *img = img_all + wv * IMGB;
-    float2 *lin = lin_all + wv * WLR;
-    for (int i = lane; i < WLR; i += 64) lin[i] = make_float2(0.f, 0.f);
+    float2 *lin = lin_all + wv * LR;
+    for (int i = lane; i < LR; i += 64) lin[i] = make_float2(0.f, 0.f);
     float at[S2K];
 #pragma unroll
     for (int k = 0; k < S2K; ++k) at[k] = afrag[64 * k + lane];
@@ -949,23 +1093,24 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_r(const In *__restrict__ iq
     const bool has_right = wv + 1 < nw;
     const int u_beg = min(wv * UQ, UT), u_end = has_right ? (wv + 1) * UQ : UT;
     const int K0 = 10 * u_beg, K1 = has_right ? 10 * u_end : M1;
-    const int ntile = active ? (K1 - K0 + 4 + RT_K - 1) / RT_K : 0;   // wave tiles with kfirst < K1
-    // tile t: lane (row ro, i) holds the block of x240[K0 + 48 t - 4 + 12 ro + i], samples
-    // 10 (K0 + 48 t) - 40 + 10 (12 ro + i) + [0, 10) = image samples 10 (12 ro + i) + [0, 10); the
-    // tile's new samples 10 (K0 + 48 t) + [0, 480) land at image sample 40.  A buffer resource over the
-    // wave's samples [10 K0, last needed]: loads past it return 0 without touching memory.
+    const int ntile = active ? (K1 - K0 + 4 + TK - 1) / TK : 0;   // wave tiles with kfirst < K1
+    // tile t: lane (row ro, i) holds the NB blocks of x240[K0 + TK t - 4 + ROWK ro + NB i + e], e < NB,
+    // samples 10 (K0 + TK t) - 40 + 10 (ROWK ro + NB i + e) + [0, 10) = image samples
+    // 10 (ROWK ro + NB i + e) + [0, 10); the tile's new samples 10 (K0 + TK t) + [0, 10 TK) land at
+    // image sample 40.  A buffer resource over the wave's samples [10 K0, last needed]: loads past
+    // it return 0 without touching memory.
     const long s0 = 10L * K0;
     const long slast = active ? min(10L * (K1 - 1) + 47, N - 1) : s0;
     const uint8_t *xp = reinterpret_cast<const uint8_t *>(iq) + ((size_t)ch * N + s0) * BPS;
     const int nbytes = active ? (int)(((slast - s0 + 1) * BPS + 15) & ~15L) : 0;
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(xp), 0, nbytes, 0x00020000);
     const int ro = lane >> 4, li = lane & 15;
-    const int blk = 12 * ro + li;
+    const int blk = ROWK * ro + NB * li;   // this lane's first block
     auto load_tile = [&](In (&pf)[NL], int t) __attribute__((always_inline)) {
 #pragma unroll
         for (int r = 0; r < NL; ++r) {
             const int c = min(64 * r + lane, NCH - 1);   // unconditional (a branch makes hipcc wait at the join)
-            const nt_f4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * c, t * RT_IN * BPS, 2 /* nt */);
+            const nt_f4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, 16 * c, t * TIN * BPS, 2 /* nt */);
             pf[r] = *reinterpret_cast<const In *>(&v);
         }
     };
@@ -1008,10 +1153,10 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_r(const In *__restrict__ iq
         __builtin_amdgcn_sched_barrier(0);
         load_tile(pf, t + PF);
         wave_sync();
-        // this lane's block: 10 samples as five pairs
-        float xre[10], xim[10];
+        // this lane's blocks: 10 NB samples as 5 NB pairs
+        float xre[10 * NB], xim[10 * NB];
 #pragma unroll
-        for (int m = 0; m < 5; ++m) {
+        for (int m = 0; m < 5 * NB; ++m) {
             const Pair v = *reinterpret_cast<const Pair *>(img + (10 * blk + 2 * m) * BPS);
             if constexpr (SC16) {
                 xre[2 * m] = (float)(int16_t)(v.x & 0xFFFFu);
@@ -1025,39 +1170,77 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_r(const In *__restrict__ iq
                 xim[2 * m + 1] = v.w;
             }
         }
-        // x240[k] = sum_j h1[j] x[10 k + j], j ascending: sample j % 10 of the block j / 10 lanes on
-        float ar = 0.f, ai = 0.f;
-        fmac_rows<0, 10>(ar, ai, xre, xim, hv);
-        fmac_rows<1, 5>(ar, ai, xre, xim, hv + 10);
-        fmac_rows<1, 5>(ar, ai, xre + 5, xim + 5, hv + 15);
-        fmac_rows<2, 5>(ar, ai, xre, xim, hv + 20);
-        fmac_rows<2, 5>(ar, ai, xre + 5, xim + 5, hv + 25);
-        fmac_rows<3, 5>(ar, ai, xre, xim, hv + 30);
-        fmac_rows<3, 5>(ar, ai, xre + 5, xim + 5, hv + 35);
-        fmac_rows<4, 5>(ar, ai, xre, xim, hv + 40);
-        fmac_rows<4, 3>(ar, ai, xre + 5, xim + 5, hv + 45);
-        const int k = K0 + RT_K * t - 4 + blk;
-        if (li < 12 && k >= K0 && k < K1) {
-            lin[k - kbase] = make_float2(ar, ai);
-            if (wv > 0 && k - K0 < SEAM) seam[(wv - 1) * SEAM + k - K0] = make_float2(ar, ai);
+        // x240[k] = sum_j h1[j] x[10 k + j], j ascending: sample j % 10 of block k + j / 10
+        const int k = K0 + TK * t - 4 + blk;
+        if constexpr (NB == 1) {   // block k + p: lane + p
+            float ar = 0.f, ai = 0.f;
+            fmac_rows<0, 10>(ar, ai, xre, xim, hv);
+            fmac_rows<1, 5>(ar, ai, xre, xim, hv + 10);
+            fmac_rows<1, 5>(ar, ai, xre + 5, xim + 5, hv + 15);
+            fmac_rows<2, 5>(ar, ai, xre, xim, hv + 20);
+            fmac_rows<2, 5>(ar, ai, xre + 5, xim + 5, hv + 25);
+            fmac_rows<3, 5>(ar, ai, xre, xim, hv + 30);
+            fmac_rows<3, 5>(ar, ai, xre + 5, xim + 5, hv + 35);
+            fmac_rows<4, 5>(ar, ai, xre, xim, hv + 40);
+            fmac_rows<4, 3>(ar, ai, xre + 5, xim + 5, hv + 45);
+            if (li < 12 && k >= K0 && k < K1) {
+                lin[k - kbase] = make_float2(ar, ai);
+                if (wv > 0 && k - K0 < SEAM) seam[(wv - 1) * SEAM + k - K0] = make_float2(ar, ai);
+            }
+        } else {   // output A = block k: blocks k, k+1 in-lane, k+2, k+3 lane + 1, k+4 lane + 2;
+                   // output B = block k + 1: k+1 in-lane, k+2, k+3 lane + 1, k+4, k+5 lane + 2
+            const float *x0r = xre, *x0i = xim, *x1r = xre + 10, *x1i = xim + 10;
+            float ar = 0.f, ai = 0.f, br = 0.f, bi = 0.f;
+            fmac_rows<0, 10>(ar, ai, x0r, x0i, hv);
+            fmac_rows<0, 10>(ar, ai, x1r, x1i, hv + 10);
+            fmac_rows<0, 10>(br, bi, x1r, x1i, hv);
+            fmac_rows<1, 5, true>(br, bi, x0r, x0i, hv + 10);   // x0's first read in B's chain
+            fmac_rows<1, 5>(ar, ai, x0r, x0i, hv + 20);
+            fmac_rows<1, 5, true>(br, bi, x0r + 5, x0i + 5, hv + 15);   // and of x0[5..9]
+            fmac_rows<1, 5>(ar, ai, x0r + 5, x0i + 5, hv + 25);
+            fmac_rows<1, 5>(br, bi, x1r, x1i, hv + 20);
+            fmac_rows<1, 5>(ar, ai, x1r, x1i, hv + 30);
+            fmac_rows<1, 5>(br, bi, x1r + 5, x1i + 5, hv + 25);
+            fmac_rows<1, 5>(ar, ai, x1r + 5, x1i + 5, hv + 35);
+            fmac_rows<2, 5>(br, bi, x0r, x0i, hv + 30);
+            fmac_rows<2, 5>(ar, ai, x0r, x0i, hv + 40);
+            fmac_rows<2, 5>(br, bi, x0r + 5, x0i + 5, hv + 35);
+            fmac_rows<2, 3>(ar, ai, x0r + 5, x0i + 5, hv + 45);
+            fmac_rows<2, 5>(br, bi, x1r, x1i, hv + 40);
+            fmac_rows<2, 3>(br, bi, x1r + 5, x1i + 5, hv + 45);
+            if (li < 14) {
+                const bool va = k >= K0 && k < K1, vb = k + 1 >= K0 && k + 1 < K1;
+                if (va && vb) {   // the two outputs side by side: one 16-B store
+                    *reinterpret_cast<float4 *>(lin + (k - kbase)) = make_float4(ar, ai, br, bi);
+                } else {
+                    if (va) lin[k - kbase] = make_float2(ar, ai);
+                    if (vb) lin[k + 1 - kbase] = make_float2(br, bi);
+                }
+                if (wv > 0) {
+                    if (va && k - K0 < SEAM) seam[(wv - 1) * SEAM + k - K0] = make_float2(ar, ai);
+                    if (vb && k + 1 - K0 < SEAM) seam[(wv - 1) * SEAM + k + 1 - K0] = make_float2(br, bi);
+                }
+            }
         }
         wave_sync();
-        // halo for the next tile: image samples [0, 40) = this tile's [480, 520)
+        // halo for the next tile: image samples [0, 40) = this tile's [10 TK, 10 TK + 40)
         if (lane < RHALO * BPS / 16)
-            reinterpret_cast<uint4 *>(img)[lane] = reinterpret_cast<const uint4 *>(img)[RT_IN * BPS / 16 + lane];
-        const int kav = min(K0 + RT_K * t + RT_K - 5, K1 - 1);   // the tile's last output
+            reinterpret_cast<uint4 *>(img)[lane] = reinterpret_cast<const uint4 *>(img)[TIN * BPS / 16 + lane];
+        const int kav = min(K0 + TK * t + TK - 5, K1 - 1);   // the tile's last output
         const int u_rdy = kav >= 113 ? min((kav - 113) / 10 + 1, u_end) : 0;
         while (u_rdy - u_done >= S2T || (t == ntile - 1 && u_rdy > u_done)) {
             const int ul = min(u_done + S2T, u_rdy);
             burst(ul);
             u_done = ul;
+            // keep x240[10 u_done, kav] at the buffer's front: <= 10 (one tile's triples) + 123
             const int from = 10 * u_done - kbase, cnt = kav + 1 - 10 * u_done;
-            float2 v[3];
+            constexpr int NE = (TK + 123 + 63) / 64;
+            float2 v[NE];
 #pragma unroll
-            for (int e = 0; e < 3; ++e) v[e] = lane + 64 * e < cnt ? lin[from + lane + 64 * e] : make_float2(0.f, 0.f);
+            for (int e = 0; e < NE; ++e) v[e] = lane + 64 * e < cnt ? lin[from + lane + 64 * e] : make_float2(0.f, 0.f);
             wave_sync();
 #pragma unroll
-            for (int e = 0; e < 3; ++e)
+            for (int e = 0; e < NE; ++e)
                 if (lane + 64 * e < cnt) lin[lane + 64 * e] = v[e];
             kbase = 10 * u_done;
         }
