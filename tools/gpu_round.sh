@@ -1,6 +1,6 @@
 #!/bin/bash
-# GPU-box check: parity tests, smoke, default bench, wideband bench; PROFILE=tag adds the rocprof
-# passes of the default bench (tools/profile_bench.sh).  Every GPU step is time-limited and the steps
+# GPU-box check: parity tests, smoke, default bench, wideband and SC16 benches; PROFILE=tag adds the
+# rocprof passes of the default bench (tools/profile_bench.sh), PROFILE_SC16=tag those of the SC16 bench.  Every GPU step is time-limited and the steps
 # are chained (set -e), so a fault or timeout ends the call.
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -15,7 +15,10 @@ timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smo
 timeout -k 10 300 python -u bench.py > $O/bench_etsi.log 2>&1
 timeout -k 10 300 python -u bench.py --no-cpu --cells given > $O/bench_etsi_given.log 2>&1
 timeout -k 10 300 python -u bench.py --chain wideband --no-cpu > $O/bench_wb.log 2>&1
+timeout -k 10 300 python -u bench.py --iq sc16 --no-cpu > $O/bench_sc16.log 2>&1
 if [ -n "$PROFILE" ]; then bash tools/profile_bench.sh $PROFILE; fi
+# PROFILE_SC16=tag: the same passes on the SC16 (BladeRF wire format) bench
+if [ -n "$PROFILE_SC16" ]; then bash tools/profile_bench.sh $PROFILE_SC16 --iq sc16; fi
 # AB="libA.so libB.so": same-box A/B of library variants, pipelined and serial cf32, pipelined SC16
 if [ -n "$AB" ]; then
   AB_ARGS=" " bash tools/ab_demod.sh $AB > $O/ab_pipe.txt 2>&1
