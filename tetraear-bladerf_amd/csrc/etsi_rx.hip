@@ -839,12 +839,12 @@ static_assert(RCfg<uint4>::wlr >= 513 + 112 && WLR >= 513 + 48, "stage-1 buffer"
 // of x (and so its conversion) >= 9 steps earlier, NOP = true opens the block with s_nop 1.
 template <int P, int N, bool NOP = false>
 __device__ __forceinline__ void fmac_rows(float &ar, float &ai, const float *xr, const float *xi, const float *h) {
-    if constexpr (P == 0) {
+    if constexpr (P == 0) {   // in-lane: one v_pk_fma_f32 per product (both halves' fma, the same bits)
+        pf2 a = {ar, ai};
 #pragma unroll
-        for (int q = 0; q < N; ++q) {
-            ar = fmaf(h[q], xr[q], ar);
-            ai = fmaf(h[q], xi[q], ai);
-        }
+        for (int q = 0; q < N; ++q) a = pfma(h[q], pf2{xr[q], xi[q]}, a);
+        ar = a.x;
+        ai = a.y;
     }
     else if constexpr (P == 1 && N == 5 && !NOP) {
         asm("v_fmac_f32_dpp %0, %2, %12 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
