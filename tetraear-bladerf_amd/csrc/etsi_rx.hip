@@ -217,19 +217,36 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
     float2 prev = make_float2(0.f, 0.f);
     bool have_prev = false;
     float zr = 0.f, zi = 0.f, am = 0.f;   // CFO sums over this lane's d_j
+    int rel = -1;   // SPLIT: progress not yet released (published after the next block's LDS reads)
     for (int kb = kstart;; kb += 64) {
         const float off = base + delta;
         const float t = (float)(4 * (kb + lane)) + off;
         const bool valid = (t - 3.0f >= 0.0f) && (t + 2.0f <= (float)(M2 - 1)) && (S + lane < smax);
         const unsigned long long bal = __ballot(!valid);
         const int nv = bal ? (__ffsll((long long)bal) - 1) : 64;
+        const bool act = lane < nv;
         float2 on = make_float2(0.f, 0.f), mid = make_float2(0.f, 0.f);
-        if (lane < nv) interp_pair(y, 0, t, on, mid);
+        if constexpr (SPLIT) {
+            // y in LDS: every lane interpolates, so the window reads do not wait for the ballot
+            // (a lane past nv reads in or past the workgroup's LDS -- past it reads return 0 -- and
+            // its values are dropped below)
+            float2 a, b;
+            interp_pair(y, 0, t, a, b);
+            asm volatile("" ::"v"(a.x), "v"(a.y), "v"(b.x), "v"(b.y));   // computed here, not sunk into the branch
+            if (act) {
+                on = a;
+                mid = b;
+            }
+            if (rel >= 0 && lane == 0)   // the previous block's d_j: its stores completed before these reads
+                __hip_atomic_store(prog, rel, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+            if (act) interp_pair(y, 0, t, on, mid);
+        }
         float2 pv = make_float2(dppf<0x138>(on.x), dppf<0x138>(on.y));   // wave_shr:1 (lane 0 replaced below)
         bool hp_ = true;
         if (lane == 0) { pv = prev; hp_ = have_prev; }
         float ev = 0.f, pw = 0.f;
-        if (lane < nv) {
+        if (act) {
             pw = fmaf(on.x, on.x, on.y * on.y);
             if (hp_) {
                 const float dr = on.x - pv.x, di = on.y - pv.y;
@@ -258,11 +275,11 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
             have_prev = true;
         }
         S += nv;
-        if constexpr (SPLIT) {   // d_j, j < S, are in dp: release them to the CFO wave
-            if (lane == 0)
-                __hip_atomic_store(prog, S | (nv < 64 ? PROG_DONE : 0), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+        if constexpr (SPLIT) rel = S;   // d_j, j < S, are in dp: released to the CFO wave next block
         if (nv < 64) break;
+    }
+    if constexpr (SPLIT) {   // the last block's d_j, and the end
+        if (lane == 0) __hip_atomic_store(prog, S | PROG_DONE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     o.S = S;
     o.base = base;
