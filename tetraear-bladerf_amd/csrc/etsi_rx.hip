@@ -1532,19 +1532,23 @@ __device__ __forceinline__ int32_t quad_perm(int32_t v) {
 // starts at or before the buffer's last byte (`last`, a dword that holds it): a clamped load reads
 // bytes the segment does not use.  Descrambling negates the int8 values whose scrambler byte is 1
 // (four at a time: x ^ 0xFF + 1 per flagged byte, carry-free SWAR), as -v in int8 does.
+// The loads go through buffer resources over the whole soft-bit buffer (sbr: from the dword that
+// holds its first byte to the dword that holds its last) and the scrambler table (scr_r): one 32-bit
+// offset per lane with the load index in the immediate field, where 64-bit clamped addresses held two
+// VGPRs per load in flight; a load past the buffer returns 0 instead of the clamped dword (bytes the
+// segment does not use either way).  seg_off: the segment's byte offset from sbr's base (whose
+// alignment is the buffer's: sbr starts at a dword boundary), scr_off: the table segment's.
 template <int ND>
-__device__ __forceinline__ void load_seg(const int8_t *seg, const int8_t *last, const uint32_t *__restrict__ scr32,
-                                         uint32_t *d32, int q) {
+__device__ __forceinline__ void load_seg(__amdgpu_buffer_rsrc_t sbr, uint32_t seg_off, __amdgpu_buffer_rsrc_t scr_r,
+                                         uint32_t scr_off, uint32_t *d32, int q) {
     constexpr int NI = (ND + 1 + 3) / 4;   // loads per lane: dwords 0 .. ND of the aligned window
-    const uintptr_t pa = (uintptr_t)seg, lim = (uintptr_t)last & ~(uintptr_t)3;
-    const int sh = (int)(pa & 3);
-    const uintptr_t a0 = pa - sh;
+    const int sh = (int)(seg_off & 3);
+    const uint32_t a0 = seg_off - sh + 4 * q, s0 = scr_off + 4 * q;
     uint32_t R[NI], S[NI];
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-        const int j = 4 * i + q;
-        R[i] = *(const uint32_t *)std::min(a0 + 4 * (uintptr_t)j, lim);
-        S[i] = scr32[std::min(j, ND - 1)];
+        R[i] = __builtin_amdgcn_raw_buffer_load_b32(sbr, a0 + 16 * i, 0, 0);
+        S[i] = __builtin_amdgcn_raw_buffer_load_b32(scr_r, s0 + 16 * i, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
@@ -1617,11 +1621,15 @@ __device__ __forceinline__ void acs_groups4(int32_t (&pm)[4], int q, const int8_
     }
 }
 
+// soft-bit and scrambler-table resources of one k_etsi_viterbi launch (wave-uniform)
+struct VitSrc {
+    __amdgpu_buffer_rsrc_t sbr, cell_r, bsch_r;
+    uint32_t sb_lead;   // bytes from sbr's base (a dword boundary) to softbits[0]
+};
+
 template <int KIND>
 __device__ __forceinline__ void viterbi_wave(int8_t *rows, const Job *__restrict__ jobs, int nj, size_t jbase, int lb,
-                                             size_t ss, const int8_t *__restrict__ softbits, int smax,
-                                             const int8_t *sb_last, const uint8_t *__restrict__ cell_scr,
-                                             const uint8_t *__restrict__ bsch_scr, uint32_t *__restrict__ surv) {
+                                             size_t ss, const VitSrc &src, int smax, uint32_t *__restrict__ surv) {
     constexpr KindP P = kind_params(KIND);
     const int lane = threadIdx.x, jw = lane >> 2, q = lane & 3;
     const int jl = lb * 16 + jw;
@@ -1631,14 +1639,15 @@ __device__ __forceinline__ void viterbi_wave(int8_t *rows, const Job *__restrict
     const Job jb = act ? jobs[j] : Job{0, 0, 0, 0, KIND, 0};
     int8_t *row = rows + jw * VROW;
     if (act) {   // the quad loads the block's type-5 soft bits and scrambler bytes as dwords
-        const int8_t *sb = softbits + (size_t)jb.ch * 2 * smax + jb.off;
-        const uint8_t *scr = KIND == 2 ? bsch_scr : cell_scr + (size_t)jb.ch * 432;
+        const uint32_t so = src.sb_lead + (uint32_t)jb.ch * 2 * smax + jb.off;
+        const __amdgpu_buffer_rsrc_t scr_r = KIND == 2 ? src.bsch_r : src.cell_r;
+        const uint32_t co = KIND == 2 ? 0u : (uint32_t)jb.ch * 432;
         uint32_t *d32 = (uint32_t *)row;
         if constexpr (KIND == 0) {   // SCH/F: BKN1 = type-5 [0, 216), BKN2 = [216, 432) 268 bits on
-            load_seg<54>(sb, sb_last, (const uint32_t *)scr, d32, q);
-            load_seg<54>(sb + 268, sb_last, (const uint32_t *)scr + 54, d32 + 54, q);
+            load_seg<54>(src.sbr, so, scr_r, co, d32, q);
+            load_seg<54>(src.sbr, so + 268, scr_r, co + 4 * 54, d32 + 54, q);
         } else {
-            load_seg<P.K / 4>(sb, sb_last, (const uint32_t *)scr, d32, q);
+            load_seg<P.K / 4>(src.sbr, so, scr_r, co, d32, q);
         }
     }
     __syncthreads();   // the quad's row (one wave per workgroup)
@@ -1719,7 +1728,15 @@ __global__ __launch_bounds__(64) void k_etsi_viterbi(const Job *__restrict__ job
                                                      uint32_t *__restrict__ surv, int kmask) {
     __shared__ __attribute__((aligned(16))) int8_t rows[16 * VROW];
     const size_t ss = 32 * (size_t)C;
-    const int8_t *sb_last = softbits + (size_t)C * 2 * smax - 1;   // the soft-bit buffer's last byte
+    // the soft-bit buffer [softbits, softbits + 2 C smax) from the dword holding its first byte to the
+    // dword holding its last (host checks: < 4 GiB); the cell table and the BSCH table
+    const uintptr_t sb0 = (uintptr_t)softbits & ~(uintptr_t)3;
+    const uintptr_t sbl = ((uintptr_t)softbits + (size_t)C * 2 * smax - 1) & ~(uintptr_t)3;
+    VitSrc src;
+    src.sbr = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(sb0), 0, (int)(sbl - sb0 + 4), 0x00020000);
+    src.cell_r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(cell_scr), 0, C * 432, 0x00020000);
+    src.bsch_r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(bsch_scr), 0, 432, 0x00020000);
+    src.sb_lead = (uint32_t)((uintptr_t)softbits - sb0);
     const unsigned long long cnt = *jcount;
     // kinds outside kmask are left to another launch (cell acquisition decodes BSCH first)
     const int n0 = kmask & 1 ? (int)(cnt & 0x1FFFFFull) : 0, n1 = kmask & 2 ? (int)((cnt >> 21) & 0x1FFFFFull) : 0,
@@ -1729,13 +1746,11 @@ __global__ __launch_bounds__(64) void k_etsi_viterbi(const Job *__restrict__ job
     const int nb0 = (n0 + 15) / 16, nb1 = (n1 + 15) / 16, nb2 = (n2 + 15) / 16;
     for (int b = blockIdx.x; b < nb0 + nb1 + nb2; b += gridDim.x) {
         if (b < nb0)
-            viterbi_wave<0>(rows, jobs, n0, job_base(0, C), b, ss, softbits, smax, sb_last, cell_scr, bsch_scr, surv);
+            viterbi_wave<0>(rows, jobs, n0, job_base(0, C), b, ss, src, smax, surv);
         else if (b < nb0 + nb1)
-            viterbi_wave<1>(rows, jobs, n1, job_base(1, C), b - nb0, ss, softbits, smax, sb_last, cell_scr, bsch_scr,
-                            surv);
+            viterbi_wave<1>(rows, jobs, n1, job_base(1, C), b - nb0, ss, src, smax, surv);
         else
-            viterbi_wave<2>(rows, jobs, n2, job_base(2, C), b - nb0 - nb1, ss, softbits, smax, sb_last, cell_scr,
-                            bsch_scr, surv);
+            viterbi_wave<2>(rows, jobs, n2, job_base(2, C), b - nb0 - nb1, ss, src, smax, surv);
         __syncthreads();   // rows are rewritten by the next wave-batch
     }
 }
@@ -2231,6 +2246,9 @@ static int lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard
     if (!cell_init && ctx->cells < C)
         return tetra_fail(ctx, TETRA_E_INVALID, "tetra_etsi_set_cells() for %zu channels first", C);
     if (2 * smax > LMAC_MAXBITS + 4) return tetra_fail(ctx, TETRA_E_INVALID, "chunk too long for tetra_lmac_etsi");
+    // k_etsi_viterbi reads the soft bits and the cell table through 32-bit buffer offsets
+    if (C * smax * 2 + 8 > (size_t)INT32_MAX || (C + 1) * 432 > (size_t)INT32_MAX)
+        return tetra_fail(ctx, TETRA_E_INVALID, "too many channels for one tetra_lmac_etsi call (%zu)", C);
     Staging st(ctx);
     uint32_t *ci = cell_init ? (uint32_t *)st.inout(cell_init, C * 4) : nullptr;
     const int8_t *sb = (const int8_t *)st.in(softbits, C * smax * 2);
