@@ -57,7 +57,7 @@ def parse():
                     help="etsi: overlap the demod of batch k+1 with the lower MAC of batch k on two streams "
                          "(auto: on for cf32 and sc16 -- sc16 since the lower MAC's traceback kernel: 1.210 -> "
                          "1.197 ms per step); compat: run consecutive batches' "
-                         "whole chains on two streams (auto: on); wideband: channeliser of capture k+1 beside "
+                         "whole chains on --compat-lanes streams (auto: on); wideband: channeliser of capture k+1 beside "
                          "the timing + lower MAC of capture k (auto: on)")
     ap.add_argument("--no-pipeline", action="store_true", help="same as --pipeline off")
     ap.add_argument("--compat-lanes", type=int, default=2,
@@ -125,9 +125,9 @@ class CompatStep:
     """process() + decode() lower MAC over the batch (tetra_demod_compat + tetra_lmac_compat).
 
     The chain's IIR passes are sequential per stream by construction (bit-exact scipy order): a
-    batch of 8192 channels is one wave per SIMD, issue-latency bound.  pipeline() runs consecutive
-    batches on two contexts / HIP streams, so batch k+1's kernels interleave with batch k's (two
-    waves per SIMD); every step still does the whole chain for one batch."""
+    batch of 8192 channels is one wave per SIMD, issue-latency bound.  pipeline(lanes) runs
+    consecutive batches on `lanes` contexts / HIP streams, so batch k+1's kernels interleave with
+    batch k's; every step still does the whole chain for one batch."""
 
     class _Lane:
         def __init__(self, c, C, smax, dev):

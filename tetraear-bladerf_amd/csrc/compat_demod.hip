@@ -83,6 +83,7 @@ __device__ __forceinline__ Biquad<T> load_section(const T *sos, const T *zi, int
 }
 
 constexpr int SKB = 32;   // ticks per prefetch batch (a multiple of every vector width below)
+constexpr int SOS_PD = 2;   // banked decimator passes: input batches in flight
 
 // 16-byte vectors: the decimator's memory traffic goes through as few VMEM instructions as
 // possible -- with one wave per SIMD the per-wave limit on outstanding VMEM operations, not
@@ -386,7 +387,6 @@ __global__ __launch_bounds__(256) void k_sos_fwd_bank(const float *__restrict__ 
     long tau = 0;
     for (; tau < pad; ++tau) tick(tau, ext(tau));
     constexpr int NW = SKB / 8;   // 8-sample windows per batch
-    f4u xa[NW], xb[NW];
     const float *xw = xr + 4 * sec + comp;
     auto ld = [&](f4u (&v)[NW], long t0) __attribute__((always_inline)) {
         const float *src = xw + 2 * (t0 - pad);
@@ -432,21 +432,22 @@ __global__ __launch_bounds__(256) void k_sos_fwd_bank(const float *__restrict__ 
         for (int k = 0; k < NW; ++k) asm volatile("" ::"v"(v[k]));
     };
     // the imaginary lanes of the last chunk read one float past their window: the batches stop
-    // one sample short of the row end, so that float is inside the row
-    if (N >= 2 * SKB + 1) {
-        ld(xa, tau);
-        ld(xb, tau + SKB);
-        for (; tau + 4 * SKB < pad + N; tau += 2 * SKB) {
-            run(xa, tau);
-            __builtin_amdgcn_sched_barrier(0);
-            ld(xa, tau + 2 * SKB);
-            run(xb, tau + SKB);
-            __builtin_amdgcn_sched_barrier(0);
-            ld(xb, tau + 3 * SKB);
+    // one sample short of the row end, so that float is inside the row.  SOS_PD batches in flight.
+    if (N >= SOS_PD * SKB + 1) {
+        f4u xs[SOS_PD][NW];
+#pragma unroll
+        for (int u = 0; u < SOS_PD; ++u) ld(xs[u], tau + u * SKB);
+        for (; tau + 2 * SOS_PD * SKB < pad + N; tau += SOS_PD * SKB) {
+#pragma unroll
+            for (int u = 0; u < SOS_PD; ++u) {
+                run(xs[u], tau + u * SKB);
+                __builtin_amdgcn_sched_barrier(0);
+                ld(xs[u], tau + (u + SOS_PD) * SKB);
+            }
         }
-        run(xa, tau);
-        run(xb, tau + SKB);
-        tau += 2 * SKB;
+#pragma unroll
+        for (int u = 0; u < SOS_PD; ++u) run(xs[u], tau + u * SKB);
+        tau += SOS_PD * SKB;
     }
     for (; tau < L + 3; ++tau) tick(tau, tau < L ? ext(tau) : 0.f);
 }
@@ -492,7 +493,6 @@ __global__ __launch_bounds__(256) void k_sos_bwd_bank(const float *__restrict__ 
     long tau = 0;
     if (phased) {
         for (; tau < tau0; ++tau) tick(tau, sp[L - 1 - tau]);
-        float4 xa[NL], xb[NL];
         const float *sw = sp + L - 4 - 4 * sec;
         auto ld = [&](float4 (&v)[NL], long t0) __attribute__((always_inline)) {
 #pragma unroll
@@ -517,20 +517,21 @@ __global__ __launch_bounds__(256) void k_sos_bwd_bank(const float *__restrict__ 
                 if (u % QT == PH && st) op[(size_t)(tq0 - u / QT) * so] = y;
             }
         };
-        if (tcur(tau + 2 * SB - 1) >= 0 && L - tau >= 2 * SB) {
-            ld(xa, tau);
-            ld(xb, tau + SB);
-            for (; tcur(tau + 4 * SB - 1) >= 0 && tau + 4 * SB <= L; tau += 2 * SB) {
-                run(xa, tau);
-                __builtin_amdgcn_sched_barrier(0);
-                ld(xa, tau + 2 * SB);
-                run(xb, tau + SB);
-                __builtin_amdgcn_sched_barrier(0);
-                ld(xb, tau + 3 * SB);
+        if (tcur(tau + SOS_PD * SB - 1) >= 0 && L - tau >= SOS_PD * SB) {
+            float4 xs[SOS_PD][NL];
+#pragma unroll
+            for (int u = 0; u < SOS_PD; ++u) ld(xs[u], tau + u * SB);
+            for (; tcur(tau + 2 * SOS_PD * SB - 1) >= 0 && tau + 2 * SOS_PD * SB <= L; tau += SOS_PD * SB) {
+#pragma unroll
+                for (int u = 0; u < SOS_PD; ++u) {
+                    run(xs[u], tau + u * SB);
+                    __builtin_amdgcn_sched_barrier(0);
+                    ld(xs[u], tau + (u + SOS_PD) * SB);
+                }
             }
-            run(xa, tau);
-            run(xb, tau + SB);
-            tau += 2 * SB;
+#pragma unroll
+            for (int u = 0; u < SOS_PD; ++u) run(xs[u], tau + u * SB);
+            tau += SOS_PD * SB;
         }
     }
     for (; tau < L + 3; ++tau) tick(tau, tau < L ? sp[L - 1 - tau] : 0.f);

@@ -161,6 +161,82 @@ __device__ void parse_burst(F symv, int *btype, bool *ok) {
     }
 }
 
+// The CRC register as a linear function of the message bits (GF(2)): crc_bit(c, b) = S(c) ^ b S(0x8000)
+// with S the shift-and-reduce step, so after n bits m_0..m_{n-1} from 0xFFFF the register is
+// init[n] ^ XOR over the 1-bits m_i of t[n - 1 - i], t[d] = S^(d+1)(0x8000), init[n] = S^n(0xFFFF).
+// That lets a wave check a burst's CRC in parallel (k_lmac: 64 lanes, eight bits each) instead of
+// one lane stepping 494 bits twice -- the same registers, so the same decisions.
+constexpr int LCRC_N = 494;   // the longest message _check_crc sees: 510 - 16 bits
+struct LinCrc {
+    uint32_t t[LCRC_N];
+    uint32_t init[LCRC_N + 1];
+};
+constexpr uint32_t crc_shift(uint32_t c) { return ((c & 0x8000u) ? ((c << 1) ^ 0x1021u) : (c << 1)) & 0xFFFFu; }
+constexpr LinCrc make_lin_crc() {
+    LinCrc l{};
+    uint32_t r = crc_shift(0x8000u);
+    for (int d = 0; d < LCRC_N; ++d) { l.t[d] = r; r = crc_shift(r); }
+    uint32_t s = 0xFFFFu;
+    for (int n = 0; n <= LCRC_N; ++n) { l.init[n] = s; s = crc_shift(s); }
+    return l;
+}
+__constant__ LinCrc LCRC = make_lin_crc();
+
+__device__ __forceinline__ uint32_t wave_xor_u32(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v ^= (uint32_t)__shfl_xor((int)v, o, 64);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o, 64);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_add_u32(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+    return v;
+}
+
+// check_crc (protocol.py:292-329) by a whole wave, L <= LCRC_N + 16 (every lane calls it): lane l
+// takes bits l, l + 64, ...; the forward register sums t[n-1-i], the reversed one (bit L-17-i fed
+// at step i) t[i], both from init[n], n = L - 16; rx gathers the last 16 bits MSB first.
+template <typename F>
+__device__ bool check_crc_wave(F get, int L, int lane) {
+    if (L < 16) return false;
+    const int n = L - 16;
+    uint32_t ones = 0, c = 0, r = 0, rx = 0;
+    for (int i = lane; i < L; i += 64) {
+        const uint32_t b = get(i);
+        ones += b;
+        if (i < n) {
+            const uint32_t m = 0u - b;
+            c ^= LCRC.t[n - 1 - i] & m;
+            r ^= LCRC.t[i] & m;
+        } else {
+            rx |= b << (L - 1 - i);
+        }
+    }
+    ones = wave_add_u32(ones);
+    c = wave_xor_u32(c) ^ LCRC.init[n];
+    r = wave_xor_u32(r) ^ LCRC.init[n];
+    rx = wave_or_u32(rx);
+    if (ones == 0 || ones == (uint32_t)L) return false;
+    return __popc(c ^ rx) <= 2 || __popc(r ^ rx) <= 2;
+}
+
+// parse_burst by a whole wave (the result is wave-uniform): the sync word's 22 bits by a ballot
+template <typename F>
+__device__ void parse_burst_wave(F symv, int lane, int *btype, bool *ok) {
+    auto bit = [&](long i) -> uint32_t { const uint32_t v = symv(i >> 1); return (i & 1) ? (v & 1u) : (v >> 1); };
+    const uint32_t w = (uint32_t)__ballot(lane < 22 && bit(255 + lane)) & MASK22;   // bits[255 : 277]
+    const int m = max(match(w, W_SCD), match(w, W_SDD));
+    const bool sync = m * 5 > 88;
+    *btype = sync ? 5 : 2;
+    if (sync) {
+        *ok = check_crc_wave(bit, 510, lane);
+    } else {
+        *ok = check_crc_wave([&](long i) -> uint32_t { return bit(i < 108 ? i : i + 14); }, 216, lane);
+    }
+}
+
 __global__ __launch_bounds__(64) void k_lmac(const int64_t *__restrict__ sym, const int32_t *__restrict__ nsym,
                                              int C, long stride, const int8_t *__restrict__ kmax,
                                              int32_t *__restrict__ nsync, int32_t *__restrict__ rec,
@@ -200,6 +276,13 @@ __global__ __launch_bounds__(64) void k_lmac(const int64_t *__restrict__ sym, co
                 bb[(size_t)f * 510 + t] = (uint8_t)((t & 1) ? (v & 1u) : (v >> 1));
             }
         }
+        int bt = 0;
+        bool ok = false;
+        int hdr = 0;
+        if (valid && nbits >= 510) {   // wave-uniform
+            parse_burst_wave([&](long t) { return st.val(s0 + t); }, lane, &bt, &ok);
+            hdr = (int)((st.bit(start) << 3) | (st.bit(start + 1) << 2) | (st.bit(start + 2) << 1) | st.bit(start + 3));
+        }
         if (lane == 0) {
             int32_t *r = rp + f * TETRA_F_FIELDS;
             r[TETRA_F_POS] = (int32_t)p;
@@ -207,13 +290,6 @@ __global__ __launch_bounds__(64) void k_lmac(const int64_t *__restrict__ sym, co
             r[TETRA_F_VALID] = valid;
             r[TETRA_F_NBITS] = (int32_t)nbits;
             r[TETRA_F_NUMBER] = valid ? (int32_t)(start / 510) : -1;
-            int bt = 0;
-            bool ok = false;
-            int hdr = 0;
-            if (valid && nbits >= 510) {
-                parse_burst([&](long t) { return st.val(s0 + t); }, &bt, &ok);
-                hdr = (int)((st.bit(start) << 3) | (st.bit(start + 1) << 2) | (st.bit(start + 2) << 1) | st.bit(start + 3));
-            }
             r[TETRA_F_BTYPE] = bt;
             r[TETRA_F_CRC] = ok;
             r[TETRA_F_HDR] = hdr;
