@@ -89,7 +89,8 @@ __device__ bool stream_is_dqpsk(const int64_t *s, long S, int lane) {
 
 // Greedy scan with count threshold k.  Returns number of hits (positions in pos[0..min(n,maxp))).
 // *maxc (optional): max of the correlations find_sync evaluates (TS2 skipped at a TS1 hit).
-__device__ int greedy(const Stream &st, long nw, int k, int lane, int64_t *pos, int maxp, int *maxc) {
+template <typename SS>
+__device__ int greedy(const SS &st, long nw, int k, int lane, int64_t *pos, int maxp, int *maxc) {
     int n = 0, mc = 0;
     long cur = 0;
     while (cur < nw) {
@@ -237,15 +238,49 @@ __device__ void parse_burst_wave(F symv, int lane, int *btype, bool *ok) {
     }
 }
 
-__global__ __launch_bounds__(64) void k_lmac(const int64_t *__restrict__ sym, const int32_t *__restrict__ nsym,
-                                             int C, long stride, const int8_t *__restrict__ kmax,
-                                             int32_t *__restrict__ nsync, int32_t *__restrict__ rec,
-                                             uint8_t *__restrict__ fbits, uint8_t *__restrict__ bbits) {
-    const int ch = blockIdx.x, lane = threadIdx.x;
-    if (ch >= C) return;
-    __shared__ int64_t pos[TETRA_MAX_SYNC];
-    Stream st{sym + (size_t)ch * stride, (long)nsym[ch], false};
-    st.dq = stream_is_dqpsk(st.s, st.S, lane);
+// The stream's bits (symbols_to_bits of the mapped symbols) packed LSB-first into LDS words, bit i
+// at word i >> 5: a 22-bit window is one funnel shift of two words, where Stream::window assembled it
+// from 12 global symbol loads.  Words past the stream are zero, as Stream::val is past S.
+struct PackedStream {
+    const uint32_t *w;
+    long S;
+    __device__ uint32_t bit(long i) const { return (w[i >> 5] >> (i & 31)) & 1u; }
+    __device__ uint32_t val(long k) const { return (bit(2 * k) << 1) | bit(2 * k + 1); }
+    __device__ uint32_t window(long i) const {
+        const long q = i >> 5;
+        return __builtin_amdgcn_alignbit(w[q + 1], w[q], (uint32_t)(i & 31)) & MASK22;
+    }
+};
+// LDS words k_lmac packs a stream of up to `stride` symbols into (two past the last bit: window reads)
+__host__ __device__ inline long lmac_words(long stride) { return (2 * stride + 31) / 32 + 2; }
+constexpr long LMAC_LDS_MAX = 48 * 1024;   // larger rows take the global-memory Stream
+
+// symbols_to_bits into LDS: 32 symbols per ballot (lane j: component j & 1 of symbol j >> 1, so the
+// ballot is the 64 bits in stream order), eight ballots' loads issued ahead
+__device__ void pack_stream(const Stream &st, uint32_t *w, long nwords, int lane) {
+    for (long i = lane; i < nwords; i += 64) w[i] = 0;
+    __syncthreads();
+    constexpr int PK = 8;
+    const int sl = lane >> 1, comp = lane & 1;
+    for (long s00 = 0; s00 < st.S; s00 += 32 * PK) {
+        uint32_t v[PK];
+#pragma unroll
+        for (int u = 0; u < PK; ++u) v[u] = st.val(s00 + 32 * u + sl);   // 0 past S
+#pragma unroll
+        for (int u = 0; u < PK; ++u) {
+            const long s0 = s00 + 32 * u;
+            if (s0 >= st.S) break;   // uniform
+            const unsigned long long b = __ballot(comp ? (v[u] & 1u) : (v[u] >> 1));
+            if (lane < 2) w[s0 / 16 + lane] = (uint32_t)(b >> (32 * lane));
+        }
+    }
+    __syncthreads();
+}
+
+template <typename SS>
+__device__ void lmac_body(const SS &st, int ch, int lane, long stride, const int8_t *__restrict__ kmax,
+                          int32_t *__restrict__ nsync, int32_t *__restrict__ rec, uint8_t *__restrict__ fbits,
+                          uint8_t *__restrict__ bbits, int64_t *pos) {
     const long nb = 2 * st.S, nw = nb - 21;
     int n = 0;
     if (nw > 0) {
@@ -294,6 +329,25 @@ __global__ __launch_bounds__(64) void k_lmac(const int64_t *__restrict__ sym, co
             r[TETRA_F_CRC] = ok;
             r[TETRA_F_HDR] = hdr;
         }
+    }
+}
+
+__global__ __launch_bounds__(64) void k_lmac(const int64_t *__restrict__ sym, const int32_t *__restrict__ nsym,
+                                             int C, long stride, const int8_t *__restrict__ kmax,
+                                             int32_t *__restrict__ nsync, int32_t *__restrict__ rec,
+                                             uint8_t *__restrict__ fbits, uint8_t *__restrict__ bbits) {
+    const int ch = blockIdx.x, lane = threadIdx.x;
+    if (ch >= C) return;   // whole workgroup (one wave)
+    __shared__ int64_t pos[TETRA_MAX_SYNC];
+    extern __shared__ uint32_t words[];   // lmac_words(stride) when the launch gives them
+    Stream st{sym + (size_t)ch * stride, (long)nsym[ch], false};
+    st.dq = stream_is_dqpsk(st.s, st.S, lane);
+    const long nwords = lmac_words(stride);
+    if (nwords * 4 <= LMAC_LDS_MAX && st.S <= stride) {   // (a count past the row: the global form, as before)
+        pack_stream(st, words, nwords, lane);
+        lmac_body(PackedStream{words, st.S}, ch, lane, stride, kmax, nsync, rec, fbits, bbits, pos);
+    } else {
+        lmac_body(st, ch, lane, stride, kmax, nsync, rec, fbits, bbits, pos);
     }
 }
 
@@ -527,7 +581,9 @@ int tetra_lmac_compat(tetra_ctx *ctx, const int64_t *sym, const int32_t *nsym, s
     uint8_t *bb = (uint8_t *)st.out(burst_bits, C * TETRA_MAX_SYNC * 510);
     if (!s || !n || !k || !ns || !r || !fb || !bb) return st.finish();
     PROF(ctx, "compat_lmac");
-    hipLaunchKernelGGL(k_lmac, dim3((unsigned)C), dim3(64), 0, ctx->stream, s, n, (int)C, (long)stride, k, ns, r, fb, bb);
+    const long lw = lmac_words((long)stride) * 4;
+    hipLaunchKernelGGL(k_lmac, dim3((unsigned)C), dim3(64), lw <= LMAC_LDS_MAX ? (unsigned)lw : 0u, ctx->stream, s, n,
+                       (int)C, (long)stride, k, ns, r, fb, bb);
     return st.finish();
 }
 
