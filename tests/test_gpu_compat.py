@@ -267,3 +267,35 @@ def _hip_ctx_on_torch_stream():
     s = torch.cuda.current_stream(torch.device("cuda", 0))
     c.check(c.lib.tetra_set_stream(c.handle, ctypes.c_void_p(s.cuda_stream)), "set_stream")
     return c
+
+
+def test_lmac_packed_equals_global_rows(hip, g2):
+    """tetra_lmac_compat packs each stream's bits into LDS when the row fits (k_lmac: PackedStream)
+    and reads symbols from global memory otherwise (Stream).  The same g2 streams through both --
+    a tight row stride, then one past the LDS cap (LMAC_LDS_MAX, 48 KB of packed bits) -- give the
+    same syncs, records and burst bits."""
+    from tetraear import _hip
+    from tetraear.core.decoder import cascade_table
+    z, recs = g2
+    streams = [np.asarray(z[f"s{i}_sym"], np.int64) for i in range(len(recs))]
+    C = len(streams)
+    c = _hip.ctx()
+    out = []
+    for stride in (max(len(s) for s in streams), 200_000):
+        sym = np.zeros((C, stride), np.int64)
+        for i, s in enumerate(streams):
+            sym[i, :len(s)] = s
+        ns = np.array([len(s) for s in streams], np.int32)
+        nsync = np.zeros(C, np.int32)
+        rec = np.zeros((C, _hip.MAX_SYNC, _hip.F_FIELDS), np.int32)
+        fb = np.zeros((C, _hip.MAX_SYNC, 510), np.uint8)
+        bb = np.zeros((C, _hip.MAX_SYNC, 510), np.uint8)
+        c.check(c.lib.tetra_lmac_compat(c.handle, _hip.ptr(sym), _hip.ptr(ns), C, stride, _hip.ptr(cascade_table()),
+                                        _hip.ptr(nsync), _hip.ptr(rec), _hip.ptr(fb), _hip.ptr(bb)), "tetra_lmac_compat")
+        out.append((nsync, rec, fb, bb))
+    (n1, r1, f1, b1), (n2, r2, f2, b2) = out
+    assert np.array_equal(n1, n2) and n1.sum() > 0
+    for i in range(C):
+        k = int(n1[i])
+        assert np.array_equal(r1[i, :k], r2[i, :k])
+        assert np.array_equal(f1[i, :k], f2[i, :k]) and np.array_equal(b1[i, :k], b2[i, :k])
