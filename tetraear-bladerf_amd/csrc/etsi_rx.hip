@@ -833,7 +833,9 @@ template <> struct RCfg<uint4> { static constexpr int bps = 4, pf = 2, nb = 2, w
 template <> struct RCfg<float4> { static constexpr int bps = 8, pf = 3, nb = 1, wlr = WLR; };  // cf32: 2 samples (4 tiles: spills)
 template <typename In> constexpr int r_tk() { return RCfg<In>::nb == 1 ? 48 : 112; }   // stage-1 outputs per wave tile
 template <typename In> constexpr int r_chunks() { return 10 * r_tk<In>() * RCfg<In>::bps / 16; }   // 16-B loads per tile
-template <typename In> constexpr int r_img16() { return (RHALO + 10 * r_tk<In>()) * RCfg<In>::bps / 16; }
+// per-wave image: two halo slots (tile t reads slot t & 1; tile t's last RHALO samples are also
+// written into slot (t + 1) & 1 as they arrive, so no halo copy) + the tile's 10 TK samples
+template <typename In> constexpr int r_img16() { return (2 * RHALO + 10 * r_tk<In>()) * RCfg<In>::bps / 16; }
 template <typename In> constexpr int r_smem4() {
     return 2 + 4 * r_img16<In>() + (4 * RCfg<In>::wlr + 3 * SEAM + YLDS) / 2;
 }
@@ -1076,6 +1078,7 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_r(const In *__restrict__ iq
     constexpr int BPS = RCfg<In>::bps, PF = RCfg<In>::pf, NCH = r_chunks<In>(), NL = (NCH + 63) / 64;
     constexpr int NB = RCfg<In>::nb, TK = r_tk<In>(), TIN = 10 * TK, LR = RCfg<In>::wlr;
     constexpr int ROWK = NB == 1 ? 12 : 28;    // outputs per 16-lane row
+    constexpr int RH16 = RHALO * BPS / 16;     // 16-B chunks per halo
     constexpr int IMGB = r_img16<In>() * 16;   // image bytes per wave
     using Pair = typename std::conditional<SC16, uint2, float4>::type;   // two samples
     __shared__ float4 smem[r_smem4<In>()];
@@ -1166,15 +1169,23 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_r(const In *__restrict__ iq
     auto tile = [&](int t, In (&pf)[NL]) __attribute__((always_inline)) {
 #pragma unroll
         for (int r = 0; r < NL; ++r)
-            if (64 * r + lane < NCH) *reinterpret_cast<In *>(img + RHALO * BPS + 16 * (64 * r + lane)) = pf[r];
+            if (64 * r + lane < NCH) *reinterpret_cast<In *>(img + 2 * RHALO * BPS + 16 * (64 * r + lane)) = pf[r];
+        // the tile's last RHALO samples: also the next tile's halo slot
+#pragma unroll
+        for (int r = 0; r < NL; ++r) {
+            const int c = 64 * r + lane - (NCH - RH16);
+            if (c >= 0 && c < RH16) *reinterpret_cast<In *>(img + ((t + 1) & 1) * RHALO * BPS + 16 * c) = pf[r];
+        }
         __builtin_amdgcn_sched_barrier(0);
         load_tile(pf, t + PF);
         wave_sync();
-        // this lane's blocks: 10 NB samples as 5 NB pairs
+        // this lane's blocks: 10 NB samples as 5 NB pairs; image sample s < RHALO is in halo slot
+        // t & 1, the rest at 2 RHALO + (s - RHALO) (a lane's blocks lie on one side: blk < 4 or >= 4)
+        const uint8_t *bimg = img + (10 * blk + (blk < 4 ? (t & 1) * RHALO : RHALO)) * BPS;
         float xre[10 * NB], xim[10 * NB];
 #pragma unroll
         for (int m = 0; m < 5 * NB; ++m) {
-            const Pair v = *reinterpret_cast<const Pair *>(img + (10 * blk + 2 * m) * BPS);
+            const Pair v = *reinterpret_cast<const Pair *>(bimg + 2 * m * BPS);
             if constexpr (SC16) {
                 xre[2 * m] = (float)(int16_t)(v.x & 0xFFFFu);
                 xim[2 * m] = (float)(int16_t)(v.x >> 16);
@@ -1240,9 +1251,6 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_r(const In *__restrict__ iq
             }
         }
         wave_sync();
-        // halo for the next tile: image samples [0, 40) = this tile's [10 TK, 10 TK + 40)
-        if (lane < RHALO * BPS / 16)
-            reinterpret_cast<uint4 *>(img)[lane] = reinterpret_cast<const uint4 *>(img)[TIN * BPS / 16 + lane];
         const int kav = min(K0 + TK * t + TK - 5, K1 - 1);   // the tile's last output
         const int u_rdy = kav >= 113 ? min((kav - 113) / 10 + 1, u_end) : 0;
         while (u_rdy - u_done >= S2T || (t == ntile - 1 && u_rdy > u_done)) {
