@@ -65,11 +65,15 @@ def parse():
     ap.add_argument("--host-input", action="store_true",
                     help="etsi: PCIe-inclusive mode -- each batch is copied from pinned host memory (double-buffered "
                          "copy stream); value is then the host-fed rate, never the HBM-resident headline")
-    ap.add_argument("--cells", choices=("acquire", "given"), default="given",
-                    help="etsi: the lower MAC is given each channel's cell (as acquired by a streaming receiver "
-                         "from an earlier chunk), or acquires it from the batch's own BSCH (colour code 0 first, "
-                         "state kept across steps; channels whose chunk has no sync burst never acquire, "
-                         "because every step re-decodes the same batch)")
+    ap.add_argument("--cells", choices=("acquire", "given"), default="acquire",
+                    help="etsi: the lower MAC acquires each channel's cell itself (default: BSCH with colour code 0 "
+                         "first, the SYNC PDU's MCC / MNC / colour code kept per channel from step to step, over "
+                         "--chunks consecutive chunks of each channel's capture, as a streaming receiver does), or "
+                         "is given the synthesised cells up front")
+    ap.add_argument("--chunks", type=int, default=None,
+                    help="etsi: each channel is one continuous capture of CHUNKS x --samples samples, resident as "
+                         "CHUNKS batches; step k decodes batch k mod CHUNKS (default: 8 with --cells acquire, so the "
+                         "cell state a step starts from was acquired from earlier chunks; 1 with --cells given)")
     ap.add_argument("--demod", choices=("fused", "split"), default="fused",
                     help="etsi: fused channel filter + timing in one launch, or split (y through HBM, timing "
                          "launched separately -- beside the next batch's channel filter when pipelined)")
@@ -248,14 +252,15 @@ def time_steps(step, steps, warmup, world, sync, on_timed=None):
     sync()
     if on_timed is not None:
         on_timed()
-    if world > 1:
+    grouped = world > 1 or (dist.is_available() and dist.is_initialized())
+    if grouped:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     sync()
-    if world > 1:
+    if grouped:
         dist.barrier()
     return time.perf_counter() - t0
 
@@ -269,11 +274,14 @@ def main():
     # path with several ranks sharing fewer GPUs (rank -> LOCAL_RANK mod device count; the timing
     # all_reduce then runs on a host tensor).
     backend = os.environ.get("TETRA_BENCH_DIST", "nccl")
-    if world > 1:
-        dist.init_process_group(backend, init_method="env://")
+    # TETRA_BENCH_FORCE_DIST=1: join the process group and run the timing all_reduce even at
+    # WORLD_SIZE 1 (torchrun --nproc-per-node 1), so a one-GPU box executes the RCCL path itself
+    force = os.environ.get("TETRA_BENCH_FORCE_DIST") == "1"
     gpu = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
+    if world > 1 or force:
+        dist.init_process_group(backend, init_method="env://")
     os.environ["TETRA_HIP_DEVICE"] = str(gpu)
     c = _hip.ctx()
     stream = torch.cuda.current_stream(dev)
@@ -288,8 +296,9 @@ def main():
         C, N = 1, a.wb_samples   # units: wideband samples
     elif a.chain == "etsi":
         from tetraear.signal.etsi import BenchStep as EtsiStep
+        chunks = a.chunks if a.chunks is not None else (8 if a.cells == "acquire" else 1)
         step = EtsiStep(c, C, N, FS, seed=rank_seed(1000, rank), device=dev, iq_format=a.iq, demod=a.demod,
-                        cells=a.cells)
+                        cells=a.cells, chunks=chunks)
         pipe = "off" if a.no_pipeline else a.pipeline
         if pipe != "off":
             step.pipeline()
@@ -316,7 +325,7 @@ def main():
     for x in ctxs:
         x.check(x.lib.tetra_profile(x.handle, 0), "profile")
     # slowest rank (RCCL all_reduce MAX); identity at N=1
-    elapsed = max_over_ranks(elapsed, dev if backend == "nccl" else None)
+    elapsed = max_over_ranks(elapsed, dev if backend == "nccl" else None, force=force)
     ms_step = elapsed / a.steps * 1e3
     value = aggregate_msps(C * N, world, a.steps, elapsed)
 
@@ -356,7 +365,11 @@ def main():
                    if getattr(step, "hostfed", False) else {}),
                 **({"demod": step.demod_mode} if hasattr(step, "demod_mode") else {}),
                 **({"cells": step.cells_mode} if hasattr(step, "cells_mode") else {}),
+                **({"chunks_per_channel": step.chunks} if getattr(step, "chunks", 1) > 1 else {}),
             },
+            # the process group the timing reduction ran over (None: single process, no collective)
+            "dist": ({"backend": dist.get_backend(), "world": dist.get_world_size(),
+                      "reduce_tensor": "cuda" if backend == "nccl" else "cpu"} if dist.is_initialized() else None),
             "realtime_channels": int(step.realtime_channels(value) if hasattr(step, "realtime_channels")
                                      else value * 1e6 / FS),
             "roofline": {
@@ -376,7 +389,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define TETRA_ABI_VERSION 1
+#define TETRA_ABI_VERSION 2
 
 enum {
     TETRA_OK = 0,
@@ -202,20 +202,51 @@ enum {
 int tetra_mac_headers(tetra_ctx *ctx, const uint8_t *bits, const int32_t *nbits, size_t F, size_t stride,
                       int32_t *fields, uint8_t *data, size_t data_stride);
 
+/* Signal-present / AFC gate of the capture loop (/root/reference/tetraear/ui/modern.py:1952-2028,
+ * SURVEY.md §8f rank 1), per channel on the 2048-point Hann spectrum of its first 2048 samples
+ * (the k_waterfall row, fused): centre band of int(25000 / (fs / 2048)) bins around bin 1024, noise
+ * floor from the bins 10 beyond it on both sides, present iff snr > 15 dB and peak > -70 dBFS and
+ * peak - band mean > 3 dB, AFC offset = the peak bin's frequency when present.  stats [C][FIELDS]
+ * (host or device); power [C][2048] the dB rows or NULL; mixer_coef / mixer_on [C] (or NULL) the
+ * offset as tetra_demod_compat's mixer arguments (-2 pi f, f != 0), so process() runs on the gate's
+ * AFC with no host round trip.  N < 2048: no detection (all zero). */
+enum {
+    TETRA_GATE_VALID = 0,     /* 1 when a centre band exists (N >= 2048 and >= 2 band bins) */
+    TETRA_GATE_SIGNAL,        /* mean dB of the centre band */
+    TETRA_GATE_PEAK,          /* max dB of the centre band */
+    TETRA_GATE_PEAK_BIN,      /* its first index (0..2047, fftshifted) */
+    TETRA_GATE_PEAK_FREQ,     /* its frequency fftshift(fftfreq(2048, 1/fs))[bin], Hz */
+    TETRA_GATE_NOISE,         /* noise floor (mean dB outside the band +- 10 bins, -100 if none) */
+    TETRA_GATE_SNR,           /* signal - noise */
+    TETRA_GATE_ABOVE,         /* peak - signal */
+    TETRA_GATE_PRESENT,       /* 1: signal present (the three thresholds) */
+    TETRA_GATE_AFC,           /* the freq_offset process() gets: PEAK_FREQ when present, else 0 */
+    TETRA_GATE_FIELDS = 10
+};
+int tetra_afc_gate(tetra_ctx *ctx, const void *iq, int iq_fmt, size_t C, size_t N, double fs, float *power,
+                   double *stats, double *mixer_coef, uint8_t *mixer_on);
+
 /* =====================================================================================
  * ETSI EN 300 392-2 receive chain (north star; no reference counterpart)
  * ===================================================================================== */
 
-/* Receiver design (filled by the host: tetraear.signal.etsi.etsi_plan).  Supported: input at
- * q1 * 240 kHz with q1 = 10 (2.4 MSps), stage-1 48-tap decimator, stage-2 RRC (0.35) prototype at
- * 720 kHz resampled x3/10 to 72 kHz (4 samples/symbol). */
+/* Receiver design (filled by the host: tetraear.signal.etsi.etsi_plan).  Stage 1: L1-tap FIR
+ * decimating by q1 (fs -> fs1 = fs / q1); stage 2: RRC (0.35) polyphase prototype of Lp taps at
+ * up * fs1 = 4 * down * 18 kHz, resampled x up/down to 72 kHz (4 samples/symbol); then timing.
+ *   2.4 MSps: q1 = 10, L1 = 48, 3/10, Lp = 321 -- the canonical plan, run by the fused per-wave
+ *             kernels (k_chanfilt_r / k_chanfilt);
+ *   any other plan with q1 <= 13, L1 <= 64, Lp <= 4096 and (Lp - 1) / up <= 256 (e.g. the
+ *             reference CLI's 1.8-2.4 MSps in 0.1 MHz steps, modern.py:5518-5519, 5630-5638): the
+ *             generic-rate channel filter k_chanfilt_g (y through HBM) + k_timing.
+ * flags bit 0 (TETRA_ETSI_FORCE_GENERIC): run a canonical plan on the generic kernel too (tests). */
+#define TETRA_ETSI_FORCE_GENERIC 1
 typedef struct tetra_etsi_plan {
     int32_t q1, L1, Lp, up, down;
     float gain;           /* block-Gardner loop gain */
     float soft_scale;     /* int8 soft-bit scale: soft = rint(x * soft_scale / mean|d|) */
-    int32_t reserved;
+    int32_t flags;
     float h1[64];
-    float hp[384];
+    float hp[4096];
 } tetra_etsi_plan;
 
 #define TETRA_ETSI_MAXB 8    /* bursts per channel chunk */

@@ -79,15 +79,35 @@ def rrc(t, alpha=0.35):
 
 
 def design(fs=FS_NOMINAL):
-    """Receiver constants: stage-1 decimator taps, RRC polyphase prototype, loop constants."""
-    q1 = int(round(fs / 240000.0))
-    if abs(q1 * 240000.0 - fs) > 1e-6 or q1 < 1:
-        raise ValueError("ETSI receiver needs fs = q * 240 kHz")
-    L1 = 48 if q1 > 1 else 1
+    """Receiver constants for input rate fs: stage-1 decimator taps, RRC polyphase prototype, loop
+    constants.  The plan (spec of tetraear.signal.etsi.rate_design): stage 1 decimates by q1 to
+    fs1 = fs / q1 >= 180 kHz (q1 <= 13), stage 2 resamples by the reduced fraction up/down =
+    72 kHz / fs1 through an 8-symbol RRC prototype of 32 down + 1 taps (4 down taps per symbol)
+    scaled by 240 kHz / fs1; of the candidates with <= 4096 taps and < 254 taps per output, the
+    smallest down wins, then the largest q1."""
+    import math
+    fs_i = int(round(fs))
+    if abs(fs - fs_i) > 1e-6 or fs_i < 72000:
+        raise ValueError("ETSI receiver needs an integer rate >= 72 kHz")
+    cands = []
+    q1 = 1
+    while q1 <= 13 and (q1 == 1 or fs_i / q1 >= 180000.0):
+        g = math.gcd(72000 * q1, fs_i)
+        up, down = 72000 * q1 // g, fs_i // g
+        Lp = 32 * down + 1
+        if Lp <= 4096 and (Lp - 1) // up + 2 < 254:
+            cands.append((down, -q1, up))
+        q1 += 1
+    if not cands:
+        raise ValueError("no ETSI channel-filter plan for this rate")
+    down, q1, up = min(cands)
+    q1 = -q1
+    L1 = 1 if q1 == 1 else min(64, 2 * int(round(2.4 * q1)))
     h1 = (_design.firwin(L1, 60e3, fs=fs, window=("kaiser", 6.0)) if q1 > 1 else np.ones(1)).astype(np.float32)
-    Lp = 321
-    hp = rrc((np.arange(Lp) - (Lp - 1) / 2) / 40.0, 0.35).astype(np.float32)
-    return dict(q1=q1, L1=L1, h1=h1, Lp=Lp, hp=hp, up=3, down=10, gain=np.float32(1.5), soft_scale=np.float32(64.0))
+    Lp = 32 * down + 1
+    hp = (rrc((np.arange(Lp) - (Lp - 1) / 2) / (4.0 * down), 0.35) * (240000.0 * q1 / fs)).astype(np.float32)
+    return dict(q1=q1, L1=L1, h1=h1, Lp=Lp, hp=hp, up=up, down=down, gain=np.float32(1.5),
+                soft_scale=np.float32(64.0))
 
 
 def scramble_seq(init, n=432):
@@ -206,7 +226,7 @@ class Receiver:
         N = len(x) // 2
         M1 = max(0, (N - d["L1"]) // d["q1"] + 1)
         x240 = np.zeros(2 * max(M1, 1), np.float32)
-        y = np.zeros(2 * max(M1 * 3 // 10 + 2, 1), np.float32)
+        y = np.zeros(2 * max(M1 * d["up"] // d["down"] + 2, 1), np.float32)
         M2 = lib().eo_chanfilt(x, N, d["h1"], d["L1"], d["q1"], d["hp"], d["Lp"], d["up"], d["down"], x240, y)
         return y[:2 * M2].view(np.complex64).copy()
 

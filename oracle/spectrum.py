@@ -51,3 +51,52 @@ def dft_power(x, nfft=N_FFT):
     xw = np.asarray(x)[:nfft].astype(np.complex128) * np.hanning(nfft)
     X = np.exp(-2j * np.pi * np.outer(n, n) / nfft) @ xw
     return 20 * np.log10(np.abs(np.fft.fftshift(X)) / nfft + 1e-20)
+
+
+# ------------------------------------------------------------------ signal-present / AFC gate
+# the capture loop's gate in front of process() (/root/reference/tetraear/ui/
+# modern.py:1952-2028), as that survey row describes it -- centre-band mean / max / argmax of the
+# frame's dB row, the peak's frequency offset, the out-of-band noise mean, and the decision
+# snr > 15 and peak > -70 and peak_above_avg > 3.  Restated from that description in float64 on
+# frame_power; pinned by analytic known answers in tests/test_spectrum.py (tone on bin k -> offset
+# k fs / 2048; each threshold flipped on its own), not by reference fixtures (parity unpinned: the
+# round-1 refusal to record the reference's gate).
+
+GATE_FIELDS = ("valid", "signal", "peak", "peak_bin", "peak_freq", "noise", "snr", "above", "present", "afc")
+
+
+def gate_bins(fs, nfft=N_FFT, bandwidth=25000.0):
+    """(start, end, noise_end, noise_start2) of the centre band and the two noise bands."""
+    per_bin = fs / nfft
+    nb = int(bandwidth / per_bin)
+    centre = nfft // 2
+    start, end = max(0, centre - nb // 2), min(nfft, centre + nb // 2)
+    return start, end, max(0, start - 10), min(nfft, end + 10)
+
+
+def gate(power, fs, nfft=N_FFT):
+    """Gate decision on one fftshifted dB row: dict over GATE_FIELDS."""
+    p = np.asarray(power, np.float64)
+    start, end, n1, n2 = gate_bins(fs, nfft)
+    out = dict.fromkeys(GATE_FIELDS, 0.0)
+    if end <= start:
+        return out
+    band = p[start:end]
+    sig, peak = float(np.mean(band)), float(np.max(band))
+    k = start + int(np.argmax(band))
+    freqs = np.fft.fftshift(np.fft.fftfreq(nfft, 1 / fs))
+    noise_bins = np.concatenate([p[0:n1], p[n2:nfft]])
+    noise = float(np.mean(noise_bins)) if len(noise_bins) else -100.0
+    snr, above = sig - noise, peak - sig
+    present = snr > 15 and peak > -70 and above > 3
+    out.update(valid=1.0, signal=sig, peak=peak, peak_bin=float(k), peak_freq=float(freqs[k]), noise=noise, snr=snr,
+               above=above, present=float(present), afc=float(freqs[k]) if present and peak > -70 else 0.0)
+    return out
+
+
+def gate_iq(x, fs, nfft=N_FFT):
+    """The gate of a chunk: on the spectrum of its first nfft samples (no detection when shorter)."""
+    x = np.asarray(x)
+    if len(x) < nfft:
+        return dict.fromkeys(GATE_FIELDS, 0.0)
+    return gate(frame_power(x, nfft), fs, nfft)

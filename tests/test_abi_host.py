@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     assert len(names) > 15
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.tetra_abi_version() == 1
+    assert lib.tetra_abi_version() == 2
 
 
 def test_binding_covers_header():

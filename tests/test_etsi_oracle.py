@@ -64,3 +64,49 @@ def test_iq_round_trip(snr):
         for _, _, dec in res:
             for kind, t1, ok in dec:
                 assert ok and tuple(t1) in sent
+
+
+# the reference CLI's rates: -s in MHz, the GUI slider 1.8-2.4 MHz in 0.1 MHz steps
+# (/root/reference/tetraear/ui/modern.py:5518-5519, 5630-5638)
+CLI_RATES = [1.8e6, 1.9e6, 2.0e6, 2.1e6, 2.2e6, 2.3e6, 2.4e6]
+
+
+@pytest.mark.parametrize("fs", CLI_RATES)
+def test_iq_round_trip_every_cli_rate(fs):
+    """The oracle receiver at each rate the reference's callers use: a 54.6 ms chunk (131072 samples
+    at 2.4 MSps, the same air time at the other rates) decodes every burst it holds, each block
+    CRC-good and a transmitted payload, with ~983 symbols out."""
+    rng = np.random.default_rng(int(fs) // 1000)
+    cell = E.scramble_init(262, 1, 5)
+    bits, jobs = E.burst_stream(rng, 6, E.scramble_seq(cell))
+    rx = E.Receiver(fs)
+    n = int(round(131072 * fs / 2.4e6))
+    x = E.modulate(bits, n, fs=fs, t0=3.37, phase0=rng.uniform(0, 6.28), cfo=rng.uniform(-600, 600), snr_db=20.0,
+                   rng=rng)
+    sym, soft, hard, diag = rx.demod(x)
+    assert 960 < len(sym) < 990, len(sym)
+    res = rx.lower_mac(soft, hard, cell)
+    assert len(res) >= 2
+    sent = [tuple(t) for _, jj in jobs for _, t in jj]
+    for _, _, dec in res:
+        for kind, t1, ok in dec:
+            assert ok and tuple(t1) in sent
+
+
+def test_rate_plans_match_host_design():
+    """The host planner (tetraear.signal.etsi.rate_design / etsi_plan) equals the oracle's design at
+    every CLI rate and a few others: the same q1, L1, up / down, Lp and bit-identical taps; 2.4 MSps
+    is the canonical plan; 20 MSps (the wideband capture) has no single-channel plan."""
+    from tetraear.signal.etsi import etsi_plan, rate_design
+    for fs in CLI_RATES + [1.0e6, 240e3, 300e3]:
+        d = E.design(fs)
+        p = etsi_plan(fs)
+        assert (p.q1, p.L1, p.up, p.down, p.Lp) == (d["q1"], d["L1"], d["up"], d["down"], d["Lp"]), fs
+        assert np.array_equal(np.ctypeslib.as_array(p.h1)[:p.L1], d["h1"]), fs
+        assert np.array_equal(np.ctypeslib.as_array(p.hp)[:p.Lp], d["hp"]), fs
+        assert 72000 * p.q1 * p.down == int(fs) * p.up   # exactly 72 kHz out
+    assert rate_design(2.4e6) == (10, 48, 3, 10, 321)
+    with pytest.raises(ValueError):
+        rate_design(20e6)
+    with pytest.raises(ValueError):
+        E.design(20e6)

@@ -44,3 +44,24 @@ def test_torchrun_two_ranks_bench():
     elapsed = d["ms_per_step"] * steps / 1e3
     want = 2 * C * N * steps / elapsed / 1e6
     assert abs(d["value"] - want) <= 1e-3 * want, (d["value"], want)
+
+
+def test_torchrun_one_rank_rccl():
+    """bench.py's RCCL branch on the box's one GPU: torchrun --nproc-per-node 1 with the nccl (= RCCL)
+    backend, and TETRA_BENCH_FORCE_DIST=1 so the process group is joined and the timing all_reduce(MAX)
+    runs on a device tensor even at world size 1 (bench.py main, shard.max_over_ranks)."""
+    C, N, steps = 256, 131072, 3
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO, "bench.py"), "--gpus", "1", "--channels", str(C), "--samples", str(N),
+           "--steps", str(steps), "--warmup", "1", "--no-cpu", "--cells", "given"]
+    env = dict(os.environ, TETRA_BENCH_DIST="nccl", TETRA_BENCH_FORCE_DIST="1", OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = lines[0]
+    assert d["dist"] == {"backend": "nccl", "world": 1, "reduce_tensor": "cuda"}, d["dist"]
+    assert d["n_gpus"] == 1 and d["steps"] == steps
+    q = d["decoded_last_step"]
+    assert q["blocks"] >= 3 * C and q["crc_ok"] == q["blocks"], q

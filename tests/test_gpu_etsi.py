@@ -135,6 +135,8 @@ def test_process_and_decode_surface():
             for key in ("type", "type_name", "number", "timeslot", "bits", "header", "position", "encrypted",
                         "encryption_algorithm", "key_id", "additional_info", "burst_crc"):
                 assert key in f, key
+            # the MAC stage ran once per CRC-good SCH/F / SCH/HD block (never on the BSCH)
+            assert len(f["mac_pdus"]) <= sum(b["channel"] != "BSCH" and b["crc_ok"] for b in f["blocks"])
         oks += [b for f in frames for b in f["blocks"] if b["crc_ok"]]
     assert len(oks) >= 2
     assert all(tuple(np.pad(b["bits"], (0, 268 - len(b["bits"])))) in sent for b in oks)
@@ -626,7 +628,7 @@ def test_c4_full_chain_4096_bursts():
                 assert np.array_equal(t1[ch, k, :len(tb)], tb)
                 k += 1
         assert k == int(nk[ch])
-    # the same batch through the acquiring lower MAC (bench default): a channel acquires its cell
+    # the same batch through the acquiring lower MAC (one chunk, no earlier state): a channel acquires its cell
     # from a sync burst in the chunk, and every block of a channel that did decodes as with the cell given
     acq = BenchStep(c, C, N, 2.4e6, seed=44, device=dev, cells="acquire")
     acq()
@@ -686,3 +688,243 @@ def test_block_codec_vs_independent_spec(kind):
             m_tx = S.codeword_metric(soft[f], S.type2(t1[f]), kind, int(inits[f]))
             assert m_dec >= m_tx, (f, m_dec, m_tx)
     assert ngood >= F // 2
+
+
+def _check_blocks_transmitted(st, C):
+    """(blocks, CRC-good) of the step's last batch; asserts every CRC-good block's type-1 bits are
+    one of the channel's transmitted payloads (vectorised over a channel's payload rows)."""
+    nk, blocks, t1 = st.nblock.cpu().numpy(), st.blocks.cpu().numpy(), st.type1.cpu().numpy()
+    payload = st.payload.cpu().numpy()
+    n1 = np.array([268, 124, 60])
+    nblk = nok = 0
+    for ch in range(C):
+        k = int(nk[ch])
+        nblk += k
+        sent = payload[ch].reshape(-1, 268)
+        for j in range(k):
+            if blocks[ch, j, 1]:
+                nok += 1
+                bits = t1[ch, j].copy()
+                bits[n1[int(blocks[ch, j, 0])]:] = 0
+                assert np.any(np.all(sent == bits[None, :], axis=1)), (ch, j)
+    return nblk, nok
+
+
+def test_c5_full_shard_8192x131072():
+    """BASELINE configs[4] (C5) at its per-GPU shard, the bench's own step: 8192 channels x 131072 cf32
+    samples (8.6 GB resident in HBM).  Every CRC-good block carries a transmitted payload, >= 97 % of
+    the blocks pass at 18 dB Es/N0, and channels 0, 4095 and 8191 equal the oracle burst for burst
+    and bit for bit (soft symbols, soft bits, hard dibits, decoded type-1 bits, CRC flags)."""
+    import torch
+    from tetraear import _hip
+    from tetraear.signal.etsi import BenchStep
+    dev = torch.device("cuda", 0)
+    c = _hip.ctx()
+    C, N = 8192, 131072
+    st = BenchStep(c, C, N, 2.4e6, seed=1000, device=dev, cells="given")   # bench.py's rank-0 seed
+    st()
+    torch.cuda.synchronize(dev)
+    nblk, nok = _check_blocks_transmitted(st, C)
+    assert nblk >= 3 * C and nok / nblk >= 0.97, (nok, nblk)
+    rx = E.Receiver()
+    soft, hard, ns = st.soft.cpu().numpy(), st.hard.cpu().numpy(), st.nsym.cpu().numpy()
+    sym = st.sym.cpu().numpy()
+    nb, blocks, t1 = st.nburst.cpu().numpy(), st.blocks.cpu().numpy(), st.type1.cpu().numpy()
+    cells = st.cells.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+    for ch in (0, 4095, 8191):
+        x = st.iq[ch].cpu().numpy().view(np.complex64)[:, 0]
+        so, sbo, ho, _ = rx.demod(x)
+        n = int(ns[ch])
+        assert n == len(so) and np.array_equal(sym[ch, :n].view(np.complex64)[:, 0], so), ch
+        assert np.array_equal(hard[ch, :n - 1], ho) and np.array_equal(soft[ch, :2 * (n - 1)], sbo), ch
+        want = rx.lower_mac(sbo, ho, int(cells[ch]))
+        assert len(want) == int(nb[ch]), ch
+        k = 0
+        for start, bk, blks in want:
+            for _, tb, okb in blks:
+                assert int(blocks[ch, k, 1]) == int(bool(okb)) and np.array_equal(t1[ch, k, :len(tb)], tb), (ch, k)
+                k += 1
+        assert k == int(st.nblock[ch])
+
+
+def test_acquire_streaming_chunks():
+    """bench.py --cells acquire: each channel is one continuous capture of 8 chunks, step k decodes
+    chunk k mod 8 with the cell state the earlier steps left (no cell configured).  After one pass
+    over the chunks every channel whose capture holds a CRC-good sync burst has acquired its cell,
+    and the next pass decodes >= 97 % of the blocks, each a transmitted payload, with the same bits
+    as the cell-given lower MAC on the same batch."""
+    import torch
+    from tetraear import _hip
+    from tetraear.signal.etsi import BenchStep
+    dev = torch.device("cuda", 0)
+    c = _hip.ctx()
+    C, N, K = 1024, 131072, 8
+    acq = BenchStep(c, C, N, 2.4e6, seed=55, device=dev, cells="acquire", chunks=K)
+    for _ in range(K + 3):
+        acq()
+    torch.cuda.synchronize(dev)
+    q = acq.quality()
+    assert q["chunk"] == (K + 2) % K and q["crc_ok_frac"] >= 0.97, q
+    nblk, nok = _check_blocks_transmitted(acq, C)
+    assert nok / nblk >= 0.97
+    assert q["cells_acquired"] >= int(0.98 * C), q
+    # the same chunk through the cell-given lower MAC: identical blocks on every acquired channel
+    blocks_a, t1_a = acq.blocks.cpu().numpy(), acq.type1.cpu().numpy()
+    got = acq.cell_state.cpu().numpy() == acq.cells.cpu().numpy()
+    acq.cells_mode = "given"
+    acq.kchunk = K + 2
+    acq()
+    torch.cuda.synchronize(dev)
+    nk, blocks_g, t1_g = acq.nblock.cpu().numpy(), acq.blocks.cpu().numpy(), acq.type1.cpu().numpy()
+    for ch in np.nonzero(got)[0]:
+        k = int(nk[ch])
+        assert np.array_equal(blocks_a[ch, :k], blocks_g[ch, :k]) and np.array_equal(t1_a[ch, :k], t1_g[ch, :k]), ch
+
+
+def test_etsi_frames_mac_per_block():
+    """TetraDecoder(mode='etsi') runs the MAC PDU stage once per CRC-good SCH/F / SCH/HD block, in
+    order, and never on the BSCH (whose MAC-SYNC layout would read as PDU type / encryption mode) or
+    on CRC-failed blocks: the frames' PDUs equal a fresh parser's parse_mac_pdu over exactly those
+    blocks in the same order."""
+    from tetraear.core import TetraDecoder
+    from tetraear.core.etsi import EtsiLowerMac
+    from tetraear.core.protocol import TetraProtocolParser
+    rng = np.random.default_rng(8)
+    res_hdr = np.array([0, 0, 0, 0, 0, 0, 1, 1], np.uint8)   # MAC-RESOURCE, clear (type 00, mode 00)
+
+    def blk(ch, n, ok, head=None):
+        b = rng.integers(0, 2, n).astype(np.uint8)
+        if head is not None:
+            b[:len(head)] = head
+        return {"channel": ch, "crc_ok": ok, "bits": b, "block": 0}
+    enc = np.array([0, 0, 1, 1], np.uint8)   # a BSCH whose first bits would read as an encrypted MAC-RESOURCE
+    raw = [
+        {"position": 510, "burst": "SB", "burst_kind": 2, "timeslot": 1,
+         "blocks": [blk("BSCH", 60, True, enc), blk("SCH/HD", 124, True, res_hdr)]},
+        {"position": 1020, "burst": "NDB (p)", "burst_kind": 1, "timeslot": 2,
+         "blocks": [blk("SCH/HD", 124, False, enc), blk("SCH/HD", 124, True, res_hdr)]},
+        {"position": 1530, "burst": "NDB (n)", "burst_kind": 0, "timeslot": 3, "blocks": [blk("SCH/F", 268, True)]},
+        {"position": 2040, "burst": "NDB (n)", "burst_kind": 0, "timeslot": 0, "blocks": [blk("SCH/F", 268, False)]},
+    ]
+    for f in raw:
+        f["crc_ok"] = all(b["crc_ok"] for b in f["blocks"])
+    d = TetraDecoder(mode="etsi")
+    d._etsi = EtsiLowerMac()
+    frames = d._etsi_frames(raw)
+    ref = TetraProtocolParser()
+    want = [ref.parse_mac_pdu(b["bits"].astype(np.int64)) for f in raw for b in f["blocks"]
+            if b["channel"] != "BSCH" and b["crc_ok"]]
+    got = [p for f in frames for p in f["mac_pdus"]]
+    assert [(p["type"], p["encrypted"], p["address"], p["length"], p["data"]) for p in got] == \
+        [(p.pdu_type.name, p.encrypted, p.address, p.length, p.data) for p in want if p is not None]
+    sb = [f for f in frames if f["burst_kind"] == 2]
+    assert sb and sb[0]["header"][:8] == "00000011"   # the header is the SCH/HD block's, not the BSCH's
+    assert d.protocol_parser.stats["total_bursts"] == 4
+
+
+CLI_RATES = [1.8e6, 1.9e6, 2.0e6, 2.1e6, 2.2e6, 2.3e6, 2.4e6]   # modern.py:5518-5519, 5630-5638
+
+
+@pytest.mark.parametrize("fs", CLI_RATES)
+def test_every_cli_rate_vs_oracle_and_round_trip(fs):
+    """The ETSI chain at each rate the reference's CLI / GUI slider offers (1.8-2.4 MSps, 0.1 MHz
+    steps): 64 channels of a 54.6 ms chunk at 18 dB Es/N0.  Soft symbols, soft bits and hard dibits
+    bit-identical to the oracle on four channels (cf32 and SC16); >= 97 % of the decoded blocks
+    CRC-good, each a transmitted payload.  2.4 MSps runs the fused kernels, the others the
+    generic-rate channel filter (k_chanfilt_g) + k_timing."""
+    from tetraear import _hip
+    from tetraear.signal.etsi import EtsiReceiver, synth, etsi_plan, lengths
+    from tetraear.core.etsi import EtsiLowerMac
+    N = 2 * int(round(131072 * fs / 2.4e6 / 2))
+    C = 64
+    iq, cells, kinds, payload, t0 = synth(C, N, fs=fs, seed=int(fs) // 1000, snr_db=18.0)
+    rx = EtsiReceiver(fs)
+    hard, soft, sym, ns = rx.demod_batch(iq)
+    orc = E.Receiver(fs)
+    for ch in (0, 1, 31, 63):
+        so, sbo, ho, _ = orc.demod(iq[ch])
+        n = int(ns[ch])
+        assert n == len(so) and 960 < n < 990, (ch, n, len(so))
+        assert np.array_equal(sym[ch, :n], so) and np.array_equal(hard[ch, :n - 1], ho), ch
+        assert np.array_equal(soft[ch, :2 * (n - 1)], sbo), ch
+    # SC16 wire format: the same bits as cf32 of the scaled samples
+    sc = np.stack([np.rint(iq.real * 32768), np.rint(iq.imag * 32768)], -1).clip(-32768, 32767).astype(np.int16)
+    h2, s2, y2, n2 = rx.demod_batch(sc)
+    assert np.array_equal(n2, ns) and np.array_equal(y2, sym) and np.array_equal(h2, hard) and np.array_equal(s2, soft)
+    res = EtsiLowerMac().decode_batch(soft, hard, ns, cells)
+    nblk = nok = 0
+    for ch in range(C):
+        sent = payload[ch].reshape(-1, 268)
+        for f in res[ch]:
+            for b in f["blocks"]:
+                nblk += 1
+                if b["crc_ok"]:
+                    nok += 1
+                    bits = np.pad(b["bits"], (0, 268 - len(b["bits"])))
+                    assert np.any(np.all(sent == bits[None, :], axis=1)), ch
+    assert nblk >= 3 * C and nok / nblk >= 0.97, (nok, nblk)
+    c = _hip.ctx()
+    p = etsi_plan(fs)
+    name = ctypes_name(c, p, N)
+    assert name == ("k_chanfilt_r" if fs == 2.4e6 else "k_chanfilt_g"), name
+
+
+def ctypes_name(c, plan, N):
+    import ctypes
+    name = ctypes.create_string_buffer(64)
+    lds = ctypes.c_int64(0)
+    c.check(c.lib.tetra_etsi_kernel_info(c.handle, plan, 0, N, 1, name, 64, ctypes.byref(lds)), "kernel_info")
+    return name.value.decode()
+
+
+@pytest.mark.parametrize("fmt", ["cf32", "sc16"])
+def test_generic_kernel_equals_fused_at_2400k(fmt):
+    """The generic-rate channel filter run on the canonical 2.4 MSps plan (TETRA_ETSI_FORCE_GENERIC)
+    gives the same 72 kHz samples as the specialised per-wave kernel (stage 2 on MFMA), and the same
+    symbols through k_timing as the fused demod: two independent implementations of eo_chanfilt's
+    operation order agree bit for bit (odd chunk lengths included)."""
+    from tetraear import _hip
+    from tetraear.signal.etsi import etsi_plan, lengths, synth
+    for N in (131072, 65538, 20002):
+        iq = synth(5, N, seed=N, snr_db=16.0)[0]
+        x = iq if fmt == "cf32" else np.stack([np.rint(iq.real * 32768), np.rint(iq.imag * 32768)], -1).clip(
+            -32768, 32767).astype(np.int16)
+        f = _hip.TETRA_CF32 if fmt == "cf32" else _hip.TETRA_SC16
+        pc, pg = etsi_plan(2.4e6), etsi_plan(2.4e6, force_generic=True)
+        _, M2, sm = lengths(pc, N)
+        c = _hip.ctx()
+        ya, yb = np.zeros((5, M2), np.complex64), np.ones((5, M2), np.complex64)
+        c.check(c.lib.tetra_etsi_chanfilt_fmt(c.handle, pc, _hip.ptr(x), f, 5, N, _hip.ptr(ya)), "chanfilt")
+        c.check(c.lib.tetra_etsi_chanfilt_fmt(c.handle, pg, _hip.ptr(x), f, 5, N, _hip.ptr(yb)), "chanfilt_g")
+        assert np.array_equal(ya, yb), N
+        outs = []
+        for p in (pc, pg):
+            o = (np.zeros((5, sm), np.complex64), np.zeros((5, 2 * sm), np.int8), np.zeros((5, sm), np.uint8),
+                 np.zeros(5, np.int32))
+            c.check(c.lib.tetra_demod_etsi_fmt(c.handle, p, _hip.ptr(x), f, 5, N, *[_hip.ptr(a) for a in o], sm, None))
+            outs.append(o)
+        for a, b in zip(*outs):
+            assert np.array_equal(a, b), N
+
+
+def test_unsupported_rate_never_raises_into_the_loop(caplog):
+    """SURVEY §5's contract for the north-star chain: a SignalProcessor(mode='etsi') built for a rate
+    no channel-filter plan serves (20 MSps is the wideband capture's rate) logs and returns empty
+    output, as the reference's process() does when decimation fails (processor.py:253-257); the
+    library itself answers such a plan with TETRA_E_INVALID."""
+    import logging
+    from tetraear import _hip
+    from tetraear.signal import SignalProcessor
+    from tetraear.signal.etsi import etsi_plan
+    p = SignalProcessor(20e6, mode="etsi")
+    with caplog.at_level(logging.WARNING):
+        out = p.process(np.zeros(131072, np.complex64))
+    assert out.dtype == np.uint8 and len(out) == 0 and len(p.symbols) == 0
+    assert any("ETSI demodulation unavailable" in r.message for r in caplog.records)
+    bad = etsi_plan(1.8e6)
+    bad2 = _hip.EtsiPlan.from_buffer_copy(bad)
+    bad2.Lp = 5000
+    c = _hip.ctx()
+    x = np.zeros((1, 131072), np.complex64)
+    y = np.zeros((1, 8192), np.complex64)
+    assert c.lib.tetra_etsi_chanfilt(c.handle, bad2, _hip.ptr(x), 1, 131072, _hip.ptr(y)) == -1

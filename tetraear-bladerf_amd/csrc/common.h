@@ -28,6 +28,7 @@ enum Slot {
     S_W12,                                                 // ETSI channel-filter tap image (kept)
     S_W13,                                                 // diagnostics (tetra_read_floor sink)
     S_W14,                                                 // ETSI: scrambler inits the cell table holds
+    S_W15,                                                 // ETSI generic-rate tap tables (etsi_rate.hip)
     S_COUNT
 };
 
@@ -49,6 +50,8 @@ struct tetra_ctx {
     char arch[64] = {0};
     float coef_etsi[128 + 39 * 64];    // host image of the channel-filter tap tables (h1, h1 / 32768, stage-2 MFMA A)
     const void *coef_etsi_dev = nullptr;   // workspace the tap image was last uploaded to
+    std::vector<float> taps_rate;      // generic-rate ETSI taps (h1, hp) as last uploaded to slot S_W15
+    const void *taps_rate_dev = nullptr;
     std::vector<float> taps_wb;        // host image of the wideband prototype + resampler taps
     std::vector<float> taps_wb_up;     // ... as last uploaded to taps_wb_dev (slot S_W9)
     const void *taps_wb_dev = nullptr;
@@ -124,3 +127,10 @@ __device__ __forceinline__ uint2 ld_nt(const uint2 *p) {
     const nt_u2 v = __builtin_nontemporal_load(reinterpret_cast<const nt_u2 *>(p));
     return make_uint2(v.x, v.y);
 }
+
+// ETSI channel filter at a non-canonical rate (etsi_rate.hip): plan limits (nullptr = supported),
+// the launch (y [C][M2] to HBM), and the kernel symbol (tetra_etsi_kernel_info).
+const char *etsi_generic_unsupported(const tetra_etsi_plan *P);
+int launch_chanfilt_generic(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *x, int fmt, size_t C, size_t N,
+                            int64_t M1, int64_t M2, float2 *y);
+const void *chanfilt_generic_fn(int fmt);

@@ -1947,10 +1947,17 @@ static void scramble_seq(uint32_t r, int n, uint8_t *out) {
     }
 }
 
+// The canonical 2.4 MSps plan runs on the fused per-wave kernels; any other supported plan (or a
+// canonical one with TETRA_ETSI_FORCE_GENERIC) on the generic-rate channel filter (etsi_rate.hip).
+static bool canonical(const tetra_etsi_plan *P) {
+    return P->q1 == 10 && P->L1 == 48 && P->up == 3 && P->down == 10 && P->Lp == 3 * TPP &&
+           !(P->flags & TETRA_ETSI_FORCE_GENERIC);
+}
 static int etsi_check(tetra_ctx *ctx, const tetra_etsi_plan *P) {
     if (!P) return tetra_fail(ctx, TETRA_E_INVALID, "plan is NULL");
-    if (P->q1 != 10 || P->L1 != 48 || P->up != 3 || P->down != 10 || P->Lp != 3 * TPP)
-        return tetra_fail(ctx, TETRA_E_INVALID, "unsupported ETSI plan (q1=10, L1=48, 3/10, Lp=321 required)");
+    if (canonical(P)) return TETRA_OK;
+    if (const char *why = etsi_generic_unsupported(P))
+        return tetra_fail(ctx, TETRA_E_INVALID, "unsupported ETSI plan: %s", why);
     return TETRA_OK;
 }
 
@@ -1989,6 +1996,7 @@ static const char *const CF_NAMES[] = {"k_chanfilt_r", "k_chanfilt_r", "k_chanfi
 // Stage-1 taps and the per-branch stage-2 tap table (k_chanfilt), then the launch.
 static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *x, int fmt, size_t C, size_t N,
                            int64_t M1, int64_t M2, float2 *y, const TimingOut *fused = nullptr) {
+    if (!canonical(P)) return fused ? TETRA_E_INVALID : launch_chanfilt_generic(ctx, P, x, fmt, C, N, M1, M2, y);
     static_assert(sizeof(ctx->coef_etsi) == CF_COEF * sizeof(float), "tap image size");
     float *coef = (float *)ws(ctx, S_W12, CF_COEF * 4);   // slot of its own: the image persists
     if (!coef) return TETRA_E_NOMEM;
@@ -2069,9 +2077,16 @@ int tetra_etsi_kernel_info(tetra_ctx *ctx, const tetra_etsi_plan *P, int fmt, si
     if (!ctx || !P || (fmt != TETRA_CF32 && fmt != TETRA_SC16)) return TETRA_E_INVALID;
     int64_t M1, M2, sm;
     tetra_etsi_lengths(P, N, &M1, &M2, &sm);
+    hipFuncAttributes a;
+    if (etsi_check(ctx, P)) return TETRA_E_INVALID;
+    if (!canonical(P)) {
+        HIP_TRY(ctx, hipFuncGetAttributes(&a, chanfilt_generic_fn(fmt)));
+        if (name && name_len) snprintf(name, name_len, "%s", "k_chanfilt_g");
+        if (lds_bytes) *lds_bytes = (int64_t)a.sharedSizeBytes;
+        return TETRA_OK;
+    }
     if (fused) fused = fused_fits(fmt, M2, sm, N);   // the fused form's own condition (tetra_demod_etsi_fmt)
     const CfKernel k = chanfilt_kernel(fmt, M2, N, fused != 0);
-    hipFuncAttributes a;
     HIP_TRY(ctx, hipFuncGetAttributes(&a, chanfilt_fn(k, fmt)));
     if (name && name_len) snprintf(name, name_len, "%s", CF_NAMES[k]);
     if (lds_bytes) *lds_bytes = (int64_t)a.sharedSizeBytes;
@@ -2164,7 +2179,7 @@ int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *i
     // fused: timing runs in the channel filter's workgroup on y in LDS (k_chanfilt_r: y never leaves
     // LDS; k_chanfilt<uint2>: y round-trips through a C x M2 scratch and is re-staged into the freed
     // image) (measured: cf32 with y through L2 at four workgroups per CU is 2.5 % slower)
-    const bool fuse = fused_fits(fmt, M2, sm, N);
+    const bool fuse = canonical(P) && fused_fits(fmt, M2, sm, N);
     if (fuse) {
         float2 *ys = nullptr;   // k_chanfilt<uint2>: y's round trip
         if (fmt == TETRA_SC16 && !per_wave(fmt, M2, N) && !(ys = (float2 *)ws(ctx, S_W3, C * (size_t)M2 * 8)))

@@ -96,13 +96,101 @@ __device__ __forceinline__ void stage8(float2 *fr, const float2 *tw, int j) {
     __syncthreads();
 }
 
-// out[g][WF_N] for frames g = (c, f): x[c * N + f * hop + n], n < 2048.
-template <int FMT>
+// The signal-present / AFC gate of the reference's capture loop (modern.py:1952-2028; SURVEY.md §8f
+// rank 1), evaluated on frame 0's dB row: the centre band [start, end) (25 kHz: int(25000 / (fs /
+// 2048)) bins around bin 1024), its mean, maximum and first argmax; the noise floor = the mean of
+// the bins below start - 10 and from end + 10 on (-100 dB when there are none); snr = mean - noise;
+// signal present iff snr > 15, peak > -70 and peak - mean > 3; the AFC offset is the peak bin's
+// frequency, fftshift(fftfreq(2048, 1/fs))[peak], when present.  The offset is also written as the
+// compat demod's mixer inputs (tetra_demod_compat: coefficient -2 pi f and on/off), so process()
+// can run on it with no host round trip.
+struct GateArgs {
+    int start, end, nb_end, nb2;   // centre band, noise bands [0, nb_end) and [nb2, 2048)
+    double val;                    // fftfreq bin spacing 1 / (2048 (1 / fs))
+    double *stats;                 // [C][TETRA_GATE_FIELDS]
+    double *mc;                    // [C] mixer coefficient (or nullptr)
+    uint8_t *mo;                   // [C] mixer on (or nullptr)
+};
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// block-wide gate reduction over the dB row in LDS (all 256 threads); thread 0 writes the results
+__device__ void gate_row(const float *pw, const GateArgs &ga, long c, double *red, float *redf, int *redi) {
+    const int j = threadIdx.x, lane = j & 63, w = j >> 6;
+    double ssum = 0.0, nsum = 0.0;
+    float pk = -INFINITY;
+    int pki = 0x7FFFFFFF;
+    for (int i = ga.start + j; i < ga.end; i += WF_T) {
+        const float v = pw[i];
+        ssum += (double)v;
+        if (v > pk) { pk = v; pki = i; }   // ascending i per thread: the first maximum
+    }
+    for (int i = j; i < ga.nb_end; i += WF_T) nsum += (double)pw[i];
+    for (int i = ga.nb2 + j; i < WF_N; i += WF_T) nsum += (double)pw[i];
+    ssum = wave_sum_d(ssum);
+    nsum = wave_sum_d(nsum);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {   // max, ties to the lower bin
+        const float pv = __shfl_xor(pk, o, 64);
+        const int pi = __shfl_xor(pki, o, 64);
+        if (pv > pk || (pv == pk && pi < pki)) { pk = pv; pki = pi; }
+    }
+    if (lane == 0) { red[2 * w] = ssum; red[2 * w + 1] = nsum; redf[w] = pk; redi[w] = pki; }
+    __syncthreads();
+    if (j == 0) {
+        double S = 0.0, Nn = 0.0;
+        float P = -INFINITY;
+        int Pi = 0x7FFFFFFF;
+        for (int q = 0; q < WF_T / 64; ++q) {
+            S += red[2 * q];
+            Nn += red[2 * q + 1];
+            if (redf[q] > P || (redf[q] == P && redi[q] < Pi)) { P = redf[q]; Pi = redi[q]; }
+        }
+        const int nsig = ga.end - ga.start, nnoise = ga.nb_end + (WF_N - ga.nb2);
+        double *st = ga.stats + (size_t)c * TETRA_GATE_FIELDS;
+        double present = 0.0, afc = 0.0;
+        if (nsig > 0) {
+            const double sig = S / nsig, peak = (double)P;
+            const double noise = nnoise > 0 ? Nn / nnoise : -100.0;
+            const double snr = sig - noise, above = peak - sig;
+            const double fo = (double)(Pi - WF_N / 2) * ga.val;
+            present = (snr > 15.0 && peak > -70.0 && above > 3.0) ? 1.0 : 0.0;
+            afc = (present != 0.0 && peak > -70.0) ? fo : 0.0;   // modern.py:2028
+            st[TETRA_GATE_SIGNAL] = sig;
+            st[TETRA_GATE_PEAK] = peak;
+            st[TETRA_GATE_PEAK_BIN] = (double)Pi;
+            st[TETRA_GATE_PEAK_FREQ] = fo;
+            st[TETRA_GATE_NOISE] = noise;
+            st[TETRA_GATE_SNR] = snr;
+            st[TETRA_GATE_ABOVE] = above;
+        } else {
+            for (int q = TETRA_GATE_SIGNAL; q <= TETRA_GATE_ABOVE; ++q) st[q] = 0.0;
+        }
+        st[TETRA_GATE_VALID] = nsig > 0 ? 1.0 : 0.0;
+        st[TETRA_GATE_PRESENT] = present;
+        st[TETRA_GATE_AFC] = afc;
+        if (ga.mc) ga.mc[c] = afc != 0.0 ? (-2.0 * 3.141592653589793) * afc : 0.0;   // processor.py:99
+        if (ga.mo) ga.mo[c] = afc != 0.0 ? 1 : 0;
+    }
+}
+
+// out[g][WF_N] for frames g = (c, f): x[c * N + f * hop + n], n < 2048.  GATE: one frame per
+// channel, the gate evaluated on its row (out may then be null).
+template <int FMT, bool GATE = false>
 __global__ __launch_bounds__(WF_T) void k_waterfall(const void *__restrict__ x, size_t N, size_t hop, int nframes,
                                                    long total, const float *__restrict__ win,
-                                                   const float2 *__restrict__ twg, float *__restrict__ out) {
+                                                   const float2 *__restrict__ twg, float *__restrict__ out,
+                                                   GateArgs ga = GateArgs{}) {
     __shared__ float2 fr[WF_PAD];
     __shared__ float2 tw[TW_N];
+    __shared__ float pw[GATE ? WF_N : 1];
+    __shared__ double red[GATE ? 2 * WF_T / 64 : 1];
+    __shared__ float redf[GATE ? WF_T / 64 : 1];
+    __shared__ int redi[GATE ? WF_T / 64 : 1];
     const int j = threadIdx.x;
     for (int i = j; i < TW_N; i += WF_T) tw[i] = twg[i];
     float w[8];
@@ -131,7 +219,7 @@ __global__ __launch_bounds__(WF_T) void k_waterfall(const void *__restrict__ x, 
         stage8<8, TW2>(fr, tw, j);
         stage8<64, TW3>(fr, tw, j);
         // stage 4: radix 4, Ns = 512, butterflies j and j + 256 -> natural-order bins j + 512 r
-        float *o = out + (size_t)g * WF_N;
+        float *o = out ? out + (size_t)g * WF_N : nullptr;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int jj = j + 256 * h;
@@ -145,10 +233,21 @@ __global__ __launch_bounds__(WF_T) void k_waterfall(const void *__restrict__ x, 
             for (int r = 0; r < 4; ++r) {
                 const int k = jj + 512 * r;
                 const float mag = sqrtf(a[r].x * a[r].x + a[r].y * a[r].y);
-                __builtin_nontemporal_store(20.0f * log10f(mag * (1.0f / WF_N) + 1e-20f), &o[(k + WF_N / 2) & (WF_N - 1)]);
+                const float db = 20.0f * log10f(mag * (1.0f / WF_N) + 1e-20f);
+                const int sidx = (k + WF_N / 2) & (WF_N - 1);
+                if constexpr (GATE) {
+                    pw[sidx] = db;
+                    if (out) __builtin_nontemporal_store(db, &o[sidx]);
+                } else {
+                    __builtin_nontemporal_store(db, &o[sidx]);
+                }
             }
         }
         __syncthreads();   // stage-4 reads done before the next frame's stage-1 scatter
+        if constexpr (GATE) {
+            gate_row(pw, ga, g, red, redf, redi);
+            __syncthreads();   // pw / red reads done before the next frame
+        }
     }
 }
 
@@ -217,6 +316,70 @@ int tetra_waterfall(tetra_ctx *ctx, const void *iq, int iq_fmt, size_t C, size_t
             default:
                 hipLaunchKernelGGL(k_waterfall<TETRA_CF64>, dim3(grid), dim3(WF_T), 0, ctx->stream, xd, N, hop,
                                    (int)nframes, total, tab->win, tab->tw, od);
+        }
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    return st.finish();
+}
+
+int tetra_afc_gate(tetra_ctx *ctx, const void *iq, int iq_fmt, size_t C, size_t N, double fs, float *power,
+                   double *stats, double *mixer_coef, uint8_t *mixer_on) {
+    if (!ctx) return TETRA_E_INVALID;
+    if (iq_fmt != TETRA_CF32 && iq_fmt != TETRA_SC16 && iq_fmt != TETRA_CF64)
+        return tetra_fail(ctx, TETRA_E_INVALID, "unknown sample format %d", iq_fmt);
+    if (!iq || !stats || C == 0 || !(fs > 0.0)) return tetra_fail(ctx, TETRA_E_INVALID, "bad gate request");
+    const size_t bps = iq_fmt == TETRA_CF32 ? 8 : iq_fmt == TETRA_SC16 ? 4 : 16;
+    Staging st(ctx);
+    double *sd = (double *)st.out(stats, C * TETRA_GATE_FIELDS * 8);
+    double *mcd = mixer_coef ? (double *)st.out(mixer_coef, C * 8) : nullptr;
+    uint8_t *mod = mixer_on ? (uint8_t *)st.out(mixer_on, C) : nullptr;
+    if (!sd || (mixer_coef && !mcd) || (mixer_on && !mod)) return st.finish();
+    if (N < (size_t)WF_N) {   // no spectrum, no detection (modern.py:1929, 1954): zeros, signal absent
+        HIP_TRY(ctx, hipMemsetAsync(sd, 0, C * TETRA_GATE_FIELDS * 8, ctx->stream));
+        if (mcd) HIP_TRY(ctx, hipMemsetAsync(mcd, 0, C * 8, ctx->stream));
+        if (mod) HIP_TRY(ctx, hipMemsetAsync(mod, 0, C, ctx->stream));
+        if (power) return tetra_fail(ctx, TETRA_E_INVALID, "no 2048-sample frame in %zu samples", N);
+        return st.finish();
+    }
+    const void *xd = st.in(iq, C * N * bps);
+    float *od = power ? (float *)st.out(power, C * WF_N * 4) : nullptr;
+    WfTables *tab = (WfTables *)ws(ctx, S_W11, sizeof(WfTables));
+    if (!xd || (power && !od) || !tab) return st.finish();
+    if (!ctx->wf_tables_ready) {
+        static WfTables host;
+        static std::once_flag once;
+        std::call_once(once, [] { wf_tables(host); });
+        HIP_TRY(ctx, hipMemcpyAsync(tab, &host, sizeof(WfTables), hipMemcpyHostToDevice, ctx->stream));
+        ctx->wf_tables_ready = true;
+    }
+    // the band and noise bins, as the capture loop derives them from fs (host doubles, same ops)
+    GateArgs ga{};
+    const double fres = fs / (double)WF_N;
+    const int bb = (int)(25000.0 / fres);
+    ga.start = std::max(0, WF_N / 2 - bb / 2);
+    ga.end = std::min(WF_N, WF_N / 2 + bb / 2);
+    ga.nb_end = std::max(0, ga.start - 10);
+    ga.nb2 = std::min(WF_N, ga.end + 10);
+    if (ga.end < ga.start) ga.end = ga.start;
+    ga.val = 1.0 / ((double)WF_N * (1.0 / fs));
+    ga.stats = sd;
+    ga.mc = mcd;
+    ga.mo = mod;
+    {
+        PROF(ctx, "afc_gate");
+        const unsigned grid = (unsigned)std::min<long>((long)C, 256 * 4);
+        switch (iq_fmt) {
+            case TETRA_CF32:
+                hipLaunchKernelGGL((k_waterfall<TETRA_CF32, true>), dim3(grid), dim3(WF_T), 0, ctx->stream, xd, N,
+                                   (size_t)WF_N, 1, (long)C, tab->win, tab->tw, od, ga);
+                break;
+            case TETRA_SC16:
+                hipLaunchKernelGGL((k_waterfall<TETRA_SC16, true>), dim3(grid), dim3(WF_T), 0, ctx->stream, xd, N,
+                                   (size_t)WF_N, 1, (long)C, tab->win, tab->tw, od, ga);
+                break;
+            default:
+                hipLaunchKernelGGL((k_waterfall<TETRA_CF64, true>), dim3(grid), dim3(WF_T), 0, ctx->stream, xd, N,
+                                   (size_t)WF_N, 1, (long)C, tab->win, tab->tw, od, ga);
         }
         HIP_TRY(ctx, hipGetLastError());
     }

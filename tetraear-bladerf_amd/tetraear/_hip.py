@@ -38,12 +38,15 @@ class CompatPlan(ctypes.Structure):
     ]
 
 
+ETSI_FORCE_GENERIC = 1   # tetra_etsi_plan.flags: run a canonical plan on the generic-rate kernel
+
+
 class EtsiPlan(ctypes.Structure):
     """Mirror of struct tetra_etsi_plan (include/tetra_hip.h)."""
     _fields_ = [
         ("q1", ctypes.c_int32), ("L1", ctypes.c_int32), ("Lp", ctypes.c_int32), ("up", ctypes.c_int32),
         ("down", ctypes.c_int32), ("gain", ctypes.c_float), ("soft_scale", ctypes.c_float),
-        ("reserved", ctypes.c_int32), ("h1", ctypes.c_float * 64), ("hp", ctypes.c_float * 384),
+        ("flags", ctypes.c_int32), ("h1", ctypes.c_float * 64), ("hp", ctypes.c_float * 4096),
     ]
 
 
@@ -115,6 +118,7 @@ def _bind(L):
         "tetra_read_floor": (_i32, [_vp, _vp, _sz, _sz, _sz]),
         "tetra_resample": (_i32, [_vp, _vp, _i32, _sz, _sz, _sz, _vp]),
         "tetra_waterfall": (_i32, [_vp, _vp, _i32, _sz, _sz, _sz, _sz, _sz, _vp]),
+        "tetra_afc_gate": (_i32, [_vp, _vp, _i32, _sz, _sz, ctypes.c_double, _vp, _vp, _vp, _vp]),
         "tetra_channelize": (_i32, [_vp, ctypes.POINTER(WbPlan), _vp, _sz, _vp, _sz]),
         "tetra_synth_wideband": (_i32, [_vp, ctypes.POINTER(WbPlan), _sz, ctypes.c_uint64, ctypes.c_float,
                                         ctypes.c_float, _vp, _vp, _vp, _vp, _vp]),

@@ -271,35 +271,50 @@ class TetraDecoder:
 
     def _etsi_frames(self, raw):
         """ETSI bursts as the reference's frame dicts (decoder.py:960-972 keys + the MAC PDU stage),
-        built from the channel-decoded type-1 bits: a burst's blocks in order (SCH/F 268 bits,
-        SCH/HD 2 x 124, BSCH 60 + SCH/HD 124), frame number start // 510, burst_crc = every block's
-        CRC-16.  The ETSI details stay on the frame: 'blocks', 'burst', 'burst_kind'.  The MAC PDU
-        stage (drop rule included) is the compat one, applied to the decoded bits."""
+        built from the channel-decoded type-1 bits.  Every logical channel block carries its own MAC
+        PDU (EN 300 392-2 §21.4), so the MAC stage runs once per CRC-good SCH/F or SCH/HD block, in
+        burst and block order: the BSCH is skipped (its MAC-SYNC PDU has another layout, and the
+        cell it carries is already EtsiLowerMac's acquisition) and CRC-failed blocks are not parsed
+        (their bits are not the transmitted ones).  Per burst: frame number start // 510,
+        burst_crc = every block's CRC-16, the frame header and type from the first MAC block, and the
+        compat drop rule (no PDU and a failed CRC drops the burst).  The burst's first PDU goes
+        through the compat MAC stage ('mac_pdu', 'encrypted', 'encryption_algorithm'); all of them
+        are on 'mac_pdus'.  The ETSI details stay on the frame: 'blocks', 'burst', 'burst_kind'."""
         from tetraear.core.protocol import BurstType, TetraBurst
-        rows, items = [], []
-        for f in raw:
-            bits = np.concatenate([b["bits"] for b in f["blocks"]]).astype(np.int64)
-            if len(bits) < 8:
-                continue
-            rows.append(bits.astype(np.uint8))
-            items.append((f, bits))
-        if not rows:
-            return []
-        fields, data = self.protocol_parser.mac_fields(rows)
+        rows, owner = [], []   # one row per CRC-good SCH/F / SCH/HD block, in order
+        for i, f in enumerate(raw):
+            for b in f["blocks"]:
+                if b["channel"] != "BSCH" and b["crc_ok"]:
+                    rows.append(np.asarray(b["bits"], np.uint8))
+                    owner.append(i)
+        fields, data = self.protocol_parser.mac_fields(rows) if rows else (None, None)
+        pdus = [[] for _ in raw]
         out = []
-        for k, (f, bits) in enumerate(items):
+        k = 0
+        for i, f in enumerate(raw):
+            mac_blocks = [b for b in f["blocks"] if b["channel"] != "BSCH"] or f["blocks"]
+            if not mac_blocks:
+                continue
+            bits = np.asarray(mac_blocks[0]["bits"]).astype(np.int64)
             number = f["position"] // 510
             frame = self._frame_dict(bits, f["position"], number)
             crc_ok = bool(f["crc_ok"])
             self.protocol_parser.count_burst(crc_ok)
             frame.update(burst_crc=crc_ok, blocks=f["blocks"], burst=f["burst"], burst_kind=f["burst_kind"])
+            while k < len(owner) and owner[k] == i:   # the MAC state advances in block order
+                pdu = self.protocol_parser.mac_state(fields[k], data[k])
+                if pdu is not None:
+                    pdus[i].append(pdu)
+                k += 1
             burst = TetraBurst(burst_type=BurstType.Synchronization if f["burst_kind"] == 2 else BurstType.NormalDownlink,
                                slot_number=number % 4, frame_number=self.protocol_parser.current_frame_number,
-                               training_sequence=np.zeros(0, np.int64), data_bits=bits, crc_ok=crc_ok,
-                               colour_code=self._etsi.colour_code or 0)
-            pdu = self.protocol_parser.mac_state(fields[k], data[k])
-            frame = self._mac_stage(frame, burst, pdu)
+                               training_sequence=np.zeros(0, np.int64),
+                               data_bits=np.concatenate([np.asarray(b["bits"]) for b in f["blocks"]]).astype(np.int64),
+                               crc_ok=crc_ok, colour_code=self._etsi.colour_code or 0)
+            frame = self._mac_stage(frame, burst, pdus[i][0] if pdus[i] else None)
             if frame:
+                frame['mac_pdus'] = [{'type': p.pdu_type.name, 'encrypted': p.encrypted, 'address': p.address,
+                                      'length': p.length, 'data': p.data} for p in pdus[i]]
                 out.append(frame)
         return out
 

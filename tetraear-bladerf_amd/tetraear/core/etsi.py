@@ -31,6 +31,15 @@ def cell_of(init):
 UNKNOWN_CELL = scrambling_init(0, 0, 0)   # colour code 0: what a receiver descrambles with before the BSCH
 
 
+def acquired_channels(nblock, blocks):
+    """[C] bool: the channel's call decoded a CRC-good BSCH block (block kind 2), i.e. the cell
+    k_cell_acquire keeps came from a SYNC PDU of this call."""
+    nblock = np.asarray(nblock)
+    blocks = np.asarray(blocks)
+    live = np.arange(blocks.shape[1])[None, :] < nblock[:, None]
+    return np.any(live & (blocks[:, :, 0] == 2) & (blocks[:, :, 1] != 0), axis=1)
+
+
 class EtsiLowerMac:
     """Lower MAC of the ETSI chain.  With a cell (mcc, mnc, colour_code) every channel is
     descrambled with it.  Without one the receiver acquires the cell itself: each chunk's BSCH
@@ -44,13 +53,16 @@ class EtsiLowerMac:
         self.acquire = mcc is None and mnc is None and colour_code is None
         self.cell = None if self.acquire else scrambling_init(mcc or 0, mnc or 0, colour_code or 0)
         self.cell_state = None   # [C] scrambling inits of the acquired cells (acquisition mode)
+        # [C] bool: a CRC-good BSCH has been decoded on the channel.  Kept apart from cell_state,
+        # because an all-zero cell (MCC = MNC = CC = 0) has the init of UNKNOWN_CELL.
+        self.acquired = None
 
     @property
     def cells(self):
         """Per channel (MCC, MNC, colour code) acquired so far, None where no BSCH decoded yet."""
         if self.cell_state is None:
             return []
-        return [None if int(v) == UNKNOWN_CELL else cell_of(v) for v in self.cell_state]
+        return [cell_of(v) if a else None for v, a in zip(self.cell_state, self.acquired)]
 
     @property
     def mcc(self):
@@ -83,10 +95,12 @@ class EtsiLowerMac:
         if self.acquire and cells is None:
             if self.cell_state is None or len(self.cell_state) != C:
                 self.cell_state = np.full(C, UNKNOWN_CELL, np.uint32)
+                self.acquired = np.zeros(C, bool)
             c.check(c.lib.tetra_lmac_etsi_acquire(c.handle, _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(nsym), C, smax,
                                                   _hip.ptr(self.cell_state), _hip.ptr(nb), _hip.ptr(bursts),
                                                   _hip.ptr(nk), _hip.ptr(blocks), _hip.ptr(t1)),
                     "tetra_lmac_etsi_acquire")
+            self.acquired |= acquired_channels(nk, blocks)
         else:
             cells = np.full(C, self.cell if self.cell is not None else UNKNOWN_CELL, np.uint32) if cells is None \
                 else np.ascontiguousarray(cells, np.uint32)

@@ -17,11 +17,12 @@ def rank_seed(base_seed, rank):
     return base_seed + 1000 * rank
 
 
-def max_over_ranks(value, device=None):
-    """max of a float over all ranks (identity when torch.distributed is not initialised)."""
+def max_over_ranks(value, device=None, force=False):
+    """max of a float over all ranks (identity when torch.distributed is not initialised).  With a
+    `device` the reduction runs on a device tensor (RCCL); `force` runs it even in a one-rank group."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()) or (dist.get_world_size() == 1 and not force):
         return float(value)
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)

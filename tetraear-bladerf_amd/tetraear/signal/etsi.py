@@ -35,17 +35,47 @@ def rrc(t, alpha=0.35):
     return out
 
 
-@functools.lru_cache(maxsize=8)
-def etsi_plan(fs=2.4e6):
-    """Receiver design for input rate fs (= 10 x 240 kHz)."""
-    q1 = int(round(fs / 240000.0))
-    if q1 != 10 or abs(q1 * 240000.0 - fs) > 1e-6:
-        raise ValueError("the ETSI receiver is built for 2.4 MSps channel captures (10 x 240 kHz)")
+def rate_design(fs):
+    """(q1, L1, up, down, Lp) of the receiver for input rate fs: stage 1 decimates by q1 (L1-tap FIR,
+    fs1 = fs / q1 >= 180 kHz), stage 2 resamples fs1 x up/down to 72 kHz (4 samples/symbol) with an
+    8-symbol RRC prototype of Lp = 32 down + 1 taps at up * fs1 = 4 down x 18 kHz.  Among the q1 <= 13
+    whose plan fits the kernels (Lp <= 4096, a stage-2 window of < 254 taps) the smallest `down` (the
+    shortest prototype) wins, then the larger q1.  2.4 MSps gives the canonical 10, 48, 3/10, 321;
+    the reference CLI's 1.8-2.4 MSps (modern.py:5518-5519, 5630-5638) give q1 = 10 / 10 / 10 / 7 / 11
+    / 10 / 10.  Raises ValueError for a rate no such plan serves (e.g. 20 MSps: that is the wideband
+    channeliser's input)."""
+    from fractions import Fraction
+    fs_i = int(round(fs))
+    if abs(fs - fs_i) > 1e-6 or fs_i < 72000:
+        raise ValueError(f"ETSI receiver: unsupported sample rate {fs!r} (integer Hz >= 72 kHz required)")
+    best = None
+    for q1 in range(1, 14):
+        if q1 > 1 and fs_i / q1 < 180000.0:
+            break
+        r = Fraction(72000 * q1, fs_i)
+        up, down = r.numerator, r.denominator
+        Lp = 32 * down + 1
+        if Lp > 4096 or (Lp - 1) // up + 2 >= 254:
+            continue
+        L1 = 1 if q1 == 1 else min(64, 2 * int(round(2.4 * q1)))
+        if best is None or (down, -q1) < best[0]:
+            best = ((down, -q1), (q1, L1, up, down, Lp))
+    if best is None:
+        raise ValueError(f"ETSI receiver: no channel-filter plan for {fs_i} Sps")
+    return best[1]
+
+
+@functools.lru_cache(maxsize=16)
+def etsi_plan(fs=2.4e6, force_generic=False):
+    """Receiver design for input rate fs (rate_design): stage-1 Kaiser FIR (60 kHz cutoff), RRC(0.35)
+    prototype scaled by 240 kHz / fs1 (1 at the canonical 2.4 MSps), loop constants."""
+    q1, L1, up, down, Lp = rate_design(fs)
     p = _hip.EtsiPlan()
-    p.q1, p.L1, p.Lp, p.up, p.down = q1, 48, 321, 3, 10
+    p.q1, p.L1, p.Lp, p.up, p.down = q1, L1, Lp, up, down
     p.gain, p.soft_scale = 1.5, 64.0
-    h1 = _design.firwin(48, 60e3, fs=fs, window=("kaiser", 6.0)).astype(np.float32)
-    hp = rrc((np.arange(321) - 160) / 40.0).astype(np.float32)
+    p.flags = _hip.ETSI_FORCE_GENERIC if force_generic else 0
+    h1 = (_design.firwin(L1, 60e3, fs=fs, window=("kaiser", 6.0)) if q1 > 1 else np.ones(1)).astype(np.float32)
+    hp = (rrc((np.arange(Lp) - (Lp - 1) / 2) / (4.0 * down)) * (240000.0 * q1 / fs)).astype(np.float32)
     for i, v in enumerate(h1):
         p.h1[i] = v
     for i, v in enumerate(hp):
@@ -130,9 +160,15 @@ class EtsiReceiver:
         uint8 dibits, one fewer than the symbols (the fused demod's decision without its CFO
         rotation; ETSI-mode demodulate_dqpsk)."""
         x = np.asarray(symbols)
+        if x.dtype in (np.float32, np.float64) and x.ndim == 2:   # interleaved I/Q: [n, 2] -> [n] complex
+            if x.shape[1] != 2:
+                raise ValueError("real-valued 2-D symbols must be interleaved I/Q of shape [n, 2]")
+            x = np.ascontiguousarray(x).view(np.complex64 if x.dtype == np.float32 else np.complex128)[:, 0]
+        elif not np.iscomplexobj(x):   # 1-D real samples: zero imaginary part, as numpy's angle() reads them
+            x = x.astype(np.complex64 if x.dtype == np.float32 else np.complex128)
         if len(x) < 2:
             return np.array([], dtype=np.uint8)
-        fmt = _hip.TETRA_CF32 if x.dtype in (np.complex64, np.float32) else _hip.TETRA_CF64
+        fmt = _hip.TETRA_CF32 if x.dtype == np.complex64 else _hip.TETRA_CF64
         xc = np.ascontiguousarray(x, np.complex64 if fmt == _hip.TETRA_CF32 else np.complex128)
         out = np.empty(len(x) - 1, np.uint8)
         c = _hip.ctx()
@@ -193,7 +229,8 @@ class BenchStep:
 
     dtype = "f32 (DSP), int8/int32 (Viterbi)"
 
-    def __init__(self, c, C, N, fs, seed, device, snr_db=18.0, iq_format="cf32", demod="fused", cells="given"):
+    def __init__(self, c, C, N, fs, seed, device, snr_db=18.0, iq_format="cf32", demod="fused", cells="given",
+                 chunks=1):
         import torch
         self.c, self.C, self.N, self.fs = c, C, N, fs
         # "acquire": the lower MAC finds each channel's cell in its BSCH (tetra_lmac_etsi_acquire,
@@ -207,18 +244,41 @@ class BenchStep:
         self.fmt = {"cf32": _hip.TETRA_CF32, "sc16": _hip.TETRA_SC16}[iq_format]
         self.plan = etsi_plan(fs)
         _, self.M2, self.smax = lengths(self.plan, N)
-        nb = c.lib.tetra_synth_bursts_per_channel(N, fs)
-        self.iq = torch.empty((C, N, 2), dtype=torch.float32, device=device)
+        # chunks > 1: every channel is one continuous capture of chunks x N samples, resident in HBM
+        # as `chunks` consecutive [C, N] batches; step k decodes batch k mod chunks, so the state the
+        # acquiring lower MAC carries into a step comes from the channel's earlier chunks -- a
+        # receiver streaming 128 Ki chunks (modern.py:1919) with the cell state of protocol.py:479-485
+        self.chunks = max(1, int(chunks))
+        NT = N * self.chunks
+        nb = c.lib.tetra_synth_bursts_per_channel(NT, fs)
         self.cells = torch.empty(C, dtype=torch.int32, device=device)
         self.kinds = torch.empty((C, nb), dtype=torch.int32, device=device)
         self.payload = torch.empty((C, nb, 2, 268), dtype=torch.uint8, device=device)
-        c.check(c.lib.tetra_synth_etsi(c.handle, C, N, fs, seed, snr_db, 600.0, _hip.ptr(self.iq), _hip.ptr(self.cells),
-                                       _hip.ptr(self.kinds), _hip.ptr(self.payload), None), "synth")
+        if self.chunks == 1:
+            self.iqs = [torch.empty((C, N, 2), dtype=torch.float32, device=device)]
+            c.check(c.lib.tetra_synth_etsi(c.handle, C, N, fs, seed, snr_db, 600.0, _hip.ptr(self.iqs[0]),
+                                           _hip.ptr(self.cells), _hip.ptr(self.kinds), _hip.ptr(self.payload), None),
+                    "synth")
+        else:
+            # synthesised in channel slices (a slice's whole capture, then cut into the chunk batches)
+            self.iqs = [torch.empty((C, N, 2), dtype=torch.float32, device=device) for _ in range(self.chunks)]
+            S = max(1, min(C, (1 << 30) // NT))
+            for s0 in range(0, C, S):
+                n = min(S, C - s0)
+                x = torch.empty((n, NT, 2), dtype=torch.float32, device=device)
+                c.check(c.lib.tetra_synth_etsi(c.handle, n, NT, fs, seed + 7919 * (s0 // S), snr_db, 600.0, _hip.ptr(x),
+                                               _hip.ptr(self.cells[s0:]), _hip.ptr(self.kinds[s0:]),
+                                               _hip.ptr(self.payload[s0:]), None), "synth")
+                for k in range(self.chunks):
+                    self.iqs[k][s0:s0 + n].copy_(x[:, k * N:(k + 1) * N])
+                del x
         c.check(c.lib.tetra_etsi_set_cells(c.handle, _hip.ptr(self.cells), C), "set_cells")
         from tetraear.core.etsi import UNKNOWN_CELL
         self.cell_state = torch.full((C,), UNKNOWN_CELL, dtype=torch.int32, device=device)
         if self.fmt == _hip.TETRA_SC16:   # the synth output is on the SC16 grid: exact
-            self.iq = torch.round(self.iq * 32768).clamp_(-32768, 32767).to(torch.int16)
+            self.iqs = [torch.round(x * 32768).clamp_(-32768, 32767).to(torch.int16) for x in self.iqs]
+        self.iq = self.iqs[0]
+        self.kchunk = 0
         sm = self.smax
         self.sym = torch.empty((C, sm, 2), dtype=torch.float32, device=device)
         self.soft = torch.empty((C, 2 * sm), dtype=torch.int8, device=device)
@@ -268,6 +328,8 @@ class BenchStep:
         overlaps batch k's demod -- the rate a host-fed receiver (SDR capture buffers) would see.
         Never the headline `value` (that is measured with the input resident in HBM)."""
         import torch
+        if self.chunks > 1:
+            raise ValueError("host-fed mode streams one resident batch (chunks=1)")
         dev = self.iq.device
         self.host = self.iq.cpu().pin_memory()
         self.dbuf = [self.iq, torch.empty_like(self.iq)]
@@ -283,7 +345,9 @@ class BenchStep:
     def _input(self):
         """Device input of this step: the resident batch, or (host-fed) the freshly copied buffer."""
         if not getattr(self, "hostfed", False):
-            return self.iq
+            x = self.iqs[self.kchunk % self.chunks]
+            self.kchunk += 1
+            return x
         import torch
         i = self.kin & 1
         self.kin += 1
@@ -391,7 +455,10 @@ class BenchStep:
         nb = self.nblock.cpu().numpy()
         blocks = self.blocks.cpu().numpy()
         ok = sum(int(blocks[i, :nb[i], 1].sum()) for i in range(self.C))
-        q = dict(blocks=int(nb.sum()), crc_ok=ok, bursts=int(self.nburst.sum().item()))
+        q = dict(blocks=int(nb.sum()), crc_ok=ok, bursts=int(self.nburst.sum().item()),
+                 crc_ok_frac=round(ok / max(1, int(nb.sum())), 5))
+        if self.chunks > 1:
+            q["chunk"] = (self.kchunk - 1) % self.chunks   # the batch the last step decoded
         if self.cells_mode == "acquire":
             q["cells_acquired"] = int((self.cell_state == self.cells).sum().item())
         return q

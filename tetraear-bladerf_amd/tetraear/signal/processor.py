@@ -259,7 +259,13 @@ class SignalProcessor:
     def process(self, samples, freq_offset=0):
         """Complete demodulation of one chunk (processor.py:221-273); sets ``self.symbols``."""
         if self.mode == "etsi":
-            hard, self.symbols = self._etsi_rx().process(np.asarray(samples), freq_offset)
+            try:
+                rx = self._etsi_rx()
+            except ValueError as e:   # a rate with no channel-filter plan: log and go on (processor.py:253-257)
+                logger.warning(f"ETSI demodulation unavailable: {e}")
+                self.symbols = np.zeros(0, np.complex64)
+                return np.zeros(0, np.uint8)
+            hard, self.symbols = rx.process(np.asarray(samples), freq_offset)
             return hard
         if len(samples) == 0:
             self.symbols = np.array([], dtype=complex)
@@ -295,24 +301,52 @@ class SignalProcessor:
 
         Returns (hard [C, S-1] uint8, symbols [C, S] complex128, nsym [C]); row c holds what
         process(samples[c], freq_offsets[c]) returns / stores in .symbols, in its first
-        nsym[c]-1 / nsym[c] entries."""
-        x = np.asarray(samples)
-        C, N = x.shape
-        fmt = _fmt_of(x)
-        xc = _as_complex(x, fmt)
-        fo = np.zeros(C) if freq_offsets is None else np.asarray(freq_offsets, np.float64)
+        nsym[c]-1 / nsym[c] entries.  ``freq_offsets``: None (no mixer), [C] Hz on the host, a [C]
+        torch tensor of Hz on the GPU (the mixer inputs are derived on the device), or ``"afc"``: the
+        capture loop's signal-present / AFC gate (modern.py:1952-2028, spectrum.afc_gate) runs on
+        the device on each channel's first 2048 samples and feeds its offset straight into the demod
+        (no host round trip); the gate's per-channel results are kept in ``self.gate`` (the loop
+        only demodulates channels with ``self.gate["present"]``)."""
+        x = np.asarray(samples) if not hasattr(samples, "data_ptr") else samples
+        C, N = x.shape[:2]
+        dev_offsets = hasattr(freq_offsets, "data_ptr")
+        afc = isinstance(freq_offsets, str)
+        if afc and freq_offsets != "afc":
+            raise ValueError("freq_offsets must be None, an array of Hz, a device tensor or 'afc'")
+        fmt = _fmt_of(x) if not hasattr(x, "data_ptr") else _hip.TETRA_CF32
+        xc = _as_complex(x, fmt) if not hasattr(x, "data_ptr") else x
         plan, m, _ = compat_plan(self.sample_rate, N, fmt)
         smax = m // plan.sps + 1
         soft = np.empty((C, smax), np.complex128)
         hard = np.empty((C, smax), np.uint8)
         ns = np.zeros(C, np.int32)
         f32 = ctypes_int()
-        mc = np.array([mixer_coefficient(f) if f != 0 else 0.0 for f in fo], np.float64)
-        mo = (fo != 0).astype(np.uint8)
         c = _hip.ctx()
+        gate = None
+        if afc or dev_offsets:
+            import torch
+            dev = torch.device("cuda", torch.cuda.current_device()) if not dev_offsets else freq_offsets.device
+            if not hasattr(xc, "data_ptr"):
+                xc = torch.from_numpy(np.ascontiguousarray(xc)).to(dev)   # staged once for gate + demod
+            if afc:
+                from tetraear.signal.spectrum import afc_gate
+                torch.cuda.current_stream(dev).synchronize()   # the library runs on its own stream
+                gate = afc_gate(xc, self.sample_rate, mixer=True)
+                mc, mo = gate["mixer_coef"], gate["mixer_on"]
+            else:
+                f = freq_offsets.to(torch.float64)
+                mc = torch.where(f != 0, f * (-2 * np.pi), torch.zeros_like(f))   # mixer_coefficient, on device
+                mo = (f != 0).to(torch.uint8)
+                torch.cuda.current_stream(dev).synchronize()
+        else:
+            fo = np.zeros(C) if freq_offsets is None else np.asarray(freq_offsets, np.float64)
+            mc = np.array([mixer_coefficient(f) if f != 0 else 0.0 for f in fo], np.float64)
+            mo = (fo != 0).astype(np.uint8)
         c.check(c.lib.tetra_demod_compat(c.handle, plan, _hip.ptr(xc), fmt, C, N, _hip.ptr(mc), _hip.ptr(mo),
                                          _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(ns), smax, f32),
                 "tetra_demod_compat")
+        if gate is not None:
+            self.gate = {k: v.cpu().numpy() for k, v in gate.items()}
         return hard, soft, ns
 
     def _etsi_rx(self):

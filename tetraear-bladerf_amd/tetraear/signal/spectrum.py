@@ -72,3 +72,45 @@ def spectrum(samples, sample_rate, center_freq=0.0, nfft=N_FFT):
     power = waterfall(samples, hop=nfft, nframes=1, nfft=nfft)[0]
     freqs = np.fft.fftshift(np.fft.fftfreq(nfft, 1 / sample_rate)) + center_freq
     return freqs, power
+
+
+GATE_FIELDS = ("valid", "signal", "peak", "peak_bin", "peak_freq", "noise", "snr", "above", "present", "afc")
+
+
+def afc_gate(iq, sample_rate, power=False, mixer=False):
+    """The capture loop's signal-present / AFC gate (modern.py:1952-2028) for every channel of a
+    [C][N] batch (or one [N] chunk), on the GPU (tetra_afc_gate: fused into the waterfall kernel's
+    frame-0 row).  Returns a dict of [C] arrays over GATE_FIELDS -- band mean ``signal``, ``peak`` and
+    ``peak_bin`` / ``peak_freq``, ``noise`` floor, ``snr``, ``above`` (peak - mean), ``present`` and
+    ``afc`` (the freq_offset the loop hands process()) -- plus ``power`` [C][2048] (power=True) and the
+    compat demod's mixer inputs ``mixer_coef`` / ``mixer_on`` (mixer=True).  Device (torch) input
+    keeps every output on the device."""
+    fmt, shape_of, dev = _fmt(iq)
+    if not dev:
+        want = {_hip.TETRA_CF32: np.complex64, _hip.TETRA_CF64: np.complex128, _hip.TETRA_SC16: np.int16}[fmt]
+        iq = np.ascontiguousarray(iq, want)
+    else:
+        iq = iq.contiguous()
+    one = len(shape_of.shape) == 1
+    C = 1 if one else shape_of.shape[0]
+    N = shape_of.shape[-1]
+    if dev:
+        import torch
+        mk = lambda shape, dt: torch.zeros(shape, dtype=getattr(torch, dt), device=iq.device)   # noqa: E731
+    else:
+        mk = lambda shape, dt: np.zeros(shape, getattr(np, dt))   # noqa: E731
+    stats = mk((C, len(GATE_FIELDS)), "float64")
+    pw = mk((C, N_FFT), "float32") if power and N >= N_FFT else None
+    mc = mk((C,), "float64") if mixer else None
+    mo = mk((C,), "uint8") if mixer else None
+    c = _hip.ctx()
+    c.check(c.lib.tetra_afc_gate(c.handle, _hip.ptr(iq), fmt, C, N, float(sample_rate),
+                                 _hip.ptr(pw) if pw is not None else None, _hip.ptr(stats),
+                                 _hip.ptr(mc) if mc is not None else None, _hip.ptr(mo) if mo is not None else None),
+            "tetra_afc_gate")
+    out = {k: (stats[0, i] if one else stats[:, i]) for i, k in enumerate(GATE_FIELDS)}
+    if pw is not None:
+        out["power"] = pw[0] if one else pw
+    if mixer:
+        out["mixer_coef"], out["mixer_on"] = mc, mo
+    return out
