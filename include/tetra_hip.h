@@ -226,6 +226,26 @@ enum {
 int tetra_afc_gate(tetra_ctx *ctx, const void *iq, int iq_fmt, size_t C, size_t N, double fs, float *power,
                    double *stats, double *mixer_coef, uint8_t *mixer_on);
 
+/* The scanner's TETRA signal detector over a batch of candidate channels (SURVEY.md §8f rank 2;
+ * replaces the per-sample Python loops of /root/reference/tetraear/signal/scanner.py:42-147 and
+ * 204-231): per channel of iq [C][N] (TETRA_CF32 / TETRA_CF64) the counts the detector's decisions
+ * are made from -- the pi/4-DQPSK cluster test over consecutive samples, the best 31-bit match of
+ * sync_pattern (bit j of the word = pattern bit j) over the bits of the samples strided by
+ * `downsample`, and the mean powers of the chunk and of its five equal windows -- into
+ * stats [C][TETRA_SCAN_FIELDS] (host or device).  At most 131072 sync bits per channel. */
+enum {
+    TETRA_SCAN_MOD_MATCHES = 0,   /* phase differences within pi/8 of a multiple of pi/4 in [-pi, 3pi/4] */
+    TETRA_SCAN_MOD_DIFFS,         /* N - 1 */
+    TETRA_SCAN_SYNC_MATCHES,      /* best match count (0..31) over the window starts */
+    TETRA_SCAN_SYNC_WINDOWS,      /* window starts searched: max(0, nbits - 31) */
+    TETRA_SCAN_SYNC_BITS,         /* bits: strided samples - 1 */
+    TETRA_SCAN_POWER,             /* mean |x|^2 */
+    TETRA_SCAN_POWER_W0,          /* mean |x|^2 of window i = [i (N/5), (i+1) (N/5)), i = 0..4 */
+    TETRA_SCAN_FIELDS = TETRA_SCAN_POWER_W0 + 5
+};
+int tetra_scan_detect(tetra_ctx *ctx, const void *iq, int iq_fmt, size_t C, size_t N, int downsample,
+                      uint32_t sync_pattern, double *stats);
+
 /* =====================================================================================
  * ETSI EN 300 392-2 receive chain (north star; no reference counterpart)
  * ===================================================================================== */

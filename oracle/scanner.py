@@ -1,0 +1,81 @@
+"""CPU oracle for the scanner's TETRA signal detector (TEST INFRASTRUCTURE -- only tests/ use it).
+
+SURVEY.md §8f rank 2: /root/reference/tetraear/signal/scanner.py:42-147 (calculate_power,
+detect_tetra_modulation, detect_sync_pattern) and :204-231 (check_power_stability), restated in
+numpy from that survey row's description of them, in the dtype numpy computes them in (complex64 ->
+float32 angles, differences and wrap; the cluster distance in float64).  Vectorised: the reference's
+per-sample loops become array expressions with the same comparisons.
+
+Parity unpinned against the reference itself: pinned by analytic known answers in
+tests/test_scanner.py -- an ideal pi/4-DQPSK walk gives modulation confidence 1.0, a phase walk
+whose strided differences spell the sync pattern gives correlation 1.0, tones at the decision edges.
+"""
+import numpy as np
+
+SYNC_PATTERN = np.array([0, 1, 0, 1, 1, 0, 0, 1, 1, 1, 0, 0, 0, 1, 0, 0,
+                         1, 0, 1, 1, 0, 0, 1, 1, 1, 0, 0, 0, 1, 0, 0])
+
+
+def _wrap(d):
+    """(d + pi) % (2 pi) - pi in d's dtype (numpy's weak Python-float scalars)."""
+    return (d + np.pi) % (2 * np.pi) - np.pi
+
+
+def calculate_power(x, bottom=-85.0):
+    x = np.asarray(x)
+    if x.size == 0:
+        return float(bottom)
+    return float(10 * np.log10(np.mean(np.abs(x) ** 2) + 1e-10))
+
+
+def modulation_counts(x):
+    """(matches, differences) of the pi/4 cluster test on the normalised samples."""
+    x = np.asarray(x)
+    x = x / (np.abs(x).max() + 1e-10)
+    d = _wrap(np.diff(np.angle(x)))
+    e = np.array([-np.pi, -3 * np.pi / 4, -np.pi / 2, -np.pi / 4, 0, np.pi / 4, np.pi / 2, 3 * np.pi / 4])
+    dist = np.abs(e[None, :] - d.astype(np.float64)[:, None]).min(axis=1)
+    return int(np.sum(dist < np.pi / 8)), len(d)
+
+
+def detect_tetra_modulation(x):
+    if len(x) < 1000:
+        return False, 0.0
+    m, n = modulation_counts(x)
+    conf = m / n
+    return conf > 0.4, conf
+
+
+def sync_bits(x, fs):
+    D = max(1, int(fs / 18000 / 10))
+    s = np.asarray(x)[::D]
+    d = _wrap(np.diff(np.angle(s)))
+    q = d / (np.pi / 4)
+    return (np.abs(q) <= 0.5).astype(np.int64), len(s)   # round(q) == 0, round half to even
+
+
+def sync_best(bits):
+    """Best match count of the 31-bit pattern over window starts 0 .. len(bits) - 32."""
+    n = len(bits) - 31
+    if n <= 0:
+        return 0, 0
+    w = np.lib.stride_tricks.sliding_window_view(bits, 31)[:n]
+    return int((w == SYNC_PATTERN[None, :]).sum(axis=1).max()), n
+
+
+def detect_sync_pattern(x, fs):
+    bits, nsym = sync_bits(x, fs)
+    if nsym < 100 or len(bits) < 31:
+        return False, 0.0
+    best, n = sync_best(bits)
+    corr = best / 31 if n > 0 else 0.0
+    return corr > 0.75, corr
+
+
+def check_power_stability(x, num_windows=5):
+    x = np.asarray(x)
+    if len(x) < num_windows * 1000:
+        return False
+    ws = len(x) // num_windows
+    p = [calculate_power(x[i * ws:(i + 1) * ws]) for i in range(num_windows)]
+    return bool(np.std(p) < 10.0)

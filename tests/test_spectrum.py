@@ -141,3 +141,136 @@ def test_waterfall_rejects_bad_requests():
         waterfall(x, nfft=1024)
     with pytest.raises(ValueError):
         waterfall(np.zeros(100, np.complex64))
+
+
+# ------------------------------------------------------------------ signal-present / AFC gate
+# SURVEY.md §8f rank 1 (/root/reference/tetraear/ui/modern.py:1952-2028).  Known answers: a comb
+# filling the 25 kHz centre band (alternating-sign tones on every band bin, so the Hann leakage
+# adds up flat) with one bin raised by g, plus white noise sigma.  Each case flips one threshold.
+GATE_FS = 2.4e6
+BIN_HZ = GATE_FS / 2048   # 1171.875
+
+
+def _comb(A, g, kp, sigma, N=131072, seed=0, fs=GATE_FS):
+    rng = np.random.default_rng(seed)
+    n = np.arange(N)
+    start, end, _, _ = S.gate_bins(fs)
+    x = np.zeros(N, np.complex128)
+    for b in range(start, end):
+        x += A * (g if b == kp else 1.0) * (-1.0) ** b * np.exp(2j * np.pi * (b - 1024) * n / 2048)
+    x += sigma * (rng.standard_normal(N) + 1j * rng.standard_normal(N))
+    return x.astype(np.complex64)
+
+
+# (A, g, peak bin, sigma) -> (present, the threshold it sits on)
+GATE_KATS = [
+    ((0.01, 4, 1030, 1e-4), True, "present, peak 6 bins up"),
+    ((0.01, 4, 1014, 1e-4), True, "present, peak on the band's first bin"),
+    ((0.001, 4, 1030, 0.01), True, "snr 17 > 15"),
+    ((0.001, 4, 1030, 0.02), False, "snr 11 < 15"),
+    ((3e-4, 4, 1020, 1e-6), True, "peak -62.5 > -70"),
+    ((1e-4, 4, 1020, 1e-6), False, "peak -72 < -70"),
+    ((0.01, 2, 1020, 1e-4), True, "peak - mean 3.4 > 3"),
+    ((0.01, 1.6, 1020, 1e-4), False, "peak - mean 2.3 < 3"),
+]
+
+
+def test_gate_oracle_known_answers():
+    """The oracle gate on the comb KATs: band = bins 1014..1033 at 2.4 MSps (int(25000 / 1171.875) = 21
+    bins, 10 each side of bin 1024, the upper one exclusive), noise from bins < 1004 and >= 1044;
+    the peak bin's offset is (bin - 1024) x 1171.875 Hz and is the AFC offset exactly when the three
+    thresholds pass; each threshold flips the decision on its own."""
+    assert S.gate_bins(GATE_FS) == (1014, 1034, 1004, 1044)
+    assert S.gate_bins(1.8e6) == (1010, 1038, 1000, 1048)   # 878.9 Hz bins: 28
+    for args, present, why in GATE_KATS:
+        g = S.gate_iq(_comb(*args), GATE_FS)
+        assert g["valid"] == 1.0 and bool(g["present"]) == present, (why, g)
+        assert g["peak_bin"] == args[2] and g["peak_freq"] == (args[2] - 1024) * BIN_HZ, why
+        assert g["afc"] == (g["peak_freq"] if present else 0.0), why
+    assert S.gate_iq(np.zeros(2047, np.complex64), GATE_FS)["valid"] == 0.0   # < 2048 samples: no detection
+
+
+def _gate_vs_oracle(got, x, fs, i=None):
+    """GPU gate row vs the float64 oracle: dB statistics within GATE_DB_TOL; the decision and peak
+    bin equal whenever the oracle's margins exceed that tolerance (no case here sits in the band)."""
+    want = S.gate_iq(x, fs)
+    pick = (lambda k: float(got[k])) if i is None else (lambda k: float(got[k][i]))
+    for k in ("signal", "peak", "noise", "snr", "above"):
+        assert abs(pick(k) - want[k]) <= GATE_DB_TOL, (k, pick(k), want[k])
+    assert pick("valid") == want["valid"] and pick("present") == want["present"]
+    assert pick("peak_bin") == want["peak_bin"] and pick("peak_freq") == want["peak_freq"]
+    assert pick("afc") == want["afc"]
+    return want
+
+
+GATE_DB_TOL = 2e-3   # fp32 FFT vs float64, averaged dB over the band / the noise bins (measured ~1e-4)
+
+
+@pytest.mark.gpu
+def test_gate_gpu_known_answers_and_formats():
+    """tetra_afc_gate (fused into the waterfall kernel) on the KATs, one batch: statistics within
+    GATE_DB_TOL of the oracle, decisions / peak bins / AFC offsets identical; SC16 input (the
+    capture's wire format) and complex128 give the same decisions; fewer than 2048 samples: no
+    detection."""
+    from tetraear.signal.spectrum import afc_gate
+    x = np.stack([_comb(*args, seed=i) for i, (args, _, _) in enumerate(GATE_KATS)])
+    got = afc_gate(x, GATE_FS, power=True, mixer=True)
+    for i, (args, present, why) in enumerate(GATE_KATS):
+        want = _gate_vs_oracle(got, x[i], GATE_FS, i)
+        assert bool(got["present"][i]) == present, why
+        f = want["afc"]
+        assert got["mixer_on"][i] == (f != 0) and got["mixer_coef"][i] == (-2 * np.pi * f if f else 0.0)
+    ref = np.stack([S.frame_power(v) for v in x])
+    near = ref >= ref.max(axis=1, keepdims=True) - 80.0   # the fused row is the waterfall's (tolerances above)
+    assert np.abs(got["power"] - ref)[near].max() < 0.05
+    sc = np.stack([np.rint(x.real * 32768), np.rint(x.imag * 32768)], -1).clip(-32768, 32767).astype(np.int16)
+    g16 = afc_gate(sc, GATE_FS)
+    big = [i for i, (a, _, _) in enumerate(GATE_KATS) if a[0] >= 1e-3]   # the SC16 grid (3e-5) hides the weak ones
+    assert np.array_equal(g16["present"][big], got["present"][big])
+    g64 = afc_gate(x.astype(np.complex128), GATE_FS)
+    assert np.array_equal(g64["present"], got["present"]) and np.array_equal(g64["peak_bin"], got["peak_bin"])
+    short = afc_gate(x[:, :2047], GATE_FS, mixer=True)
+    assert not short["valid"].any() and not short["present"].any() and not short["mixer_on"].any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fs", [1.8e6, 2.4e6])
+def test_gate_gpu_tetra_chunks_vs_oracle(fs):
+    """The gate on TETRA-like chunks (the ETSI synthesiser's pi/4-DQPSK bursts, CFO up to 600 Hz,
+    Es/N0 10-25 dB, and pure-noise channels): GPU equals the oracle (tolerance above) channel by
+    channel at both ends of the reference's rate range."""
+    from tetraear.signal.etsi import synth
+    from tetraear.signal.spectrum import afc_gate
+    N = 2 * int(131072 * fs / 2.4e6 / 2)
+    xs = [synth(4, N, fs=fs, seed=s, snr_db=snr)[0] for s, snr in ((1, 25.0), (2, 10.0))]
+    rng = np.random.default_rng(9)
+    noise = (1e-3 * (rng.standard_normal((2, N)) + 1j * rng.standard_normal((2, N)))).astype(np.complex64)
+    x = np.concatenate(xs + [noise])
+    got = afc_gate(x, fs)
+    npres = 0
+    for i in range(len(x)):
+        npres += _gate_vs_oracle(got, x[i], fs, i)["present"]
+    assert not got["present"][-2:].any()   # noise alone: never present
+
+
+@pytest.mark.gpu
+def test_process_batch_afc_feeds_the_demod_on_device():
+    """SignalProcessor.process_batch(x, 'afc'): the gate's offsets go to the compat demod as device
+    arrays.  Every channel equals process(x[c], freq_offset = the gate's AFC offset) -- what the
+    capture loop does per chunk (modern.py:2028-2029) -- and a device tensor of offsets gives the
+    same rows as the host array."""
+    import torch
+    from tetraear.signal import SignalProcessor
+    offs = [0, 3, -5, 7]
+    x = np.stack([_comb(0.01, 4, 1024 + k, 1e-4, seed=k + 20) for k in offs])
+    p = SignalProcessor(GATE_FS, mode="compat")
+    hard, soft, ns = p.process_batch(x, "afc")
+    assert np.array_equal(p.gate["afc"], np.array(offs) * BIN_HZ) and p.gate["present"].all()
+    for c in range(len(x)):
+        h = p.process(x[c], freq_offset=float(p.gate["afc"][c]))
+        n = int(ns[c])
+        assert np.array_equal(hard[c, :n - 1], h), c
+    fo = torch.tensor(np.array(offs) * BIN_HZ, dtype=torch.float64, device="cuda")
+    h2, s2, n2 = p.process_batch(x, fo)
+    h3, s3, n3 = p.process_batch(x, np.array(offs) * BIN_HZ)
+    assert np.array_equal(h2, hard) and np.array_equal(s2, soft) and np.array_equal(h3, hard) and np.array_equal(n3, ns)

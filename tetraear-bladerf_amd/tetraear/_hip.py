@@ -119,6 +119,7 @@ def _bind(L):
         "tetra_resample": (_i32, [_vp, _vp, _i32, _sz, _sz, _sz, _vp]),
         "tetra_waterfall": (_i32, [_vp, _vp, _i32, _sz, _sz, _sz, _sz, _sz, _vp]),
         "tetra_afc_gate": (_i32, [_vp, _vp, _i32, _sz, _sz, ctypes.c_double, _vp, _vp, _vp, _vp]),
+        "tetra_scan_detect": (_i32, [_vp, _vp, _i32, _sz, _sz, _i32, ctypes.c_uint32, _vp]),
         "tetra_channelize": (_i32, [_vp, ctypes.POINTER(WbPlan), _vp, _sz, _vp, _sz]),
         "tetra_synth_wideband": (_i32, [_vp, ctypes.POINTER(WbPlan), _sz, ctypes.c_uint64, ctypes.c_float,
                                         ctypes.c_float, _vp, _vp, _vp, _vp, _vp]),

@@ -21,8 +21,8 @@ if [ -n "$PROFILE" ]; then bash tools/profile_bench.sh $PROFILE; fi
 if [ -n "$PROFILE_SC16" ]; then bash tools/profile_bench.sh $PROFILE_SC16 --iq sc16; fi
 # AB="libA.so libB.so": same-box A/B of library variants, pipelined and serial cf32, pipelined SC16
 if [ -n "$AB" ]; then
-  AB_ARGS=" " bash tools/ab_demod.sh $AB > $O/ab_pipe.txt 2>&1
-  if [ -n "$AB_SERIAL" ]; then AB_ARGS="--pipeline off" bash tools/ab_demod.sh $AB > $O/ab_serial.txt 2>&1; fi
-  AB_ARGS="--iq sc16" bash tools/ab_demod.sh $AB > $O/ab_sc16.txt 2>&1
+  AB_ARGS=" " bash tools/ab.sh run $AB > $O/ab_pipe.txt 2>&1
+  if [ -n "$AB_SERIAL" ]; then AB_ARGS="--pipeline off" bash tools/ab.sh run $AB > $O/ab_serial.txt 2>&1; fi
+  AB_ARGS="--iq sc16" bash tools/ab.sh run $AB > $O/ab_sc16.txt 2>&1
 fi
 echo done
