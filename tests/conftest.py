@@ -42,9 +42,18 @@ def g3():
     return np.load(os.path.join(GOLDEN, "g3_burst.npz"))
 
 
+# What the build's decode() frames do NOT carry (the reference's upper MAC, decoder.py:1055-1117,
+# out of scope per SURVEY.md §2; TetraDecoder.upper_mac is the hook): frame keys recorded in the
+# golden g2 records as 'upper_keys', and additional_info entries beyond the MAC PDU stage's.
+UPPER_MAC_KEYS = {"call_metadata", "sds_message", "decoded_text", "is_reassembled"}
+UPPER_MAC_INFO = {"talkgroup", "source_ssi", "sds_text", "mcc", "mnc"}   # call metadata: decoder.py:1062-1080
+
+
 def decoded_view(frame):
     """The fields of one decode() frame dict the golden g2 'decoded' records compare on: the
-    lower-MAC fields and the MAC PDU stage (decoder.py:960-1053)."""
+    lower-MAC fields and the MAC PDU stage (decoder.py:960-1053).  The upper-MAC keys
+    (UPPER_MAC_KEYS, UPPER_MAC_INFO) are excluded by declaration: test_g2_upper_mac_gap_declared
+    checks the recorded reference frames hold no other keys."""
     info = frame.get("additional_info", {})
     mp = frame.get("mac_pdu")
     if mp is not None and not isinstance(mp.get("data"), str):

@@ -83,6 +83,26 @@ def test_g2_decode_mac_stage(g2):
     assert kept > 100 and dropped > 10
 
 
+def test_g2_upper_mac_gap_declared(g2):
+    """The gap between the build's decode() frames and the reference's is exactly the upper MAC
+    (decoder.py:1055-1117; TetraDecoder.upper_mac): every recorded reference frame's keys are the
+    ones decoded_view compares plus frame-dict constants, its 'upper_keys' lie in UPPER_MAC_KEYS and
+    its additional_info beyond the description / encryption_mode in UPPER_MAC_INFO.  A reference
+    field outside these sets would fail here instead of going unnoticed."""
+    from conftest import UPPER_MAC_KEYS, UPPER_MAC_INFO
+    _, recs = g2
+    base = {"number", "timeslot", "type", "header", "position", "burst_crc", "encrypted", "encryption_algorithm",
+            "additional_info", "mac_pdu", "upper_keys"}
+    seen_upper, seen_info = set(), set()
+    for r in recs:
+        for d in r["decoded"]:
+            assert set(d) <= base, set(d) - base
+            seen_upper |= set(d["upper_keys"])
+            seen_info |= set(d["additional_info"]) - {"description", "encryption_mode"}
+    assert seen_upper <= UPPER_MAC_KEYS and seen_info <= UPPER_MAC_INFO, (seen_upper, seen_info)
+    assert seen_upper and seen_info   # the recorded streams do exercise the upper MAC
+
+
 def test_g3_crc_and_bursts(g3):
     z = g3
     assert int("".join(map(str, z["kat_crc"])), 2) == 0x29B1

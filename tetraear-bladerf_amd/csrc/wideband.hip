@@ -19,6 +19,8 @@
 // Bytes: the analysis reads 8 B per wideband sample (the fold's P = 2 re-reads come from L2),
 // writes/reads Y once (8 B x M per D input samples = 32 B per input sample at D = 200 -- the FFT
 // stage dominates), and the resampler writes 8 B per 72 kHz output.
+#include <cstdlib>
+
 #include "common.h"
 
 
@@ -283,6 +285,189 @@ __global__ __launch_bounds__(AN_T) void k_pfb_analysis(const float4 *__restrict_
         }
         // block j + 1's stage 1 writes the other frame; its stage 2 (after the next barrier) is the
         // first to touch this one again
+    }
+}
+
+// Two blocks per iteration (k_pfb_analysis's next step): blocks j and j + 1 go through
+// the stages together, so one iteration's three barriers and LDS round trips serve 2 x 800 outputs,
+// and more of the workgroup works in each stage: five compute waves (stage 1: 200 butterflies, stage
+// 2: 400, stages 3 and 4: 320 each) and one loader wave.  Per block the operations are
+// k_pfb_analysis's, in the same order, so Y is bit-identical.  The loader writes the next pair's
+// 2 D new samples into the ring during stage 2 (after every stage-1 read of the pair's windows), so
+// the ring holds one pair's windows, L + D samples.
+constexpr int A2_C = 320, A2_T = A2_C + 64, A2_AF = 3;   // compute threads, + loader wave; pairs ahead
+
+template <int P>
+__global__ __launch_bounds__(A2_T, 5) void k_pfb_analysis2(const float4 *__restrict__ x2, int nblk, int JB,
+                                                        const float *__restrict__ h, const float2 *__restrict__ twg,
+                                                        float2 *__restrict__ Y) {
+    constexpr int M = AN_M, D = M / 4, L = P * M;
+    constexpr int RING = L + D <= 2048 ? 2048 : (L + D <= 4096 ? 4096 : 8192);   // samples, power of 2 (>= one pair's windows)
+    __shared__ float4 ring4[RING / 2];
+    __shared__ float2 frb[2][2][AN_FR];   // [block of the pair][ping-pong]
+    __shared__ float2 tw[AN_TWN];
+    const float2 *ring = reinterpret_cast<const float2 *>(ring4);
+    const int t = threadIdx.x;
+    const int j0 = blockIdx.x * JB, j1 = min(nblk, j0 + JB);
+    const int npair = (j1 - j0 + 1) / 2;
+    for (int i = t; i < AN_TWN; i += A2_T) tw[i] = twg[i];
+    // the first pair's windows x[j0 D, j0 D + L + D) (pairs of samples: j0 D is even), within the
+    // capture: its last block's window ends at sample L - 1 + (nblk - 1) D
+    const long npr = (long)(L + (long)(nblk - 1) * D) / 2;   // pairs of samples any block reads
+    for (int q = t; q < (L + D) / 2; q += A2_T) {
+        const long pr = (long)j0 * (D / 2) + q;
+        if (pr < npr) ring4[(int)(pr & (RING / 2 - 1))] = x2[pr];
+    }
+    if (t >= A2_C) {
+        // loader: pair i (blocks j0 + 2i, +1) adds the samples x[L + (j0 + 2i - 1) D, L + (j0 + 2i + 1) D)
+        // beyond the previous pair's windows: D pairs of samples from newbase(i); lane l carries pairs
+        // l + 64 m (< D), loaded A2_AF pairs ahead and written into the ring during the stage 2 before
+        const int l = t - A2_C;
+        auto newbase = [&](int i) -> long { return (long)(L + (long)(j0 + 2 * i - 1) * D) / 2; };
+        // loads through a buffer resource over the capture: one 32-bit lane offset, the pair's start
+        // as the wave-uniform soffset, and the range check returning 0 past the capture (no clamps,
+        // no 64-bit addresses held across the prefetch: those spilled)
+        const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float4 *>(x2), 0, (int)(16 * npr),
+                                                                            0x00020000);
+        const int vo = 16 * (int)(newbase(0) + l);
+        auto ld = [&](int i, int m) -> float4 {
+            const nt_f4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024 * m, 16 * D * i, 0);
+            return make_float4(v.x, v.y, v.z, v.w);
+        };
+        static_assert(A2_AF == 3, "loader unroll");
+        // slot s holds pair i + 1's samples when pair i (i mod 3 = s) is transformed (named registers:
+        // an array indexed inside the macro went to scratch)
+#define A2_FETCH(A, B, C, E, I)                                                                    \
+        A = ld((I), 0); B = ld((I), 1); C = ld((I), 2); E = ld((I), 3);
+        float4 r0a, r0b, r0c, r0d, r1a, r1b, r1c, r1d, r2a, r2b, r2c, r2d;
+        A2_FETCH(r0a, r0b, r0c, r0d, 1)
+        A2_FETCH(r1a, r1b, r1c, r1d, 2)
+        A2_FETCH(r2a, r2b, r2c, r2d, 3)
+        __syncthreads();
+#define A2_LOAD_PAIR(I, A, B, C, E)                                                                \
+        {                                                                                          \
+            const int ii = (I);                                                                    \
+            __syncthreads(); /* after stage 1 of pair ii: its windows have been read */            \
+            if (ii + 1 < npair) {                                                                  \
+                const long b = newbase(ii + 1) + l;                                                \
+                ring4[(int)(b & (RING / 2 - 1))] = A;                                              \
+                ring4[(int)((b + 64) & (RING / 2 - 1))] = B;                                       \
+                ring4[(int)((b + 128) & (RING / 2 - 1))] = C;                                      \
+                if (l + 192 < D) ring4[(int)((b + 192) & (RING / 2 - 1))] = E;                     \
+            }                                                                                      \
+            A2_FETCH(A, B, C, E, ii + 1 + A2_AF)                                                   \
+            __syncthreads(); /* after stage 2 */                                                   \
+            __syncthreads(); /* after stage 3 */                                                   \
+        }
+        static_assert(D > 128 && D <= 256, "four loads per lane cover D pairs");
+        int i = 0;
+        for (; i + 3 <= npair; i += 3) {
+            A2_LOAD_PAIR(i, r0a, r0b, r0c, r0d)
+            A2_LOAD_PAIR(i + 1, r1a, r1b, r1c, r1d)
+            A2_LOAD_PAIR(i + 2, r2a, r2b, r2c, r2d)
+        }
+        if (i < npair) A2_LOAD_PAIR(i, r0a, r0b, r0c, r0d)
+        if (i + 1 < npair) A2_LOAD_PAIR(i + 1, r1a, r1b, r1c, r1d)
+#undef A2_FETCH
+#undef A2_LOAD_PAIR
+        return;
+    }
+    // stage-1 thread: block bb of the pair, butterfly tt on u[tt + 100 r]
+    const int bb = t / 100, tt = t - 100 * bb;
+    float hr[8][P];
+    if (t < 200) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+#pragma unroll
+            for (int p = 0; p < P; ++p) hr[r][p] = h[p * M + tt + 100 * r];
+    }
+    __syncthreads();
+    for (int i = 0; i < npair; ++i) {
+        const int ja = j0 + 2 * i;
+        const int ph = i & 1;
+        // stage 1 (R = 8, Ns = 1)
+        if (t < 200) {
+            const long nj = (long)L - 1 + (long)(ja + bb) * D;
+            float2 v[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int ii = tt + 100 * r;
+                float ar = 0.f, ai = 0.f;
+#pragma unroll
+                for (int p = 0; p < P; ++p) {
+                    const float2 xv = ring[(int)((nj - p * M - ii) & (RING - 1))];
+                    ar = fmaf(hr[r][p], xv.x, ar);
+                    ai = fmaf(hr[r][p], xv.y, ai);
+                }
+                v[r] = make_float2(ar, ai);
+            }
+            bdft8(v);
+            float2 *fa = frb[bb][ph];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) fa[an_pad(8 * tt + r)] = v[r];
+        }
+        __syncthreads();
+        // stage 2 (R = 4, Ns = 8): 2 x 200 butterflies on 320 threads, fa -> fb
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+            const int g = t + A2_C * h2;
+            if (g < 400) {
+                const int b2 = g / 200, b = g - 200 * b2;
+                const float2 *fa = frb[b2][ph];
+                float2 *fb = frb[b2][ph ^ 1];
+                float2 v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = fa[an_pad(b + 200 * r)];
+                const int m = b & 7;
+#pragma unroll
+                for (int r = 1; r < 4; ++r) v[r] = c_mul(v[r], tw[AN_TW2 + (r - 1) * 8 + m]);
+                bdft4(v[0], v[1], v[2], v[3]);
+                const int base = (b >> 3) * 32 + m;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) fb[an_pad(base + 8 * r)] = v[r];
+            }
+        }
+        __syncthreads();
+        // stage 3 (R = 5, Ns = 32): 2 x 160 butterflies, fb -> fa
+        const int b3 = t / 160, u3 = t - 160 * b3;
+        {
+            const float2 *fb = frb[b3][ph ^ 1];
+            float2 *fa = frb[b3][ph];
+            float2 v[5];
+#pragma unroll
+            for (int r = 0; r < 5; ++r) v[r] = fb[an_pad(u3 + 160 * r)];
+            const int m = u3 & 31;
+#pragma unroll
+            for (int r = 1; r < 5; ++r) v[r] = c_mul(v[r], tw[AN_TW3 + (r - 1) * 32 + m]);
+            bdft5(v);
+            const int base = (u3 >> 5) * 160 + m;
+#pragma unroll
+            for (int r = 0; r < 5; ++r) fa[an_pad(base + 32 * r)] = v[r];
+        }
+        __syncthreads();
+        // stage 4 (R = 5, Ns = 160): outputs k = u3 + 160 r of block ja + b3, natural order, to HBM
+        const int j = ja + b3;
+        if (j < j1) {
+            const float2 *fa = frb[b3][ph];
+            float2 v[5];
+#pragma unroll
+            for (int r = 0; r < 5; ++r) v[r] = fa[an_pad(u3 + 160 * r)];
+#pragma unroll
+            for (int r = 1; r < 5; ++r) v[r] = c_mul(v[r], tw[AN_TW4 + (r - 1) * 160 + u3]);
+            bdft5(v);
+            const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(Y + (size_t)j * M, 0, 8 * M, 0x00020000);
+#pragma unroll
+            for (int r = 0; r < 5; ++r) {
+                const int k = u3 + 160 * r, q = (k * (j & 3)) & 3;
+                const float a = (q & 1) ? v[r].y : v[r].x, b4 = (q & 1) ? -v[r].x : v[r].y;
+                typedef unsigned u2v __attribute__((ext_vector_type(2)));
+                const float2 o = (q & 2) ? make_float2(-a, -b4) : make_float2(a, b4);
+                __builtin_amdgcn_raw_buffer_store_b64(u2v{__float_as_uint(o.x), __float_as_uint(o.y)}, yr, 8 * k, 0,
+                                                      2 /* nt */);
+            }
+        }
+        // the next pair's stage 1 writes frames [.][ph ^ 1]; its stage 2 (after the next barrier) is
+        // the first to touch frames [.][ph] again
     }
 }
 
@@ -569,12 +754,27 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
         PROF(ctx, "wb_analysis");
         // one round of workgroups (four per CU at <= 53 KB LDS) when the capture allows, >= 16
         // blocks each (the L-sample window each workgroup loads first is its overhead)
-        const int jb = std::max<int>(16, (int)((nblk + 4 * 256 - 1) / (4 * 256)));
-        const unsigned grid = (unsigned)((nblk + jb - 1) / jb);
-        switch (P->P) {
+        // k_pfb_analysis2 addresses the capture with 32-bit byte offsets; TETRA_WB_ANALYSIS=1 keeps the
+        // one-block kernel (same-box A/B)
+        static const bool one_block_env = getenv("TETRA_WB_ANALYSIS") && atoi(getenv("TETRA_WB_ANALYSIS")) == 1;
+        if (one_block_env || Nw * 8 >= (size_t)1 << 31) {
+            const int jb = std::max<int>(16, (int)((nblk + 4 * 256 - 1) / (4 * 256)));
+            const unsigned grid = (unsigned)((nblk + jb - 1) / jb);
+            switch (P->P) {
 #define AN(PP) case PP: hipLaunchKernelGGL(k_pfb_analysis<PP>, dim3(grid), dim3(AN_T), 0, ctx->stream, (const float4 *)xd, (int)nblk, jb, taps, (const float2 *)(taps + tw_off), u); break;
-            AN(1) AN(2) AN(3) AN(4)
+                AN(1) AN(2) AN(3) AN(4)
 #undef AN
+            }
+        } else {
+            // three 384-thread workgroups per CU (51 KB of LDS each); an even number of >= 16 blocks each
+            int jb = std::max<int>(16, (int)((nblk + 3 * 256 - 1) / (3 * 256)));
+            jb += jb & 1;
+            const unsigned grid = (unsigned)((nblk + jb - 1) / jb);
+            switch (P->P) {
+#define AN(PP) case PP: hipLaunchKernelGGL(k_pfb_analysis2<PP>, dim3(grid), dim3(A2_T), 0, ctx->stream, (const float4 *)xd, (int)nblk, jb, taps, (const float2 *)(taps + tw_off), u); break;
+                AN(1) AN(2) AN(3) AN(4)
+#undef AN
+            }
         }
         HIP_TRY(ctx, hipGetLastError());
     } else {

@@ -5,8 +5,10 @@ Mirrors the hot-path methods of /root/reference/tetraear/core/decoder.py:
 Correlation, the greedy sync scan, burst slicing, burst typing and CRC run on the GPU
 (tetra_lmac_compat / tetra_find_sync / tetra_symbols_to_bits).  The Python here keeps the
 reference's float decisions (threshold comparisons, the adaptive re-search rule) and builds the
-frame dicts.  Upper-MAC parsing, SDS and decryption (decoder.py:994-1117) are not part of this
-hot-path build: they stay the reference's Python and attach through ``upper_mac``.
+frame dicts, through decode_frame's MAC PDU stage (decoder.py:994-1053: parse_mac_pdu on the GPU,
+the drop rule, mac_pdu, the encryption fields).  Call metadata, SDS and decryption
+(decoder.py:1055-1117) are not part of this hot-path build: they stay the reference's Python and
+attach through ``upper_mac``.
 
 ``mode="etsi"`` (or ``TETRAEAR_DEMOD=etsi`` for callers that construct ``TetraDecoder()``
 unchanged) decodes ETSI channel coding (cell acquisition from the BSCH, descramble, deinterleave,
@@ -263,10 +265,15 @@ class TetraDecoder:
         """Hook for the reference's call metadata / SDS / decryption (decoder.py:1055-1117), called
         with every frame the MAC PDU stage keeps and its MacPDU (None when the slot has none).
 
-        This build stops at the MAC PDU and returns the frame unchanged; INTEGRATION.md shows how
-        the reference's own Python parsers attach here.  They cannot change which frames are kept:
-        the reference drops a frame only on an exception inside its MAC stage, and call metadata
-        and SDS only index the PDU's bytes within the lengths they check first."""
+        This build stops at the MAC PDU and returns the frame unchanged: its frames carry the
+        reference's lower-MAC and MAC PDU fields (number, header, burst_crc, encrypted,
+        encryption_algorithm, additional_info['encryption_mode'], mac_pdu) and NOT the upper-MAC
+        ones -- call_metadata, sds_message, decoded_text, is_reassembled, additional_info's
+        talkgroup / source_ssi / mcc / mnc / sds_text -- nor auto_decrypt's decryption (upper MAC
+        out of scope; tests/test_oracle_golden.py declares exactly these keys as the gap).  A hook
+        that runs the reference's parsers here restores them; to keep the reference's frame
+        selection it must also drop (return None) a frame whose CRC failed when one of those parsers
+        raises, as decoder.py:1097-1100 does.  INTEGRATION.md shows such a hook."""
         return frame
 
     def _etsi_frames(self, raw):
