@@ -5,29 +5,39 @@ The reference has no channeliser (it tunes the SDR to one carrier per capture,
 /root/reference/tetraear/ui/modern.py:1886-1887), so this float64 numpy restatement IS the
 specification of tetraear-bladerf_amd/csrc/wideband.hip:
 
-  analysis  u_j[r] = sum_p h[pM + r] x[n_j - pM - r],  n_j = L - 1 + jD   (L = MP, D = M/4)
+  analysis  u_j[r] = sum_p h[pM + r] x[n_j - pM - r],  n_j = L - 1 + jD   (L = MP, D = M/2 or M/4)
             Y_j[k] = sum_r u_j[r] exp(+2 pi i k r / M)
-            v_k[j] = (-i)^(k j mod 4) Y_j[k]
+            v_k[j] = exp(-2 pi i k j D / M) Y_j[k] = (-i)^(k j 4D/M mod 4) Y_j[k]
   resample  y_k[n] = sum_{q<Q} g[(down n mod up) + up q] v_k[floor(down n / up) + Q - 1 - q]
   synthesis x[n]   = sum_j D h[n - jD] W_j[n mod M],  W_j[r] = sum_k s_k[j] exp(+2 pi i k r / M)
 
 Parity: the GPU runs in fp32 with a rocFFT transform, so y is compared within a tolerance; the
 timing stage downstream of y is bit-exact against oracle/etsi.py on the GPU's own y.
 """
+import os
+
 import numpy as np
 from scipy import signal as _design
 
 from etsi import rrc
 
-FS_WB, M_WB, P_WB, UP, DOWN, LG = 20e6, 800, 2, 18, 25, 810
+FS_WB, M_WB = 20e6, 800
+# the filter bank's two designs (tetraear.signal.wideband.DESIGNS restates them for the product):
+#   oversample 2 -- D = M / 2, 50 kHz carriers, P = 5 branches (cut-off 25 kHz, Kaiser 8), resampler
+#                   36 / 25 with 828 taps; the default
+#   oversample 4 -- D = M / 4, 100 kHz carriers, P = 2 (cut-off 50 kHz, Kaiser 7), 18 / 25, 810 taps
+OVERSAMPLE = {2: (5, 25e3, 8.0, 36, 25, 828), 4: (2, 50e3, 7.0, 18, 25, 810)}
+DEFAULT_OVERSAMPLE = int(os.environ.get("TETRA_WB_OVERSAMPLE", "2"))
 
 
-def design(fs=FS_WB, M=M_WB):
-    D = M // 4
-    h = _design.firwin(M * P_WB, 2.0 * fs / M, fs=fs, window=("kaiser", 7.0)).astype(np.float32)
-    sps = fs / D * UP / 18000.0
-    g = rrc((np.arange(LG) - (LG - 1) / 2.0) / sps).astype(np.float32)
-    return dict(M=M, D=D, P=P_WB, up=UP, down=DOWN, Lg=LG, fs=fs, h=h, g=g)
+def design(fs=FS_WB, M=M_WB, oversample=None):
+    ov = DEFAULT_OVERSAMPLE if oversample is None else oversample
+    P, cut, beta, up, down, Lg = OVERSAMPLE[ov]
+    D = M // ov
+    h = _design.firwin(M * P, cut, fs=fs, window=("kaiser", beta)).astype(np.float32)
+    sps = fs / D * up / 18000.0
+    g = rrc((np.arange(Lg) - (Lg - 1) / 2.0) / sps).astype(np.float32)
+    return dict(M=M, D=D, P=P, up=up, down=down, Lg=Lg, fs=fs, h=h, g=g)
 
 
 def lengths(d, Nw):
@@ -52,7 +62,7 @@ def analysis(x, d):
         u += h[p * M + r][None, :] * x[nj[:, None] - p * M - r[None, :]]
     Y = np.fft.ifft(u, axis=1) * M
     k = np.arange(M)
-    q = (k[:, None] * np.arange(nblk)[None, :]) % 4
+    q = (k[:, None] * (np.arange(nblk) * (4 * D // M))[None, :]) % 4   # e^{-2 pi i k j D / M}
     return (-1j) ** q * Y.T
 
 

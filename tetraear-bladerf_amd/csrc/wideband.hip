@@ -292,17 +292,39 @@ __global__ __launch_bounds__(AN_T) void k_pfb_analysis(const float4 *__restrict_
 // the stages together, so one iteration's three barriers and LDS round trips serve 2 x 800 outputs,
 // and more of the workgroup works in each stage: five compute waves (stage 1: 200 butterflies, stage
 // 2: 400, stages 3 and 4: 320 each) and one loader wave.  Per block the operations are
-// k_pfb_analysis's, in the same order, so Y is bit-identical.  The loader writes the next pair's
-// 2 D new samples into the ring during stage 2 (after every stage-1 read of the pair's windows), so
-// the ring holds one pair's windows, L + D samples.
+// k_pfb_analysis's, in the same order.  The loader writes the next pair's 2 D new samples into the
+// ring during stage 2 (after every stage-1 read of the pair's windows), so the ring holds one pair's
+// windows, L + D samples.
+//   DM = 4 D / M: 1 (D = 200, 4x oversampled carriers at 100 kHz, mixer (-i)^{kj}) or 2 (D = 400,
+//   2x at 50 kHz, mixer (-1)^{kj}: half the blocks -- half the FFTs and half of Y -- for a prototype
+//   of P = 5 branches, since images now alias onto a carrier from 37.5 kHz instead of 87.5).
+//   A power-of-two ring is indexed by masks; the D = 400 ring (L + D = 4400) is 4608 samples,
+//   indexed by a per-block base and one conditional wrap per read.
 constexpr int A2_C = 320, A2_T = A2_C + 64, A2_AF = 3;   // compute threads, + loader wave; pairs ahead
 
-template <int P>
-__global__ __launch_bounds__(A2_T, 5) void k_pfb_analysis2(const float4 *__restrict__ x2, int nblk, int JB,
-                                                        const float *__restrict__ h, const float2 *__restrict__ twg,
-                                                        float2 *__restrict__ Y) {
-    constexpr int M = AN_M, D = M / 4, L = P * M;
-    constexpr int RING = L + D <= 2048 ? 2048 : (L + D <= 4096 ? 4096 : 8192);   // samples, power of 2 (>= one pair's windows)
+template <int P, int DM> struct A2Cfg {
+    static constexpr int M = AN_M, D = M * DM / 4, L = P * M;
+    static constexpr int RING = L + D <= 2048 ? 2048 : (L + D <= 4096 ? 4096 : ((L + D + 511) / 512) * 512);
+    static constexpr bool POW2 = (RING & (RING - 1)) == 0;
+    static constexpr int NLD = (D + 63) / 64;                 // loader float4 loads per lane per pair
+    static constexpr int WAVES = L + D <= 4096 ? 5 : 3;      // waves per SIMD the LDS allows
+};
+template <int R> __device__ __forceinline__ int rwrap(int i) {   // i in (-R, 2R) -> [0, R)
+    if constexpr ((R & (R - 1)) == 0) {
+        return i & (R - 1);
+    } else {
+        i = i < 0 ? i + R : i;
+        return i >= R ? i - R : i;
+    }
+}
+
+template <int P, int DM>
+__global__ __launch_bounds__(A2_T, (A2Cfg<P, DM>::WAVES)) void k_pfb_analysis2(const float4 *__restrict__ x2, int nblk,
+                                                                             int JB, const float *__restrict__ h,
+                                                                             const float2 *__restrict__ twg,
+                                                                             float2 *__restrict__ Y) {
+    using Cf = A2Cfg<P, DM>;
+    constexpr int M = Cf::M, D = Cf::D, L = Cf::L, RING = Cf::RING, NLD = Cf::NLD;
     __shared__ float4 ring4[RING / 2];
     __shared__ float2 frb[2][2][AN_FR];   // [block of the pair][ping-pong]
     __shared__ float2 tw[AN_TWN];
@@ -312,64 +334,60 @@ __global__ __launch_bounds__(A2_T, 5) void k_pfb_analysis2(const float4 *__restr
     const int npair = (j1 - j0 + 1) / 2;
     for (int i = t; i < AN_TWN; i += A2_T) tw[i] = twg[i];
     // the first pair's windows x[j0 D, j0 D + L + D) (pairs of samples: j0 D is even), within the
-    // capture: its last block's window ends at sample L - 1 + (nblk - 1) D
+    // capture: its last block's window ends at sample L - 1 + (nblk - 1) D.  Ring position of pair q:
+    // (pair index) mod RING / 2, the window's first pair at 0
     const long npr = (long)(L + (long)(nblk - 1) * D) / 2;   // pairs of samples any block reads
+    const long pr0 = (long)j0 * (D / 2);                      // ring pair 0
     for (int q = t; q < (L + D) / 2; q += A2_T) {
-        const long pr = (long)j0 * (D / 2) + q;
-        if (pr < npr) ring4[(int)(pr & (RING / 2 - 1))] = x2[pr];
+        if (pr0 + q < npr) ring4[q] = x2[pr0 + q];            // L + D <= RING: no wrap yet
     }
     if (t >= A2_C) {
         // loader: pair i (blocks j0 + 2i, +1) adds the samples x[L + (j0 + 2i - 1) D, L + (j0 + 2i + 1) D)
         // beyond the previous pair's windows: D pairs of samples from newbase(i); lane l carries pairs
         // l + 64 m (< D), loaded A2_AF pairs ahead and written into the ring during the stage 2 before
         const int l = t - A2_C;
-        auto newbase = [&](int i) -> long { return (long)(L + (long)(j0 + 2 * i - 1) * D) / 2; };
         // loads through a buffer resource over the capture: one 32-bit lane offset, the pair's start
         // as the wave-uniform soffset, and the range check returning 0 past the capture (no clamps,
         // no 64-bit addresses held across the prefetch: those spilled)
         const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float4 *>(x2), 0, (int)(16 * npr),
                                                                             0x00020000);
-        const int vo = 16 * (int)(newbase(0) + l);
-        auto ld = [&](int i, int m) -> float4 {
-            const nt_f4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024 * m, 16 * D * i, 0);
-            return make_float4(v.x, v.y, v.z, v.w);
+        const long nb0 = (long)(L + (long)(j0 - 1) * D) / 2;   // newbase(0)
+        const int vo = 16 * (int)(nb0 + l);
+        // ring pair position of newbase(i) + l: (L + D) / 2 - D + l + D i (mod RING / 2)
+        int rpos = rwrap<RING / 2>((L + D) / 2 - D + l + D);     // for pair 1
+        float4 sl[A2_AF][NLD];                                   // slot s: pair i + 1 while pair i (i mod AF = s) runs
+        auto fetch = [&](float4 (&v)[NLD], int i) __attribute__((always_inline)) {
+#pragma unroll
+            for (int m = 0; m < NLD; ++m) {
+                const nt_f4 w = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024 * m, 16 * D * i, 0);
+                v[m] = make_float4(w.x, w.y, w.z, w.w);
+            }
+        };
+        auto step = [&](float4 (&v)[NLD], int ii) __attribute__((always_inline)) {
+            __syncthreads();   // after stage 1 of pair ii: its windows have been read
+            if (ii + 1 < npair) {
+#pragma unroll
+                for (int m = 0; m < NLD; ++m)
+                    if (l + 64 * m < D) ring4[rwrap<RING / 2>(rpos + 64 * m)] = v[m];
+            }
+            rpos = rwrap<RING / 2>(rpos + D);
+            fetch(v, ii + 1 + A2_AF);
+            __syncthreads();   // after stage 2
+            __syncthreads();   // after stage 3
         };
         static_assert(A2_AF == 3, "loader unroll");
-        // slot s holds pair i + 1's samples when pair i (i mod 3 = s) is transformed (named registers:
-        // an array indexed inside the macro went to scratch)
-#define A2_FETCH(A, B, C, E, I)                                                                    \
-        A = ld((I), 0); B = ld((I), 1); C = ld((I), 2); E = ld((I), 3);
-        float4 r0a, r0b, r0c, r0d, r1a, r1b, r1c, r1d, r2a, r2b, r2c, r2d;
-        A2_FETCH(r0a, r0b, r0c, r0d, 1)
-        A2_FETCH(r1a, r1b, r1c, r1d, 2)
-        A2_FETCH(r2a, r2b, r2c, r2d, 3)
+        fetch(sl[0], 1);
+        fetch(sl[1], 2);
+        fetch(sl[2], 3);
         __syncthreads();
-#define A2_LOAD_PAIR(I, A, B, C, E)                                                                \
-        {                                                                                          \
-            const int ii = (I);                                                                    \
-            __syncthreads(); /* after stage 1 of pair ii: its windows have been read */            \
-            if (ii + 1 < npair) {                                                                  \
-                const long b = newbase(ii + 1) + l;                                                \
-                ring4[(int)(b & (RING / 2 - 1))] = A;                                              \
-                ring4[(int)((b + 64) & (RING / 2 - 1))] = B;                                       \
-                ring4[(int)((b + 128) & (RING / 2 - 1))] = C;                                      \
-                if (l + 192 < D) ring4[(int)((b + 192) & (RING / 2 - 1))] = E;                     \
-            }                                                                                      \
-            A2_FETCH(A, B, C, E, ii + 1 + A2_AF)                                                   \
-            __syncthreads(); /* after stage 2 */                                                   \
-            __syncthreads(); /* after stage 3 */                                                   \
-        }
-        static_assert(D > 128 && D <= 256, "four loads per lane cover D pairs");
         int i = 0;
         for (; i + 3 <= npair; i += 3) {
-            A2_LOAD_PAIR(i, r0a, r0b, r0c, r0d)
-            A2_LOAD_PAIR(i + 1, r1a, r1b, r1c, r1d)
-            A2_LOAD_PAIR(i + 2, r2a, r2b, r2c, r2d)
+            step(sl[0], i);
+            step(sl[1], i + 1);
+            step(sl[2], i + 2);
         }
-        if (i < npair) A2_LOAD_PAIR(i, r0a, r0b, r0c, r0d)
-        if (i + 1 < npair) A2_LOAD_PAIR(i + 1, r1a, r1b, r1c, r1d)
-#undef A2_FETCH
-#undef A2_LOAD_PAIR
+        if (i < npair) step(sl[0], i);
+        if (i + 1 < npair) step(sl[1], i + 1);
         return;
     }
     // stage-1 thread: block bb of the pair, butterfly tt on u[tt + 100 r]
@@ -382,20 +400,21 @@ __global__ __launch_bounds__(A2_T, 5) void k_pfb_analysis2(const float4 *__restr
             for (int p = 0; p < P; ++p) hr[r][p] = h[p * M + tt + 100 * r];
     }
     __syncthreads();
+    // ring position of sample n_j - tt of block j = ja + bb: the window's last sample, L - 1 + bb D
+    // at the first pair (ring sample 0 = x[j0 D]), + 2 D per pair
+    int rbase = rwrap<RING>(L - 1 + bb * D - tt);
     for (int i = 0; i < npair; ++i) {
         const int ja = j0 + 2 * i;
         const int ph = i & 1;
         // stage 1 (R = 8, Ns = 1)
         if (t < 200) {
-            const long nj = (long)L - 1 + (long)(ja + bb) * D;
             float2 v[8];
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
-                const int ii = tt + 100 * r;
                 float ar = 0.f, ai = 0.f;
 #pragma unroll
                 for (int p = 0; p < P; ++p) {
-                    const float2 xv = ring[(int)((nj - p * M - ii) & (RING - 1))];
+                    const float2 xv = ring[rwrap<RING>(rbase - p * M - 100 * r)];
                     ar = fmaf(hr[r][p], xv.x, ar);
                     ai = fmaf(hr[r][p], xv.y, ai);
                 }
@@ -406,6 +425,7 @@ __global__ __launch_bounds__(A2_T, 5) void k_pfb_analysis2(const float4 *__restr
 #pragma unroll
             for (int r = 0; r < 8; ++r) fa[an_pad(8 * tt + r)] = v[r];
         }
+        rbase = rwrap<RING>(rbase + 2 * D);
         __syncthreads();
         // stage 2 (R = 4, Ns = 8): 2 x 200 butterflies on 320 threads, fa -> fb
 #pragma unroll
@@ -456,9 +476,11 @@ __global__ __launch_bounds__(A2_T, 5) void k_pfb_analysis2(const float4 *__restr
             for (int r = 1; r < 5; ++r) v[r] = c_mul(v[r], tw[AN_TW4 + (r - 1) * 160 + u3]);
             bdft5(v);
             const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(Y + (size_t)j * M, 0, 8 * M, 0x00020000);
+            // the mixer term: v_k[j] = e^{-2 pi i k j D / M} Y_j[k] = (-i)^{(k j DM) mod 4} Y_j[k]
+            const int jq = (j * DM) & 3;
 #pragma unroll
             for (int r = 0; r < 5; ++r) {
-                const int k = u3 + 160 * r, q = (k * (j & 3)) & 3;
+                const int k = u3 + 160 * r, q = (k * jq) & 3;
                 const float a = (q & 1) ? v[r].y : v[r].x, b4 = (q & 1) ? -v[r].x : v[r].y;
                 typedef unsigned u2v __attribute__((ext_vector_type(2)));
                 const float2 o = (q & 2) ? make_float2(-a, -b4) : make_float2(a, b4);
@@ -673,8 +695,8 @@ __global__ __launch_bounds__(256) void k_pfb_synth(const float2 *__restrict__ W,
 
 int wb_check(tetra_ctx *ctx, const tetra_wb_plan *P) {
     if (!P || !P->h || !P->g) return tetra_fail(ctx, TETRA_E_INVALID, "null wideband plan");
-    if (P->M <= 0 || P->D <= 0 || P->M != 4 * P->D || P->P < 1 || P->P > 8)
-        return tetra_fail(ctx, TETRA_E_INVALID, "wideband plan needs M = 4 D and 1 <= P <= 8");
+    if (P->M <= 0 || P->D <= 0 || (P->M != 4 * P->D && P->M != 2 * P->D) || P->P < 1 || P->P > 8)
+        return tetra_fail(ctx, TETRA_E_INVALID, "wideband plan needs M = 4 D or M = 2 D, and 1 <= P <= 8");
     if (P->up <= 0 || P->down <= 0 || P->Lg <= 0 || P->Lg % P->up)
         return tetra_fail(ctx, TETRA_E_INVALID, "resampler taps Lg must be a multiple of up");
     return TETRA_OK;
@@ -706,8 +728,12 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
     const float2 *xd = (const float2 *)st.in(x, Nw * 8);
     float2 *yd = (float2 *)st.out(y, (size_t)M * n_keep * 8);
     float2 *u = (float2 *)ws(ctx, S_W8, (size_t)nblk * M * 8);
-    if (Q != 45 || P->up > 32) return tetra_fail(ctx, TETRA_E_INVALID, "resampler built for Lg / up = 45 taps");
-    const bool fixed = P->up == 18 && P->down == 25;   // 100 kHz -> 72 kHz (the 20 MSps / 800 plan)
+    const int DM = 4 * P->D / M;   // 1: carriers at 4x, 2: at 2x the carrier spacing
+    if (Q != 45 && Q != 23) return tetra_fail(ctx, TETRA_E_INVALID, "resampler built for Lg / up = 45 or 23 taps");
+    if (P->up > RS_QP) return tetra_fail(ctx, TETRA_E_INVALID, "resampler up %d > %d", P->up, RS_QP);
+    // the compiled-in rate pairs: 100 kHz -> 72 kHz (D = M / 4) and 50 kHz -> 72 kHz (D = M / 2)
+    const bool fix18 = P->up == 18 && P->down == 25 && Q == 45, fix36 = P->up == 36 && P->down == 25 && Q == 23;
+    const bool fixed = fix18 || fix36;
     float *taps = (float *)ws(ctx, S_W9, (size_t)(L + P->up * RS_QP + P->Lg + 2 + 2 * AN_TWN) * 4);
     if (!xd || !yd || !u || !taps) return st.finish();
     // h, then g phase-major: gT[rho][q] = g[rho + up q] (zero-padded to RS_QP), then g as given
@@ -715,20 +741,29 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
     ctx->taps_wb.resize((size_t)L + P->up * RS_QP, 0.f);
     for (int rho = 0; rho < P->up; ++rho)
         for (int q = 0; q < Q; ++q) ctx->taps_wb[L + rho * RS_QP + q] = P->g[rho + P->up * q];
-    if (fixed) {   // k_pfb_resamp_fix's use-ordered table gU (see ResampUse)
-        constexpr ResampUse<18, 25, 45> use{};
+    // k_pfb_resamp_fix's use-ordered table gU (see ResampUse)
+    auto use_table = [&](const auto &use, int UPc, int DOWNc, int Qc, int ROWSc) {
         std::vector<float> gU((size_t)use.n);
-        for (int i = 0; i < ResampUse<18, 25, 45>::ROWS; ++i)
-            for (int o = 0; o < 18; ++o)
+        for (int i = 0; i < ROWSc; ++i)
+            for (int o = 0; o < UPc; ++o)
                 if (use.idx[i][o] >= 0) {
-                    const int lo = (25 * o) / 18, rho = (25 * o) % 18;
-                    gU[use.idx[i][o]] = P->g[rho + 18 * (lo + 45 - 1 - i)];
+                    const int lo = (DOWNc * o) / UPc, rho = (DOWNc * o) % UPc;
+                    gU[use.idx[i][o]] = P->g[rho + UPc * (lo + Qc - 1 - i)];
                 }
         ctx->taps_wb.insert(ctx->taps_wb.end(), gU.begin(), gU.end());
+    };
+    if (fix18) {
+        constexpr ResampUse<18, 25, 45> use{};
+        use_table(use, 18, 25, 45, ResampUse<18, 25, 45>::ROWS);
+    } else if (fix36) {
+        constexpr ResampUse<36, 25, 23> use{};
+        use_table(use, 36, 25, 23, ResampUse<36, 25, 23>::ROWS);
     } else {
         ctx->taps_wb.insert(ctx->taps_wb.end(), P->g, P->g + P->Lg);
     }
-    const bool fused = M == AN_M && P->P <= 4;   // fold + FFT in one pass (k_pfb_analysis)
+    // fold + FFT in one pass (k_pfb_analysis / k_pfb_analysis2); D = M / 2 only so
+    const bool fused = M == AN_M && ((DM == 1 && P->P <= 4) || (DM == 2 && P->P >= 4 && P->P <= 6));
+    if (!fused && DM != 1) return tetra_fail(ctx, TETRA_E_INVALID, "D = M / 2 needs M = 800 and 4 <= P <= 6");
     const size_t tw_off = ctx->taps_wb.size() + (ctx->taps_wb.size() & 1);   // float2-aligned
     if (fused) {   // backward twiddles e^{+2 pi i m r / (Ns R)}, r-major per stage
         ctx->taps_wb.resize(tw_off + 2 * AN_TWN, 0.f);
@@ -757,7 +792,9 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
         // k_pfb_analysis2 addresses the capture with 32-bit byte offsets; TETRA_WB_ANALYSIS=1 keeps the
         // one-block kernel (same-box A/B)
         static const bool one_block_env = getenv("TETRA_WB_ANALYSIS") && atoi(getenv("TETRA_WB_ANALYSIS")) == 1;
-        if (one_block_env || Nw * 8 >= (size_t)1 << 31) {
+        if (DM == 2 && Nw * 8 >= (size_t)1 << 31)
+            return tetra_fail(ctx, TETRA_E_INVALID, "D = M / 2 capture over 2 GiB: split it");
+        if (DM == 1 && (one_block_env || Nw * 8 >= (size_t)1 << 31)) {
             const int jb = std::max<int>(16, (int)((nblk + 4 * 256 - 1) / (4 * 256)));
             const unsigned grid = (unsigned)((nblk + jb - 1) / jb);
             switch (P->P) {
@@ -766,13 +803,16 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
 #undef AN
             }
         } else {
-            // three 384-thread workgroups per CU (51 KB of LDS each); an even number of >= 16 blocks each
-            int jb = std::max<int>(16, (int)((nblk + 3 * 256 - 1) / (3 * 256)));
+            // 384-thread workgroups: three per CU at D = M / 4 (51 KB of LDS), two at D = M / 2 (72 KB);
+            // an even number of >= 16 blocks each, about one round of workgroups
+            const int wpc = DM == 1 ? 3 : 2;
+            int jb = std::max<int>(16, (int)((nblk + wpc * 256 - 1) / (wpc * 256)));
             jb += jb & 1;
             const unsigned grid = (unsigned)((nblk + jb - 1) / jb);
-            switch (P->P) {
-#define AN(PP) case PP: hipLaunchKernelGGL(k_pfb_analysis2<PP>, dim3(grid), dim3(A2_T), 0, ctx->stream, (const float4 *)xd, (int)nblk, jb, taps, (const float2 *)(taps + tw_off), u); break;
-                AN(1) AN(2) AN(3) AN(4)
+            const int key = 10 * DM + P->P;
+            switch (key) {
+#define AN(PP, DD) case 10 * DD + PP: hipLaunchKernelGGL((k_pfb_analysis2<PP, DD>), dim3(grid), dim3(A2_T), 0, ctx->stream, (const float4 *)xd, (int)nblk, jb, taps, (const float2 *)(taps + tw_off), u); break;
+                AN(1, 1) AN(2, 1) AN(3, 1) AN(4, 1) AN(4, 2) AN(5, 2) AN(6, 2)
 #undef AN
             }
         }
@@ -795,13 +835,17 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
     }
     if (fixed) {
         PROF(ctx, "wb_resamp");
-        const dim3 gr((unsigned)((M + RS_C - 1) / RS_C), (unsigned)((n_keep + 4 * 18 - 1) / (4 * 18)));
-        if (fused)   // Y already carries the mixer rotation
-            hipLaunchKernelGGL((k_pfb_resamp_fix<18, 25, 45, false>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk,
-                               taps + L + P->up * RS_QP, yd, (int)n_keep);
+        const dim3 gr((unsigned)((M + RS_C - 1) / RS_C), (unsigned)((n_keep + 4 * P->up - 1) / (4 * P->up)));
+        const float *gu = taps + L + P->up * RS_QP;
+        if (fix36)   // D = M / 2: always the fused analysis, Y rotated there
+            hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk, gu,
+                               yd, (int)n_keep);
+        else if (fused)   // Y already carries the mixer rotation
+            hipLaunchKernelGGL((k_pfb_resamp_fix<18, 25, 45, false>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk, gu,
+                               yd, (int)n_keep);
         else
-            hipLaunchKernelGGL((k_pfb_resamp_fix<18, 25, 45, true>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk,
-                               taps + L + P->up * RS_QP, yd, (int)n_keep);
+            hipLaunchKernelGGL((k_pfb_resamp_fix<18, 25, 45, true>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk, gu,
+                               yd, (int)n_keep);
         HIP_TRY(ctx, hipGetLastError());
     } else {
         PROF(ctx, "wb_resamp");
@@ -809,12 +853,15 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
         const size_t lds = (size_t)std::max(rows * RS_C, RS_C * (RS_T + 1)) * 8;
         if (lds > 160 * 1024) return tetra_fail(ctx, TETRA_E_INVALID, "resampler tile does not fit LDS");
         const dim3 gr((unsigned)((M + RS_C - 1) / RS_C), (unsigned)((n_keep + RS_T - 1) / RS_T));
-        if (fused)
+        if (Q == 23)   // D = M / 2 (fused analysis: Y rotated)
+            hipLaunchKernelGGL((k_pfb_resamp<23, false>), gr, dim3(256), lds, ctx->stream, u, M, (int)nblk, P->up, P->down,
+                               taps + L, yd, (int)n_keep);
+        else if (fused)
             hipLaunchKernelGGL((k_pfb_resamp<45, false>), gr, dim3(256), lds, ctx->stream, u, M, (int)nblk, P->up, P->down,
-                           taps + L, yd, (int)n_keep);
+                               taps + L, yd, (int)n_keep);
         else
             hipLaunchKernelGGL((k_pfb_resamp<45, true>), gr, dim3(256), lds, ctx->stream, u, M, (int)nblk, P->up, P->down,
-                           taps + L, yd, (int)n_keep);
+                               taps + L, yd, (int)n_keep);
         HIP_TRY(ctx, hipGetLastError());
     }
     return st.finish();

@@ -11,6 +11,7 @@ moves arrays; oracle/wideband.py is the float64 specification the tests hold it 
 """
 import ctypes
 import functools
+import os
 
 import numpy as np
 from scipy import signal as _design
@@ -20,37 +21,50 @@ from tetraear.signal.etsi import etsi_plan, rrc
 
 FS_WB = 20e6
 M_WB = 800
-P_WB = 2            # prototype taps per polyphase branch (L = 1600)
-UP, DOWN = 18, 25   # 100 kHz -> 72 kHz
-LG = 810            # resampler taps at 1.8 MHz (8.1 symbols of RRC)
 M2_CHUNK = 3932     # 72 kHz samples per timing chunk (as a 128 Ki chunk at 2.4 MSps)
+# Two filter-bank designs (the carrier's output rate fs / D and what it implies):
+#   oversample 2 (default): D = M / 2 -> 50 kHz carriers.  A carrier's band aliases onto itself from
+#     37.5 kHz, so the prototype is 5 branches long (cut-off 25 kHz, Kaiser 8: 0.003 dB ripple over
+#     +-12.5 kHz, 74 dB down from 37.5 kHz); resampler 50 -> 72 kHz = 36 / 25 with 828 RRC taps (23 per
+#     output).  Half the blocks of oversample 4: half the FFTs, half the filter-bank output Y.
+#   oversample 4 (round 1-3): D = M / 4 -> 100 kHz carriers, 2 branches (cut-off 2 spacings, 72 dB
+#     down from 87.5 kHz), resampler 18 / 25 with 810 taps (45 per output).
+DESIGNS = {2: dict(P=5, cut=25e3, beta=8.0, up=36, down=25, Lg=828),
+           4: dict(P=2, cut=None, beta=7.0, up=18, down=25, Lg=810)}
+OVERSAMPLE = int(os.environ.get("TETRA_WB_OVERSAMPLE", "2"))   # 4: the round-3 design (A/B)
+# the default design's constants (module attributes the tests and the bench read)
+P_WB, UP, DOWN, LG = (DESIGNS[OVERSAMPLE][k] for k in ("P", "up", "down", "Lg"))
 
 
-@functools.lru_cache(maxsize=4)
-def wb_design(fs=FS_WB, M=M_WB):
-    """Prototype lowpass h [M P] (unity DC gain, cut-off 2 carrier spacings: flat over +-12.5 kHz,
-    72 dB down from 87.5 kHz, the first band that aliases onto a carrier at fs/D) and the
-    resampler RRC g [LG] at up * fs / D."""
-    D = M // 4
-    if abs(fs / D * UP / DOWN - 72000.0) > 1e-6:
-        raise ValueError("the channeliser is built for fs / (M / 4) = 100 kHz carriers (20 MSps, 800 carriers)")
-    h = _design.firwin(M * P_WB, 2.0 * fs / M, fs=fs, window=("kaiser", 7.0)).astype(np.float32)
-    sps = fs / D * UP / 18000.0
-    g = rrc((np.arange(LG) - (LG - 1) / 2.0) / sps).astype(np.float32)
+@functools.lru_cache(maxsize=8)
+def wb_design(fs=FS_WB, M=M_WB, oversample=None):
+    """Prototype lowpass h [M P] (unity DC gain, flat over +-12.5 kHz, and down >= 72 dB from the
+    first band that aliases onto a carrier at fs / D) and the resampler RRC g [Lg] at up * fs / D."""
+    ov = OVERSAMPLE if oversample is None else oversample
+    d = DESIGNS[ov]
+    D = M // ov
+    if abs(fs / D * d["up"] / d["down"] - 72000.0) > 1e-6:
+        raise ValueError(f"the channeliser is built for fs / (M / {ov}) = {72000.0 * d['down'] / d['up']:.0f} Hz carriers")
+    cut = d["cut"] if d["cut"] is not None else 2.0 * fs / M
+    h = _design.firwin(M * d["P"], cut, fs=fs, window=("kaiser", d["beta"])).astype(np.float32)
+    sps = fs / D * d["up"] / 18000.0
+    g = rrc((np.arange(d["Lg"]) - (d["Lg"] - 1) / 2.0) / sps).astype(np.float32)
     return h, g
 
 
 class WbPlan:
     """tetra_wb_plan plus the tap arrays it points at."""
 
-    def __init__(self, fs=FS_WB, M=M_WB):
-        self.h, self.g = wb_design(fs, M)
+    def __init__(self, fs=FS_WB, M=M_WB, oversample=None):
+        ov = OVERSAMPLE if oversample is None else oversample
+        d = DESIGNS[ov]
+        self.h, self.g = wb_design(fs, M, ov)
         p = _hip.WbPlan()
-        p.M, p.D, p.P, p.up, p.down, p.Lg, p.fs = M, M // 4, P_WB, UP, DOWN, LG, fs
+        p.M, p.D, p.P, p.up, p.down, p.Lg, p.fs = M, M // ov, d["P"], d["up"], d["down"], d["Lg"], fs
         p.h = self.h.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
         p.g = self.g.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
         self.c = p
-        self.M, self.D, self.fs = M, M // 4, fs
+        self.M, self.D, self.fs, self.oversample = M, M // ov, fs, ov
 
     def lengths(self, Nw):
         nb, n72 = ctypes.c_int64(), ctypes.c_int64()
@@ -58,9 +72,9 @@ class WbPlan:
         return nb.value, n72.value
 
 
-@functools.lru_cache(maxsize=4)
-def wb_plan(fs=FS_WB, M=M_WB):
-    return WbPlan(fs, M)
+@functools.lru_cache(maxsize=8)
+def wb_plan(fs=FS_WB, M=M_WB, oversample=None):
+    return WbPlan(fs, M, oversample)
 
 
 def chunking(plan, Nw, m2=M2_CHUNK):
@@ -228,8 +242,10 @@ class BenchStep:
         8 B symbol, 2 soft bits and a hard dibit.  bench.py reports the slowest of them."""
         M, D, fs = self.plan.M, self.plan.D, self.fs
         yb = 8.0 * M * 72000.0 / fs
+        ana = "k_pfb_analysis" if os.environ.get("TETRA_WB_ANALYSIS") == "1" and self.plan.oversample == 4 \
+            else "k_pfb_analysis2"
         return {"waterfall": (12.0 * self.nfr * 2048 / self.Nw, "k_waterfall"),
-                "wb_analysis": (8.0 + 8.0 * M / D, "k_pfb_analysis"),   # fused fold + FFT: x in, Y out
+                "wb_analysis": (8.0 + 8.0 * M / D, ana),   # fused fold + FFT: x in, Y out
                 "wb_fold": (8.0 + 8.0 * M / D, "k_pfb_fold"), "wb_fft": (2 * 8.0 * M / D, None),
                 "wb_resamp": (8.0 * M / D + yb, "k_pfb_resamp_fix"),
                 "etsi_timing": (yb + 11.0 * M * 18000.0 / fs, "k_timing")}
@@ -239,6 +255,7 @@ class BenchStep:
                             f"{self.plan.M} carriers x {self.nchunk} timing chunks of {self.m2}",
                 "wideband_samples_per_gpu": self.Nw, "sample_rate": self.fs, "carriers": self.plan.M,
                 "timing_chunks_per_carrier": self.nchunk, "parallelism": f"capture-sharded x{world}",
+                "filter_bank": f"D = M / {self.plan.oversample} ({self.fs / self.plan.D / 1e3:g} kHz carriers)",
                 "pipeline": self.pipelined}
 
     def realtime_channels(self, value_msps):
