@@ -928,3 +928,41 @@ def test_unsupported_rate_never_raises_into_the_loop(caplog):
     x = np.zeros((1, 131072), np.complex64)
     y = np.zeros((1, 8192), np.complex64)
     assert c.lib.tetra_etsi_chanfilt(c.handle, bad2, _hip.ptr(x), 1, 131072, _hip.ptr(y)) == -1
+
+
+def test_hard_symbol_decode_rate():
+    """TetraDecoder(mode='etsi').decode() on plain uint8 dibits (a caller that kept only process()'s
+    hard symbols, not their soft_bits) decodes with +-64 pseudo-soft bits: the Viterbi then runs on
+    hard decisions.  Measured against the soft-decision path on the same demodulated chunks: at 18 dB
+    Es/N0 both decode >= 97 % of the blocks; at 9 dB the hard path keeps a share of them but never beats
+    the soft one by more than noise, and every CRC-good block is a transmitted payload."""
+    from tetraear.signal.etsi import EtsiReceiver, synth
+    from tetraear.core.etsi import EtsiLowerMac
+    C = 48
+    rates = {}
+    for snr in (18.0, 9.0):
+        iq, cells, kinds, payload, t0 = synth(C, 131072, seed=int(snr) + 40, snr_db=snr)
+        hard, soft, sym, ns = EtsiReceiver().demod_batch(iq)
+        res = {}
+        for mode in ("soft", "hard"):
+            nblk = nok = 0
+            for ch in range(C):
+                n = int(ns[ch])
+                lm = EtsiLowerMac(*__import__("tetraear.core.etsi", fromlist=["cell_of"]).cell_of(int(cells[ch])))
+                frames = lm.decode(hard[ch, :n - 1], soft[ch, :2 * (n - 1)] if mode == "soft" else None)
+                sent = payload[ch].reshape(-1, 268)
+                for f in frames:
+                    for b in f["blocks"]:
+                        nblk += 1
+                        if b["crc_ok"]:
+                            nok += 1
+                            bits = np.pad(b["bits"], (0, 268 - len(b["bits"])))
+                            assert np.any(np.all(sent == bits[None, :], axis=1)), (snr, mode, ch)
+            res[mode] = (nok, nblk)
+        rates[snr] = res
+    for mode in ("soft", "hard"):
+        nok, nblk = rates[18.0][mode]
+        assert nblk >= 3 * C and nok / nblk >= 0.97, (mode, nok, nblk)
+    (sk, sn), (hk, hn) = rates[9.0]["soft"], rates[9.0]["hard"]
+    assert sn == hn and hk <= sk + 2 and hk / hn >= 0.3, rates[9.0]
+    print("decode rates (ok, blocks):", rates)

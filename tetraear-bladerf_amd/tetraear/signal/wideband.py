@@ -3,11 +3,12 @@
 The reference receives one carrier per capture: the BladeRF is tuned to it and 2.4 MSps IQ goes
 to SignalProcessor.process (/root/reference/tetraear/ui/modern.py:1886-1887, 2029).  The north
 star's "polyphase FIR channeliser" instead takes a 20 MSps capture holding 800 carriers at 25 kHz
-spacing and splits it on the device: a polyphase filter bank (libtetra_hip.so k_pfb_fold +
-rocFFT, D = M/4), then per carrier an RRC(0.35) matched-filter resampler 100 kHz -> 72 kHz
-(k_pfb_resamp), which is exactly the sample stream the ETSI timing stage takes (4 samples per
-symbol, tetra_etsi_timing), followed by the ETSI lower MAC.  This module designs the filters and
-moves arrays; oracle/wideband.py is the float64 specification the tests hold it to.
+spacing and splits it on the device: a polyphase filter bank (libtetra_hip.so k_pfb_analysis2: fold
++ 800-point FFT fused, two blocks per iteration; D = M / 2 by default, so every carrier comes out at
+50 kHz), then per carrier an RRC(0.35) matched-filter resampler to 72 kHz (k_pfb_resamp_fix), which
+is exactly the sample stream the ETSI timing stage takes (4 samples per symbol, tetra_etsi_timing),
+followed by the ETSI lower MAC.  This module designs the filters and moves arrays;
+oracle/wideband.py is the float64 specification the tests hold it to.
 """
 import ctypes
 import functools
