@@ -110,3 +110,38 @@ def test_rate_plans_match_host_design():
         rate_design(20e6)
     with pytest.raises(ValueError):
         E.design(20e6)
+
+
+def test_rate_design_invariants():
+    """Every rate from 0.1 to 5 MSps in 0.1 MHz steps either gets a plan inside the generic kernel's
+    limits (q1 <= 13, L1 <= 64, Lp <= 4096, < 254 taps per stage-2 output, 72 kHz out exactly,
+    fs1 >= 180 kHz unless q1 = 1) or raises ValueError -- never a plan the library would refuse."""
+    from tetraear.signal.etsi import rate_design
+    served = 0
+    for k in range(1, 51):
+        fs = k * 100e3
+        try:
+            q1, L1, up, down, Lp = rate_design(fs)
+        except ValueError:
+            continue
+        served += 1
+        assert 1 <= q1 <= 13 and 1 <= L1 <= 64 and Lp == 32 * down + 1 <= 4096 and (Lp - 1) // up + 2 < 254, fs
+        assert 72000 * q1 * down == int(fs) * up, fs
+        assert q1 == 1 or fs / q1 >= 180e3, fs
+    assert served >= 40
+
+
+@pytest.mark.parametrize("fs", [1.0e6, 500e3])
+def test_iq_round_trip_other_rates(fs):
+    """The oracle receiver at rates outside the GUI slider (1.0 MSps: q1 = 5, 9/25; 500 kSps: q1 = 2)."""
+    rng = np.random.default_rng(int(fs) // 1000 + 7)
+    cell = E.scramble_init(901, 77, 12)
+    bits, jobs = E.burst_stream(rng, 6, E.scramble_seq(cell))
+    rx = E.Receiver(fs)
+    n = int(round(131072 * fs / 2.4e6))
+    x = E.modulate(bits, n, fs=fs, t0=4.1, phase0=rng.uniform(0, 6.28), cfo=rng.uniform(-600, 600), snr_db=20.0,
+                   rng=rng)
+    sym, soft, hard, diag = rx.demod(x)
+    res = rx.lower_mac(soft, hard, cell)
+    sent = [tuple(t) for _, jj in jobs for _, t in jj]
+    assert len(res) >= 2 and all(ok and tuple(t1) in sent for _, _, dec in res for _, t1, ok in dec)
