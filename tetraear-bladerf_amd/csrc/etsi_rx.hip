@@ -134,6 +134,32 @@ __device__ __forceinline__ void interp_pair(const float2 *w, int w0, float t, fl
     mid = one(i - 2);
 }
 
+// interp_pair over a 1024-sample LDS ring holding y[n] at ring[n & 1023] (k_timing: the Gardner
+// window staged from global memory a block ahead); the same operations as interp_pair
+constexpr int TRING = 1024;
+__device__ __forceinline__ void interp_pair_ring(const float2 *w, float t, float2 &on, float2 &mid) {
+    const float K6 = 1.0f / 6.0f;
+    const float fi = floorf(t);
+    const int i = (int)fi;
+    const float f = t - fi;
+    const float fm1 = f - 1.0f, fm2 = f - 2.0f, fp1 = f + 1.0f;
+    const float cm = -(f * fm1 * fm2) * K6;
+    const float c0 = (fp1 * fm1 * fm2) * 0.5f;
+    const float c1 = -(fp1 * f * fm2) * 0.5f;
+    const float c2 = (fp1 * f * fm1) * K6;
+    auto one = [&](int j) -> float2 {
+        const float2 a = w[(j - 1) & (TRING - 1)], b = w[j & (TRING - 1)], c = w[(j + 1) & (TRING - 1)],
+                     d = w[(j + 2) & (TRING - 1)];
+        float r = cm * a.x, q = cm * a.y;
+        r = fmaf(c0, b.x, r); q = fmaf(c0, b.y, q);
+        r = fmaf(c1, c.x, r); q = fmaf(c1, c.y, q);
+        r = fmaf(c2, d.x, r); q = fmaf(c2, d.y, q);
+        return make_float2(r, q);
+    };
+    on = one(i);
+    mid = one(i - 2);
+}
+
 __device__ __forceinline__ float2 csqrt_p(float x, float y) {
     const float r = sqrtf(fmaf(x, x, y * y));
     if (r == 0.0f) return make_float2(0.f, 0.f);
@@ -181,10 +207,15 @@ __device__ __forceinline__ float om_part(const float2 *y, int M2, int w, int lan
     return s;
 }
 
-template <bool SPLIT = false>
+// RING (k_timing, y in global memory): the Gardner loop reads y from a 1024-sample LDS ring that is
+// filled a block ahead -- block b needs y[4 kb - 5, 4 kb + 260) (|delta| <= 1.5, the cubic window),
+// the ring holds [0, 320) before the loop and block b writes the 256 samples the previous block
+// loaded into registers, [320 + 256 (b - 1), 320 + 256 b), then loads the next 256: each block's
+// window reads wait on LDS, not on L2 / HBM.  Same interpolation arithmetic, same bits.
+template <bool SPLIT = false, bool RING = false>
 __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float gain, float soft_scale, float2 *sp,
                                                  float2 *dp, int smax, int lane, int *prog = nullptr,
-                                                 const float *om = nullptr) {
+                                                 const float *om = nullptr, float2 *ring = nullptr) {
     TrackOut o{0, 1.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     if (M2 < 16) {
         if constexpr (SPLIT) {
@@ -218,7 +249,24 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
     bool have_prev = false;
     float zr = 0.f, zi = 0.f, am = 0.f;   // CFO sums over this lane's d_j
     int rel = -1;   // SPLIT: progress not yet released (published after the next block's LDS reads)
+    float2 pre[4];   // RING: the next block's 256 samples in flight
+    auto ld = [&](int n) -> float2 { return n < M2 ? y[n] : make_float2(0.f, 0.f); };
+    if constexpr (RING) {
+#pragma unroll
+        for (int u = 0; u < 5; ++u) ring[64 * u + lane] = ld(64 * u + lane);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) pre[u] = ld(320 + 64 * u + lane);
+    }
     for (int kb = kstart;; kb += 64) {
+        if constexpr (RING) {
+            if (kb != kstart) {   // the previous block's loads: y[320 + 256 (b - 1) ...)
+                const int n0 = 320 + 4 * (kb - kstart) - 256;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) ring[(n0 + 64 * u + lane) & (TRING - 1)] = pre[u];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) pre[u] = ld(n0 + 256 + 64 * u + lane);
+            }
+        }
         const float off = base + delta;
         const float t = (float)(4 * (kb + lane)) + off;
         const bool valid = (t - 3.0f >= 0.0f) && (t + 2.0f <= (float)(M2 - 1)) && (S + lane < smax);
@@ -239,6 +287,8 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
             }
             if (rel >= 0 && lane == 0)   // the previous block's d_j: its stores completed before these reads
                 __hip_atomic_store(prog, rel, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if constexpr (RING) {
+            if (act) interp_pair_ring(ring, t, on, mid);
         } else {
             if (act) interp_pair(y, 0, t, on, mid);
         }
@@ -365,10 +415,11 @@ __device__ __forceinline__ void timing_decide(const TrackOut &o, const float2 *d
     }
 }
 
+template <bool RING = false>
 __device__ __forceinline__ void timing_wave(const float2 *y, int M2, float gain, float soft_scale, float2 *sp,
                                             float2 *dp, int8_t *sb, uint8_t *hp, int32_t *nsym_ch, float4 *diag_ch,
-                                            int smax, int lane) {
-    const TrackOut o = timing_track(y, M2, gain, soft_scale, sp, dp, smax, lane);
+                                            int smax, int lane, float2 *ring = nullptr) {
+    const TrackOut o = timing_track<false, RING>(y, M2, gain, soft_scale, sp, dp, smax, lane, nullptr, nullptr, ring);
     __threadfence_block();   // dp written by other lanes is read below
     timing_decide(o, dp, sb, hp, 0, 1, lane);
     if (lane == 0) {
@@ -377,14 +428,21 @@ __device__ __forceinline__ void timing_wave(const float2 *y, int M2, float gain,
     }
 }
 
+template <bool RING>
 __global__ __launch_bounds__(64) void k_timing(const float2 *__restrict__ yall, int M2, float gain, float soft_scale,
                                                float2 *__restrict__ sym, float2 *__restrict__ dscr,
                                                int8_t *__restrict__ softbits, uint8_t *__restrict__ hard,
                                                int32_t *__restrict__ nsym, int smax, float4 *__restrict__ diag) {
+    __shared__ float2 ring[RING ? TRING : 1];
     const int ch = blockIdx.x;
-    timing_wave(yall + (size_t)ch * M2, M2, gain, soft_scale, sym + (size_t)ch * smax, dscr + (size_t)ch * smax,
-                softbits + (size_t)ch * 2 * smax, hard + (size_t)ch * smax, nsym + ch, diag ? diag + ch : nullptr,
-                smax, threadIdx.x);
+    timing_wave<RING>(yall + (size_t)ch * M2, M2, gain, soft_scale, sym + (size_t)ch * smax, dscr + (size_t)ch * smax,
+                      softbits + (size_t)ch * 2 * smax, hard + (size_t)ch * smax, nsym + ch, diag ? diag + ch : nullptr,
+                      smax, threadIdx.x, ring);
+}
+// TETRA_TIMING_RING=0: the Gardner windows read straight from global memory (same-box A/B)
+static bool timing_ring() {
+    static const bool on = !(getenv("TETRA_TIMING_RING") && atoi(getenv("TETRA_TIMING_RING")) == 0);
+    return on;
 }
 
 // --------------------------------------------------------------------------- E1 channel filter
@@ -2147,7 +2205,7 @@ int tetra_etsi_timing(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *y, s
     if (!yd || !so || !sbo || !ho || !no || !dscr) return st.finish();
     {
         PROF(ctx, "etsi_timing");
-        hipLaunchKernelGGL(k_timing, dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yd, (int)M2, P->gain,
+        hipLaunchKernelGGL(timing_ring() ? k_timing<true> : k_timing<false>, dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yd, (int)M2, P->gain,
                            P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg);
     }
     return st.finish();
@@ -2196,7 +2254,7 @@ int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *i
     if (rc) return rc;
     {
         PROF(ctx, "etsi_timing");
-        hipLaunchKernelGGL(k_timing, dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yb, (int)M2, P->gain,
+        hipLaunchKernelGGL(timing_ring() ? k_timing<true> : k_timing<false>, dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yb, (int)M2, P->gain,
                            P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg);
     }
     return st.finish();
