@@ -33,12 +33,18 @@ def _sync_walk(D, before=40, after=80, rng=None):
 
 
 def _edge_count_mod(x):
-    """Differences within EDGE of the cluster test's edges (multiples of pi/4 +- pi/8, and +pi)."""
+    """Differences within EDGE of the cluster test's edges: the multiples of pi/4 +- pi/8, and the
+    wrap point +-pi, where (d + pi) % 2 pi - pi sends a difference one ulp below -pi to just under
+    +pi (no match) and one ulp above to -pi (a match).  Clipped captures hit that edge often: samples
+    pinned to the diagonals (+-1, +-1) differ by exactly -pi up to the last ulp of atan2."""
     x = np.asarray(x)
     x = x / (np.abs(x).max() + 1e-10)
-    d = O._wrap(np.diff(np.angle(x))).astype(np.float64)
+    d = np.diff(np.angle(x)).astype(np.float64)
+    w = O._wrap(np.diff(np.angle(x))).astype(np.float64)
     edges = np.pi / 8 + np.pi / 4 * np.arange(-8, 8)
-    return int((np.abs(d[:, None] - edges[None, :]).min(axis=1) < EDGE).sum())
+    near = (np.abs(w[:, None] - edges[None, :]).min(axis=1) < EDGE) | (np.abs(np.abs(w) - np.pi) < EDGE)
+    near |= np.abs(np.abs(d) - np.pi) < EDGE   # the raw difference at +-pi itself
+    return int(near.sum())
 
 
 # ----------------------------------------------------------------------------- CPU: oracle KATs

@@ -92,6 +92,22 @@ def test_channelize_vs_oracle(capture):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("oversample,form", [(2, "1"), (2, "2"), (4, "1"), (4, "2")])
+def test_channelize_every_analysis_form(oversample, form, monkeypatch):
+    """Both filter-bank designs (D = M / 2 and M / 4) through each analysis kernel the host can pick
+    (TETRA_WB_ANALYSIS: 1 one block per iteration, 2 two blocks), held to the oracle of that design;
+    a capture long enough for several blocks per workgroup and a ragged tail."""
+    from tetraear.signal.wideband import WidebandReceiver, synth_wideband
+    monkeypatch.setenv("TETRA_WB_ANALYSIS", form)
+    x = synth_wideband(400_037, seed=5, snr_db=20.0, oversample=oversample)[0]
+    d = W.design(oversample=oversample)
+    y = WidebandReceiver(oversample=oversample).channelize(x)
+    want = W.channelize(x.astype(np.complex128), d)
+    assert y.shape == want.shape
+    assert np.abs(y - want).max() <= Y_TOL * np.abs(want).max()
+
+
+@pytest.mark.gpu
 def test_wideband_timing_bit_exact(capture):
     """From y on the chain is the ETSI one: the GPU timing on the channeliser's own output equals
     oracle/etsi.py on the same y, carrier by carrier."""

@@ -134,9 +134,9 @@ __device__ __forceinline__ void interp_pair(const float2 *w, int w0, float t, fl
     mid = one(i - 2);
 }
 
-// interp_pair over a 1024-sample LDS ring holding y[n] at ring[n & 1023] (k_timing: the Gardner
+// interp_pair over a 512-sample LDS ring holding y[n] at ring[n & 511] (k_timing: the Gardner
 // window staged from global memory a block ahead); the same operations as interp_pair
-constexpr int TRING = 1024;
+constexpr int TRING = 512;
 __device__ __forceinline__ void interp_pair_ring(const float2 *w, float t, float2 &on, float2 &mid) {
     const float K6 = 1.0f / 6.0f;
     const float fi = floorf(t);
@@ -207,11 +207,12 @@ __device__ __forceinline__ float om_part(const float2 *y, int M2, int w, int lan
     return s;
 }
 
-// RING (k_timing, y in global memory): the Gardner loop reads y from a 1024-sample LDS ring that is
-// filled a block ahead -- block b needs y[4 kb - 5, 4 kb + 260) (|delta| <= 1.5, the cubic window),
-// the ring holds [0, 320) before the loop and block b writes the 256 samples the previous block
-// loaded into registers, [320 + 256 (b - 1), 320 + 256 b), then loads the next 256: each block's
-// window reads wait on LDS, not on L2 / HBM.  Same interpolation arithmetic, same bits.
+// RING (k_timing, y in global memory): the Gardner loop reads y from a 512-sample LDS ring (4 KB: eight
+// one-wave workgroups per SIMD still fit) filled a block ahead -- block b needs y[4 kb - 5, 4 kb + 260)
+// (|delta| <= 1.5, the cubic window), the ring holds [0, 320) before the loop, and block b first writes
+// the 256 samples the previous block loaded into registers, [320 + 256 (b - 1), 320 + 256 b) (over
+// [256 b - 448, 256 b - 192), which no later block reads), then loads the next 256: each block's window
+// reads wait on LDS, not on L2 / HBM.  Same interpolation arithmetic, same bits.
 template <bool SPLIT = false, bool RING = false>
 __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float gain, float soft_scale, float2 *sp,
                                                  float2 *dp, int smax, int lane, int *prog = nullptr,

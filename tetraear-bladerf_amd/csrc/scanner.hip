@@ -13,7 +13,8 @@
 // wrap ((d + pi) mod 2 pi - pi, Python-style remainder), the cluster distance test in float64 against
 // the float64 multiples of pi/4; complex128 -> float64 throughout.  atan2 is the device's (the host's
 // libm rounds its last ulp differently), so a difference within ~1e-6 rad of a decision edge may
-// land on the other side -- the parity tests count those edges (tests/test_scanner.py).
+// land on the other side -- the edges are the pi/8 boundaries and the wrap point +-pi, which clipped
+// captures (samples pinned to the diagonals) hit often; the parity tests count them (tests/test_scanner.py).
 #include "common.h"
 
 namespace {

@@ -493,6 +493,163 @@ __global__ __launch_bounds__(A2_T, (A2Cfg<P, DM>::WAVES)) void k_pfb_analysis2(c
     }
 }
 
+// One block per iteration at any D (k_pfb_analysis's structure -- waves 0-2 fold + transform +
+// store, wave 3 loads -- with analysis2's ring indexing and buffer-resource loader): the D = M / 2
+// filter bank's default analysis.  LDS: the 4608-sample ring (L + D = 4400 at P = 5), two frames
+// and the twiddles, 57 KB: two workgroups per CU.
+template <int P, int DM>
+__global__ __launch_bounds__(AN_T, 2) void k_pfb_analysis1(const float4 *__restrict__ x2, int nblk, int JB,
+                                                           const float *__restrict__ h,
+                                                           const float2 *__restrict__ twg, float2 *__restrict__ Y) {
+    using Cf = A2Cfg<P, DM>;
+    constexpr int M = Cf::M, D = Cf::D, L = Cf::L, RING = Cf::RING;
+    constexpr int NLD1 = (D / 2 + 63) / 64;   // loader float4 loads per lane per block
+    constexpr int AF1 = 4;                    // blocks ahead
+    __shared__ float4 ring4[RING / 2];
+    __shared__ float2 frb[2][AN_FR];
+    __shared__ float2 tw[AN_TWN];
+    const float2 *ring = reinterpret_cast<const float2 *>(ring4);
+    const int t = threadIdx.x;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int j0 = blockIdx.x * JB, j1 = min(nblk, j0 + JB);
+    const int nb = j1 - j0;
+    for (int i = t; i < AN_TWN; i += AN_T) tw[i] = twg[i];
+    const long npr = (long)(L + (long)(nblk - 1) * D) / 2;   // pairs of samples any block reads
+    const long pr0 = (long)j0 * (D / 2);                      // ring pair 0 = x[j0 D]
+    for (int q = t; q < L / 2; q += AN_T)                     // the first block's window
+        if (pr0 + q < npr) ring4[q] = x2[pr0 + q];
+    if (wv == 3) {
+        // block jj (>= 1) adds x[L + (j0 + jj - 1) D, + D): D / 2 pairs from relative pair
+        // (L + (jj - 1) D) / 2; written during block jj - 1's stage 1 (disjoint from its window)
+        const int l = t - 192;
+        const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float4 *>(x2), 0, (int)(16 * npr),
+                                                                            0x00020000);
+        const int vo = 16 * (int)(pr0 + (L - D) / 2 + l);     // block jj's pairs at soffset 8 D jj
+        int rpos = rwrap<RING / 2>(L / 2 + l);                 // ring pair position for block 1
+        float4 sl[AF1][NLD1];
+        auto fetch = [&](float4 (&v)[NLD1], int jj) __attribute__((always_inline)) {
+#pragma unroll
+            for (int m = 0; m < NLD1; ++m) {
+                const nt_f4 w = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024 * m, 8 * D * jj, 0);
+                v[m] = make_float4(w.x, w.y, w.z, w.w);
+            }
+        };
+        auto step = [&](float4 (&v)[NLD1], int jj) __attribute__((always_inline)) {
+            if (jj + 1 < nb) {
+#pragma unroll
+                for (int m = 0; m < NLD1; ++m)
+                    if (l + 64 * m < D / 2) ring4[rwrap<RING / 2>(rpos + 64 * m)] = v[m];
+            }
+            rpos = rwrap<RING / 2>(rpos + D / 2);
+            fetch(v, jj + 1 + AF1);
+            __syncthreads();   // after stage 1
+            __syncthreads();   // after stage 2
+            __syncthreads();   // after stage 3
+        };
+        static_assert(AF1 == 4, "loader unroll");
+        fetch(sl[0], 1);
+        fetch(sl[1], 2);
+        fetch(sl[2], 3);
+        fetch(sl[3], 4);
+        __syncthreads();
+        int jj = 0;
+        for (; jj + 4 <= nb; jj += 4) {
+            step(sl[0], jj);
+            step(sl[1], jj + 1);
+            step(sl[2], jj + 2);
+            step(sl[3], jj + 3);
+        }
+        if (jj < nb) step(sl[0], jj);
+        if (jj + 1 < nb) step(sl[1], jj + 1);
+        if (jj + 2 < nb) step(sl[2], jj + 2);
+        return;
+    }
+    float hr[8][P];
+    if (t < 100) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+#pragma unroll
+            for (int p = 0; p < P; ++p) hr[r][p] = h[p * M + t + 100 * r];
+    }
+    __syncthreads();
+    int rbase = rwrap<RING>(L - 1 - (t < 100 ? t : 0));   // ring sample of n_j - t, block jj = 0
+    for (int j = j0; j < j1; ++j) {
+        float2 *fa = frb[(j - j0) & 1], *fb = frb[((j - j0) & 1) ^ 1];
+        // stage 1 (R = 8, Ns = 1): butterfly t < 100 on u[t + 100 r], folded from the ring
+        if (t < 100) {
+            float2 v[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                float ar = 0.f, ai = 0.f;
+#pragma unroll
+                for (int p = 0; p < P; ++p) {
+                    const float2 xv = ring[rwrap<RING>(rbase - p * M - 100 * r)];
+                    ar = fmaf(hr[r][p], xv.x, ar);
+                    ai = fmaf(hr[r][p], xv.y, ai);
+                }
+                v[r] = make_float2(ar, ai);
+            }
+            bdft8(v);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) fa[an_pad(8 * t + r)] = v[r];
+        }
+        rbase = rwrap<RING>(rbase + D);
+        __syncthreads();
+        // stage 2 (R = 4, Ns = 8): 200 butterflies on 192 threads, fa -> fb
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+            const int b = t + 192 * h2;
+            if (b < 200) {
+                float2 v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = fa[an_pad(b + 200 * r)];
+                const int m = b & 7;
+#pragma unroll
+                for (int r = 1; r < 4; ++r) v[r] = c_mul(v[r], tw[AN_TW2 + (r - 1) * 8 + m]);
+                bdft4(v[0], v[1], v[2], v[3]);
+                const int base = (b >> 3) * 32 + m;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) fb[an_pad(base + 8 * r)] = v[r];
+            }
+        }
+        __syncthreads();
+        // stage 3 (R = 5, Ns = 32): 160 butterflies, fb -> fa
+        if (t < 160) {
+            float2 v[5];
+#pragma unroll
+            for (int r = 0; r < 5; ++r) v[r] = fb[an_pad(t + 160 * r)];
+            const int m = t & 31;
+#pragma unroll
+            for (int r = 1; r < 5; ++r) v[r] = c_mul(v[r], tw[AN_TW3 + (r - 1) * 32 + m]);
+            bdft5(v);
+            const int base = (t >> 5) * 160 + m;
+#pragma unroll
+            for (int r = 0; r < 5; ++r) fa[an_pad(base + 32 * r)] = v[r];
+        }
+        __syncthreads();
+        // stage 4 (R = 5, Ns = 160): outputs k = t + 160 r, natural order, mixer rotation, to HBM
+        if (t < 160) {
+            float2 v[5];
+#pragma unroll
+            for (int r = 0; r < 5; ++r) v[r] = fa[an_pad(t + 160 * r)];
+#pragma unroll
+            for (int r = 1; r < 5; ++r) v[r] = c_mul(v[r], tw[AN_TW4 + (r - 1) * 160 + t]);
+            bdft5(v);
+            const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(Y + (size_t)j * M, 0, 8 * M, 0x00020000);
+            const int jq = (j * DM) & 3;
+#pragma unroll
+            for (int r = 0; r < 5; ++r) {
+                const int k = t + 160 * r, q = (k * jq) & 3;
+                const float a = (q & 1) ? v[r].y : v[r].x, b4 = (q & 1) ? -v[r].x : v[r].y;
+                typedef unsigned u2v __attribute__((ext_vector_type(2)));
+                const float2 o = (q & 2) ? make_float2(-a, -b4) : make_float2(a, b4);
+                __builtin_amdgcn_raw_buffer_store_b64(u2v{__float_as_uint(o.x), __float_as_uint(o.y)}, yr, 8 * k, 0,
+                                                      2 /* nt */);
+            }
+        }
+    }
+}
+
 // y[k][n] for 64 channels x RS_T outputs: v rows staged (rotated) in LDS, one lane per channel,
 // so an output's taps are wave-uniform: the phase-major table gT[rho][q] comes in by scalar loads
 // and the Q-tap loop is unrolled; the tile is transposed through LDS for row-contiguous stores.
@@ -787,14 +944,25 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
     }
     if (fused) {
         PROF(ctx, "wb_analysis");
-        // one round of workgroups (four per CU at <= 53 KB LDS) when the capture allows, >= 16
-        // blocks each (the L-sample window each workgroup loads first is its overhead)
-        // k_pfb_analysis2 addresses the capture with 32-bit byte offsets; TETRA_WB_ANALYSIS=1 keeps the
-        // one-block kernel (same-box A/B)
-        static const bool one_block_env = getenv("TETRA_WB_ANALYSIS") && atoi(getenv("TETRA_WB_ANALYSIS")) == 1;
+        // About one round of workgroups when the capture allows, >= 16 blocks each (the L-sample
+        // window each workgroup loads first is its overhead).  TETRA_WB_ANALYSIS: 1 one block per
+        // iteration (default), 2 two blocks per iteration (k_pfb_analysis2; same-box A/B and the
+        // parity tests, which switch it between calls).  The D = M / 2 kernels address the capture
+        // with 32-bit byte offsets.
+        const char *fe = getenv("TETRA_WB_ANALYSIS");
+        const int form = fe ? atoi(fe) : 1;
         if (DM == 2 && Nw * 8 >= (size_t)1 << 31)
             return tetra_fail(ctx, TETRA_E_INVALID, "D = M / 2 capture over 2 GiB: split it");
-        if (DM == 1 && (one_block_env || Nw * 8 >= (size_t)1 << 31)) {
+        if (DM == 2 && form != 2) {
+            // two 256-thread workgroups per CU (57 KB of LDS), >= 16 blocks each, about one round
+            const int jb = std::max<int>(16, (int)((nblk + 2 * 256 - 1) / (2 * 256)));
+            const unsigned grid = (unsigned)((nblk + jb - 1) / jb);
+            switch (P->P) {
+#define AN(PP) case PP: hipLaunchKernelGGL((k_pfb_analysis1<PP, 2>), dim3(grid), dim3(AN_T), 0, ctx->stream, (const float4 *)xd, (int)nblk, jb, taps, (const float2 *)(taps + tw_off), u); break;
+                AN(4) AN(5) AN(6)
+#undef AN
+            }
+        } else if (DM == 1 && (form != 2 || Nw * 8 >= (size_t)1 << 31)) {
             const int jb = std::max<int>(16, (int)((nblk + 4 * 256 - 1) / (4 * 256)));
             const unsigned grid = (unsigned)((nblk + jb - 1) / jb);
             switch (P->P) {

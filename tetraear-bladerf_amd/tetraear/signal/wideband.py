@@ -90,8 +90,8 @@ def chunking(plan, Nw, m2=M2_CHUNK):
 class WidebandReceiver:
     """Channeliser + per-carrier ETSI demod (timing, decision) for host or device arrays."""
 
-    def __init__(self, fs=FS_WB, M=M_WB, m2=M2_CHUNK):
-        self.plan = wb_plan(fs, M)
+    def __init__(self, fs=FS_WB, M=M_WB, m2=M2_CHUNK, oversample=None):
+        self.plan = wb_plan(fs, M, oversample)
         self.etsi = etsi_plan(2.4e6)   # timing-loop constants (the channel-filter taps are not used)
         self.m2 = m2
 
@@ -124,10 +124,10 @@ class WidebandReceiver:
                 ns.reshape(M, nchunk))
 
 
-def synth_wideband(Nw, seed=1, snr_db=30.0, cfo_max=300.0, fs=FS_WB, M=M_WB):
+def synth_wideband(Nw, seed=1, snr_db=30.0, cfo_max=300.0, fs=FS_WB, M=M_WB, oversample=None):
     """Synthetic capture (device-generated, copied to the host): x [Nw] complex64, cells [M],
     kinds [M][NB], payload [M][NB][2][268], t0 [M] (carrier k is FFT bin k, at +k fs/M)."""
-    plan = wb_plan(fs, M)
+    plan = wb_plan(fs, M, oversample)
     c = _hip.ctx()
     nbb = Nw // plan.D + 1
     nb = c.lib.tetra_synth_bursts_per_channel(nbb, fs / plan.D)
@@ -243,8 +243,8 @@ class BenchStep:
         8 B symbol, 2 soft bits and a hard dibit.  bench.py reports the slowest of them."""
         M, D, fs = self.plan.M, self.plan.D, self.fs
         yb = 8.0 * M * 72000.0 / fs
-        ana = "k_pfb_analysis" if os.environ.get("TETRA_WB_ANALYSIS") == "1" and self.plan.oversample == 4 \
-            else "k_pfb_analysis2"
+        ana = "k_pfb_analysis2" if os.environ.get("TETRA_WB_ANALYSIS") == "2" else \
+            ("k_pfb_analysis1" if self.plan.oversample == 2 else "k_pfb_analysis")
         return {"waterfall": (12.0 * self.nfr * 2048 / self.Nw, "k_waterfall"),
                 "wb_analysis": (8.0 + 8.0 * M / D, ana),   # fused fold + FFT: x in, Y out
                 "wb_fold": (8.0 + 8.0 * M / D, "k_pfb_fold"), "wb_fft": (2 * 8.0 * M / D, None),
