@@ -63,6 +63,39 @@ def test_chanfilt_and_timing_bit_exact(synth_small):
         assert np.array_equal(hard[ch, :n - 1], ho), ch
 
 
+@pytest.mark.parametrize("ring,lean", [(0, 0), (0, 1), (1, 0), (1, 1), (2, 0), (2, 1)])
+def test_timing_forms_bit_exact(synth_small, ring, lean, monkeypatch):
+    """Every k_timing form the host can pick (TETRA_TIMING_RING: Gardner windows from global memory,
+    an LDS ring fed one or two blocks ahead; TETRA_TIMING_LEAN: the Oerder-Meyr pass with all quarters'
+    loads together and d_j recomputed from the stored symbols, or round 3's form) equals the oracle's timing bit for bit, on full chunks and on ragged
+    lengths (a partial last block, a chunk shorter than the ring's prefill)."""
+    from tetraear import _hip
+    from tetraear.signal.etsi import etsi_plan, lengths
+    monkeypatch.setenv("TETRA_TIMING_RING", str(ring))
+    monkeypatch.setenv("TETRA_TIMING_LEAN", str(lean))
+    iq = synth_small[0][:4]
+    rx = E.Receiver()
+    plan = etsi_plan()
+    C, N = iq.shape
+    _, M2, smax = lengths(plan, N)
+    c = _hip.ctx()
+    y = np.zeros((C, M2), np.complex64)
+    c.check(c.lib.tetra_etsi_chanfilt(c.handle, plan, _hip.ptr(iq), C, N, _hip.ptr(y)))
+    for m2 in (M2, M2 - 37, 1001, 300, 17):
+        yy = np.ascontiguousarray(y[:, :m2])
+        sm = m2 // 4 + 2
+        sym = np.zeros((C, sm), np.complex64)
+        soft, hard, ns = np.zeros((C, 2 * sm), np.int8), np.zeros((C, sm), np.uint8), np.zeros(C, np.int32)
+        c.check(c.lib.tetra_etsi_timing(c.handle, plan, _hip.ptr(yy), C, m2, _hip.ptr(sym), _hip.ptr(soft),
+                                        _hip.ptr(hard), _hip.ptr(ns), sm, None))
+        for ch in range(C):
+            so, sbo, ho, _ = rx.timing(yy[ch])
+            n = int(ns[ch])
+            assert n == len(so), (m2, ch)
+            assert np.array_equal(sym[ch, :n], so) and np.array_equal(hard[ch, :n - 1], ho), (m2, ch)
+            assert np.array_equal(soft[ch, :2 * (n - 1)], sbo), (m2, ch)
+
+
 def test_lower_mac_matches_oracle(synth_small):
     from tetraear.signal.etsi import EtsiReceiver
     from tetraear.core.etsi import EtsiLowerMac

@@ -206,14 +206,48 @@ __device__ __forceinline__ float om_part(const float2 *y, int M2, int w, int lan
     }
     return s;
 }
+// The four om_part sums of one lane with the quarters' loads interleaved (k_timing, y in global
+// memory): OM_U loads of each quarter in flight together -- 4 OM_U -- instead of om_part's 8 of one
+// quarter, so the pass waits on 4x fewer round trips; each quarter still sums in ascending n and the
+// quarters are added in order, so the result is om_part(0) + .. + om_part(3) to the bit.
+constexpr int OM_U = 4;
+__device__ __forceinline__ float om_all(const float2 *y, int M2, int lane) {
+    const int nb = (M2 + 63) / 64, q4 = (nb + 3) / 4;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < q4; i += OM_U) {
+        float2 v[4][OM_U];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const int n1 = min(64 * min((w + 1) * q4, nb), M2);
+#pragma unroll
+            for (int u = 0; u < OM_U; ++u) {
+                const int n = 64 * (w * q4 + i + u) + lane;
+                v[w][u] = (i + u < q4 && n < n1) ? y[n] : make_float2(0.f, 0.f);
+            }
+        }
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const int n1 = min(64 * min((w + 1) * q4, nb), M2);
+#pragma unroll
+            for (int u = 0; u < OM_U; ++u) {
+                const int n = 64 * (w * q4 + i + u) + lane;
+                if (i + u < q4 && n < n1) s[w] += fmaf(v[w][u].x, v[w][u].x, v[w][u].y * v[w][u].y);
+            }
+        }
+    }
+    return ((s[0] + s[1]) + s[2]) + s[3];
+}
 
 // RING (k_timing, y in global memory): the Gardner loop reads y from a 512-sample LDS ring (4 KB: eight
 // one-wave workgroups per SIMD still fit) filled a block ahead -- block b needs y[4 kb - 5, 4 kb + 260)
 // (|delta| <= 1.5, the cubic window), the ring holds [0, 320) before the loop, and block b first writes
 // the 256 samples the previous block loaded into registers, [320 + 256 (b - 1), 320 + 256 b) (over
 // [256 b - 448, 256 b - 192), which no later block reads), then loads the next 256: each block's window
-// reads wait on LDS, not on L2 / HBM.  Same interpolation arithmetic, same bits.
-template <bool SPLIT = false, bool RING = false>
+// reads wait on LDS, not on L2 / HBM.  Same interpolation arithmetic, same bits.  RING = 2 keeps two
+// blocks' loads in flight in registers (pre, pre2: the ring's contents at every block are the same).
+// LEAN (k_timing): the Oerder-Meyr pass by om_all (all quarters' loads together) instead of om_part per
+// quarter, and no d_j stores -- the decision pass recomputes d_j from the stored symbols (timing_decide_sym).
+template <bool SPLIT = false, int RING = 0, bool LEAN = false>
 __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float gain, float soft_scale, float2 *sp,
                                                  float2 *dp, int smax, int lane, int *prog = nullptr,
                                                  const float *om = nullptr, float2 *ring = nullptr) {
@@ -232,6 +266,8 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
         s = om[lane];
 #pragma unroll
         for (int w = 1; w < 4; ++w) s = s + om[64 * w + lane];
+    } else if constexpr (LEAN) {
+        s = om_all(y, M2, lane);
     } else {
         s = om_part(y, M2, 0, lane);
 #pragma unroll
@@ -250,22 +286,34 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
     bool have_prev = false;
     float zr = 0.f, zi = 0.f, am = 0.f;   // CFO sums over this lane's d_j
     int rel = -1;   // SPLIT: progress not yet released (published after the next block's LDS reads)
-    float2 pre[4];   // RING: the next block's 256 samples in flight
+    float2 pre[4], pre2[4];   // RING: the next block's 256 samples in flight (RING 2: and the one after)
     auto ld = [&](int n) -> float2 { return n < M2 ? y[n] : make_float2(0.f, 0.f); };
-    if constexpr (RING) {
+    if constexpr (RING > 0) {
 #pragma unroll
         for (int u = 0; u < 5; ++u) ring[64 * u + lane] = ld(64 * u + lane);
 #pragma unroll
         for (int u = 0; u < 4; ++u) pre[u] = ld(320 + 64 * u + lane);
+        if constexpr (RING > 1) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) pre2[u] = ld(576 + 64 * u + lane);
+        }
     }
     for (int kb = kstart;; kb += 64) {
-        if constexpr (RING) {
+        if constexpr (RING > 0) {
             if (kb != kstart) {   // the previous block's loads: y[320 + 256 (b - 1) ...)
                 const int n0 = 320 + 4 * (kb - kstart) - 256;
 #pragma unroll
                 for (int u = 0; u < 4; ++u) ring[(n0 + 64 * u + lane) & (TRING - 1)] = pre[u];
+                if constexpr (RING > 1) {
 #pragma unroll
-                for (int u = 0; u < 4; ++u) pre[u] = ld(n0 + 256 + 64 * u + lane);
+                    for (int u = 0; u < 4; ++u) {
+                        pre[u] = pre2[u];
+                        pre2[u] = ld(n0 + 512 + 64 * u + lane);
+                    }
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) pre[u] = ld(n0 + 256 + 64 * u + lane);
+                }
             }
         }
         const float off = base + delta;
@@ -288,7 +336,7 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
             }
             if (rel >= 0 && lane == 0)   // the previous block's d_j: its stores completed before these reads
                 __hip_atomic_store(prog, rel, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else if constexpr (RING) {
+        } else if constexpr (RING > 0) {
             if (act) interp_pair_ring(ring, t, on, mid);
         } else {
             if (act) interp_pair(y, 0, t, on, mid);
@@ -304,7 +352,7 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
                 ev = fmaf(dr, mid.x, di * mid.y);
                 const int j = S + lane;
                 const float xr = fmaf(on.x, pv.x, on.y * pv.y), xi = fmaf(on.y, pv.x, -(on.x * pv.y));
-                dp[j - 1] = make_float2(xr, xi);
+                if constexpr (!LEAN) dp[j - 1] = make_float2(xr, xi);
                 if constexpr (!SPLIT) {
                     // CFO: 4th power and magnitude of d_j (j = lane mod 64, ascending: the oracle's order)
                     const float sr = fmaf(xr, xr, -(xi * xi)), si = (xr * xi) * 2.0f;
@@ -416,34 +464,75 @@ __device__ __forceinline__ void timing_decide(const TrackOut &o, const float2 *d
     }
 }
 
-template <bool RING = false>
+// timing_decide with d_j = s_j conj(s_{j-1}) recomputed from the stored symbols sp -- the same fmas on
+// the same values the tracking loop formed it from, so the same bits (k_timing LEAN: d_j is not stored)
+__device__ __forceinline__ void timing_decide_sym(const TrackOut &o, const float2 *sp, int8_t *sb, uint8_t *hp,
+                                                  int lane) {
+    for (int j0 = 1 + lane; j0 < o.S; j0 += 4 * 64) {
+        float2 a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + 64 * u;
+            a[u] = j < o.S ? sp[j] : make_float2(0.f, 0.f);
+            b[u] = j < o.S ? sp[j - 1] : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + 64 * u;
+            if (j >= o.S) break;
+            const float2 on = a[u], pv = b[u];
+            const float dx = fmaf(on.x, pv.x, on.y * pv.y), dy = fmaf(on.y, pv.x, -(on.x * pv.y));
+            const float xr = fmaf(dx, o.rr, -(dy * o.ri)), xi = fmaf(dx, o.ri, dy * o.rr);
+            float q1 = rintf(xi * o.sc), q2 = rintf(xr * o.sc);
+            q1 = q1 > 127.f ? 127.f : (q1 < -127.f ? -127.f : q1);
+            q2 = q2 > 127.f ? 127.f : (q2 < -127.f ? -127.f : q2);
+            sb[2 * (j - 1)] = (int8_t)q1;
+            sb[2 * (j - 1) + 1] = (int8_t)q2;
+            hp[j - 1] = (uint8_t)(((xi < 0.0f) << 1) | (xr < 0.0f));
+        }
+    }
+}
+
+template <int RING = 0, bool LEAN = false>
 __device__ __forceinline__ void timing_wave(const float2 *y, int M2, float gain, float soft_scale, float2 *sp,
                                             float2 *dp, int8_t *sb, uint8_t *hp, int32_t *nsym_ch, float4 *diag_ch,
                                             int smax, int lane, float2 *ring = nullptr) {
-    const TrackOut o = timing_track<false, RING>(y, M2, gain, soft_scale, sp, dp, smax, lane, nullptr, nullptr, ring);
-    __threadfence_block();   // dp written by other lanes is read below
-    timing_decide(o, dp, sb, hp, 0, 1, lane);
+    const TrackOut o = timing_track<false, RING, LEAN>(y, M2, gain, soft_scale, sp, dp, smax, lane, nullptr, nullptr, ring);
+    __threadfence_block();   // dp / sp written by other lanes is read below
+    if constexpr (LEAN)
+        timing_decide_sym(o, sp, sb, hp, lane);
+    else
+        timing_decide(o, dp, sb, hp, 0, 1, lane);
     if (lane == 0) {
         *nsym_ch = o.S;
         if (diag_ch && M2 >= 16) *diag_ch = make_float4(o.base, o.delta, o.rr, o.ri);
     }
 }
 
-template <bool RING>
+template <int RING, bool LEAN>
 __global__ __launch_bounds__(64) void k_timing(const float2 *__restrict__ yall, int M2, float gain, float soft_scale,
                                                float2 *__restrict__ sym, float2 *__restrict__ dscr,
                                                int8_t *__restrict__ softbits, uint8_t *__restrict__ hard,
                                                int32_t *__restrict__ nsym, int smax, float4 *__restrict__ diag) {
     __shared__ float2 ring[RING ? TRING : 1];
     const int ch = blockIdx.x;
-    timing_wave<RING>(yall + (size_t)ch * M2, M2, gain, soft_scale, sym + (size_t)ch * smax, dscr + (size_t)ch * smax,
+    timing_wave<RING, LEAN>(yall + (size_t)ch * M2, M2, gain, soft_scale, sym + (size_t)ch * smax, dscr + (size_t)ch * smax,
                       softbits + (size_t)ch * 2 * smax, hard + (size_t)ch * smax, nsym + ch, diag ? diag + ch : nullptr,
                       smax, threadIdx.x, ring);
 }
-// TETRA_TIMING_RING=0: the Gardner windows read straight from global memory (same-box A/B)
-static bool timing_ring() {
-    static const bool on = !(getenv("TETRA_TIMING_RING") && atoi(getenv("TETRA_TIMING_RING")) == 0);
-    return on;
+// k_timing's form (same-box A/B): TETRA_TIMING_RING = 0 (the Gardner windows read straight from
+// global memory), 1 (one block ahead, default) or 2 (two); TETRA_TIMING_LEAN = 0 keeps om_part per
+// quarter for the Oerder-Meyr pass and the d_j round trip through dscr (default 1: om_all, d_j
+// recomputed from the symbols)
+using timing_fn = void (*)(const float2 *, int, float, float, float2 *, float2 *, int8_t *, uint8_t *, int32_t *, int,
+                           float4 *);
+static timing_fn timing_kernel() {
+    const char *r = getenv("TETRA_TIMING_RING"), *o = getenv("TETRA_TIMING_LEAN");
+    const int ring = r ? atoi(r) : 1;
+    const bool lean = !(o && atoi(o) == 0);
+    if (ring <= 0) return lean ? k_timing<0, true> : k_timing<0, false>;
+    if (ring == 1) return lean ? k_timing<1, true> : k_timing<1, false>;
+    return lean ? k_timing<2, true> : k_timing<2, false>;
 }
 
 // --------------------------------------------------------------------------- E1 channel filter
@@ -2206,7 +2295,7 @@ int tetra_etsi_timing(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *y, s
     if (!yd || !so || !sbo || !ho || !no || !dscr) return st.finish();
     {
         PROF(ctx, "etsi_timing");
-        hipLaunchKernelGGL(timing_ring() ? k_timing<true> : k_timing<false>, dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yd, (int)M2, P->gain,
+        hipLaunchKernelGGL(timing_kernel(), dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yd, (int)M2, P->gain,
                            P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg);
     }
     return st.finish();
@@ -2255,7 +2344,7 @@ int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *i
     if (rc) return rc;
     {
         PROF(ctx, "etsi_timing");
-        hipLaunchKernelGGL(timing_ring() ? k_timing<true> : k_timing<false>, dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yb, (int)M2, P->gain,
+        hipLaunchKernelGGL(timing_kernel(), dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yb, (int)M2, P->gain,
                            P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg);
     }
     return st.finish();
