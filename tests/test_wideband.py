@@ -108,6 +108,22 @@ def test_channelize_every_analysis_form(oversample, form, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("oversample", [2, 4])
+def test_resampler_wave_tiles_equal(oversample, monkeypatch):
+    """TETRA_WB_RESAMP_WT=1 (per-wave transposing tiles) changes only how the resampler's outputs are
+    stored: y is bit-identical to the workgroup-tile form, ragged capture length included."""
+    from tetraear.signal.wideband import WidebandReceiver, synth_wideband
+    x = synth_wideband(300_011, seed=9, snr_db=20.0, oversample=oversample)[0]
+    rx = WidebandReceiver(oversample=oversample)
+    monkeypatch.setenv("TETRA_WB_RESAMP_WT", "0")
+    y0 = rx.channelize(x)
+    monkeypatch.setenv("TETRA_WB_RESAMP_WT", "1")
+    y1 = rx.channelize(x)
+    y2 = rx.channelize(x, 1001)
+    assert np.array_equal(y0, y1) and np.array_equal(y2, y0[:, :1001])
+
+
+@pytest.mark.gpu
 def test_wideband_timing_bit_exact(capture):
     """From y on the chain is the ETSI one: the GPU timing on the channeliser's own output equals
     oracle/etsi.py on the same y, carrier by carrier."""

@@ -12,8 +12,8 @@ timeout -k 10 400 python -u -m pytest -v --timeout 150 --timeout-method thread t
 tail -1 $O/r04d_pytest.log
 if [ $rc -gt 1 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi
 AB_ARGS="--chain wideband --pipeline off" bash tools/ab.sh env "TETRA_WB_OVERSAMPLE=2" "TETRA_WB_OVERSAMPLE=2 TETRA_WB_ANALYSIS=2" \
-  "TETRA_WB_OVERSAMPLE=4" "TETRA_WB_OVERSAMPLE=2 TETRA_TIMING_RING=2" "TETRA_WB_OVERSAMPLE=2 TETRA_TIMING_LEAN=0" > $O/r04d_ab_serial.txt 2>&1
+  "TETRA_WB_OVERSAMPLE=4" "TETRA_WB_OVERSAMPLE=2 TETRA_TIMING_RING=2" "TETRA_WB_OVERSAMPLE=2 TETRA_TIMING_LEAN=0" "TETRA_WB_OVERSAMPLE=2 TETRA_WB_RESAMP_WT=1" > $O/r04d_ab_serial.txt 2>&1
 AB_ARGS="--chain wideband" bash tools/ab.sh env "TETRA_WB_OVERSAMPLE=2" "TETRA_WB_OVERSAMPLE=2 TETRA_WB_ANALYSIS=2" \
-  "TETRA_WB_OVERSAMPLE=4" "TETRA_WB_OVERSAMPLE=2 TETRA_TIMING_RING=0" > $O/r04d_ab_pipe.txt 2>&1
+  "TETRA_WB_OVERSAMPLE=4" "TETRA_WB_OVERSAMPLE=2 TETRA_WB_RESAMP_WT=1" > $O/r04d_ab_pipe.txt 2>&1
 AB_ARGS="--demod split" AB_ROUNDS=2 bash tools/ab.sh env "TETRA_TIMING_RING=1" "TETRA_TIMING_RING=2" "TETRA_TIMING_RING=1 TETRA_TIMING_LEAN=0" "TETRA_TIMING_RING=0" > $O/r04d_ab_split.txt 2>&1
 echo done
