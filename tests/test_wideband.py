@@ -92,11 +92,12 @@ def test_channelize_vs_oracle(capture):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("oversample,form", [(2, "1"), (2, "2"), (4, "1"), (4, "2")])
+@pytest.mark.parametrize("oversample,form", [(2, "1"), (2, "2"), (2, "3"), (4, "1"), (4, "2")])
 def test_channelize_every_analysis_form(oversample, form, monkeypatch):
     """Both filter-bank designs (D = M / 2 and M / 4) through each analysis kernel the host can pick
-    (TETRA_WB_ANALYSIS: 1 one block per iteration, 2 two blocks), held to the oracle of that design;
-    a capture long enough for several blocks per workgroup and a ragged tail."""
+    (TETRA_WB_ANALYSIS: 1 one block per iteration, 2 two blocks, 3 one block with every twiddle in
+    LDS), held to the oracle of that design; a capture long enough for several blocks per workgroup
+    and a ragged tail."""
     from tetraear.signal.wideband import WidebandReceiver, synth_wideband
     monkeypatch.setenv("TETRA_WB_ANALYSIS", form)
     x = synth_wideband(400_037, seed=5, snr_db=20.0, oversample=oversample)[0]

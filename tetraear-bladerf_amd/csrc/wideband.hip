@@ -496,9 +496,11 @@ __global__ __launch_bounds__(A2_T, (A2Cfg<P, DM>::WAVES)) void k_pfb_analysis2(c
 // One block per iteration at any D (k_pfb_analysis's structure -- waves 0-2 fold + transform +
 // store, wave 3 loads -- with analysis2's ring indexing and buffer-resource loader): the D = M / 2
 // filter bank's default analysis.  LDS: the 4608-sample ring (L + D = 4400 at P = 5), two frames
-// and the twiddles, 57 KB: two workgroups per CU.
-template <int P, int DM>
-__global__ __launch_bounds__(AN_T, 2) void k_pfb_analysis1(const float4 *__restrict__ x2, int nblk, int JB,
+// and stages 2-3's twiddles, 52.5 KB (TREG: stage 4's 640 twiddles are four registers per thread, and
+// the VGPRs are held to 168): three workgroups per CU at P <= 5.  !TREG: all twiddles in LDS, 57.6 KB,
+// two workgroups per CU (TETRA_WB_ANALYSIS=3, same-box A/B).
+template <int P, int DM, bool TREG = true>
+__global__ __launch_bounds__(AN_T, (TREG && P <= 5 ? 3 : 2)) void k_pfb_analysis1(const float4 *__restrict__ x2, int nblk, int JB,
                                                            const float *__restrict__ h,
                                                            const float2 *__restrict__ twg, float2 *__restrict__ Y) {
     using Cf = A2Cfg<P, DM>;
@@ -507,13 +509,17 @@ __global__ __launch_bounds__(AN_T, 2) void k_pfb_analysis1(const float4 *__restr
     constexpr int AF1 = 4;                    // blocks ahead
     __shared__ float4 ring4[RING / 2];
     __shared__ float2 frb[2][AN_FR];
-    __shared__ float2 tw[AN_TWN];
+    __shared__ float2 tw[TREG ? AN_TW4 : AN_TWN];   // TREG: stages 2-3; stage 4's sit in registers (tw4)
     const float2 *ring = reinterpret_cast<const float2 *>(ring4);
     const int t = threadIdx.x;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
     const int j0 = blockIdx.x * JB, j1 = min(nblk, j0 + JB);
     const int nb = j1 - j0;
-    for (int i = t; i < AN_TWN; i += AN_T) tw[i] = twg[i];
+    for (int i = t; i < (TREG ? AN_TW4 : AN_TWN); i += AN_T) tw[i] = twg[i];
+    float2 tw4[4];
+#pragma unroll
+    for (int r = 1; r < 5; ++r)
+        tw4[r - 1] = TREG && t < 160 ? twg[AN_TW4 + (r - 1) * 160 + t] : make_float2(0.f, 0.f);
     const long npr = (long)(L + (long)(nblk - 1) * D) / 2;   // pairs of samples any block reads
     const long pr0 = (long)j0 * (D / 2);                      // ring pair 0 = x[j0 D]
     for (int q = t; q < L / 2; q += AN_T)                     // the first block's window
@@ -633,7 +639,7 @@ __global__ __launch_bounds__(AN_T, 2) void k_pfb_analysis1(const float4 *__restr
 #pragma unroll
             for (int r = 0; r < 5; ++r) v[r] = fa[an_pad(t + 160 * r)];
 #pragma unroll
-            for (int r = 1; r < 5; ++r) v[r] = c_mul(v[r], tw[AN_TW4 + (r - 1) * 160 + t]);
+            for (int r = 1; r < 5; ++r) v[r] = c_mul(v[r], TREG ? tw4[r - 1] : tw[AN_TW4 + (r - 1) * 160 + t]);
             bdft5(v);
             const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(Y + (size_t)j * M, 0, 8 * M, 0x00020000);
             const int jq = (j * DM) & 3;
@@ -970,20 +976,23 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
         PROF(ctx, "wb_analysis");
         // About one round of workgroups when the capture allows, >= 16 blocks each (the L-sample
         // window each workgroup loads first is its overhead).  TETRA_WB_ANALYSIS: 1 one block per
-        // iteration (default), 2 two blocks per iteration (k_pfb_analysis2; same-box A/B and the
-        // parity tests, which switch it between calls).  The D = M / 2 kernels address the capture
+        // iteration (default), 2 two blocks per iteration (k_pfb_analysis2), 3 (D = M / 2) one block
+        // with every twiddle in LDS -- same-box A/B and the parity tests, which switch it between calls.  The D = M / 2 kernels address the capture
         // with 32-bit byte offsets.
         const char *fe = getenv("TETRA_WB_ANALYSIS");
         const int form = fe ? atoi(fe) : 1;
         if (DM == 2 && Nw * 8 >= (size_t)1 << 31)
             return tetra_fail(ctx, TETRA_E_INVALID, "D = M / 2 capture over 2 GiB: split it");
         if (DM == 2 && form != 2) {
-            // two 256-thread workgroups per CU (57 KB of LDS), >= 16 blocks each, about one round
-            const int jb = std::max<int>(16, (int)((nblk + 2 * 256 - 1) / (2 * 256)));
+            // three (P <= 5, twiddles in registers) or two 256-thread workgroups per CU, >= 16 blocks
+            // each, about one round
+            const bool treg = form != 3;
+            const int per_cu = treg && P->P <= 5 ? 3 : 2;
+            const int jb = std::max<int>(16, (int)((nblk + per_cu * 256 - 1) / (per_cu * 256)));
             const unsigned grid = (unsigned)((nblk + jb - 1) / jb);
-            switch (P->P) {
-#define AN(PP) case PP: hipLaunchKernelGGL((k_pfb_analysis1<PP, 2>), dim3(grid), dim3(AN_T), 0, ctx->stream, (const float4 *)xd, (int)nblk, jb, taps, (const float2 *)(taps + tw_off), u); break;
-                AN(4) AN(5) AN(6)
+            switch (P->P * 2 + (treg ? 1 : 0)) {
+#define AN(PP, TR) case PP * 2 + TR: hipLaunchKernelGGL((k_pfb_analysis1<PP, 2, TR>), dim3(grid), dim3(AN_T), 0, ctx->stream, (const float4 *)xd, (int)nblk, jb, taps, (const float2 *)(taps + tw_off), u); break;
+                AN(4, 0) AN(5, 0) AN(6, 0) AN(4, 1) AN(5, 1) AN(6, 1)
 #undef AN
             }
         } else if (DM == 1 && (form != 2 || Nw * 8 >= (size_t)1 << 31)) {

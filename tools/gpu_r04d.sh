@@ -11,9 +11,9 @@ timeout -k 10 400 python -u -m pytest -v --timeout 150 --timeout-method thread t
   "tests/test_gpu_etsi.py::test_hard_symbol_decode_rate" -m gpu > $O/r04d_pytest.log 2>&1 || rc=$?
 tail -1 $O/r04d_pytest.log
 if [ $rc -gt 1 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi
-AB_ARGS="--chain wideband --pipeline off" bash tools/ab.sh env "TETRA_WB_OVERSAMPLE=2" "TETRA_WB_OVERSAMPLE=2 TETRA_WB_ANALYSIS=2" \
+AB_ROUNDS=2 AB_ARGS="--chain wideband --pipeline off" bash tools/ab.sh env "TETRA_WB_OVERSAMPLE=2" "TETRA_WB_OVERSAMPLE=2 TETRA_WB_ANALYSIS=2" "TETRA_WB_OVERSAMPLE=2 TETRA_WB_ANALYSIS=3" \
   "TETRA_WB_OVERSAMPLE=4" "TETRA_WB_OVERSAMPLE=2 TETRA_TIMING_RING=2" "TETRA_WB_OVERSAMPLE=2 TETRA_TIMING_LEAN=0" "TETRA_WB_OVERSAMPLE=2 TETRA_WB_RESAMP_WT=1" > $O/r04d_ab_serial.txt 2>&1
-AB_ARGS="--chain wideband" bash tools/ab.sh env "TETRA_WB_OVERSAMPLE=2" "TETRA_WB_OVERSAMPLE=2 TETRA_WB_ANALYSIS=2" \
+AB_ROUNDS=2 AB_ARGS="--chain wideband" bash tools/ab.sh env "TETRA_WB_OVERSAMPLE=2" "TETRA_WB_OVERSAMPLE=2 TETRA_WB_ANALYSIS=2" "TETRA_WB_OVERSAMPLE=2 TETRA_WB_ANALYSIS=3" \
   "TETRA_WB_OVERSAMPLE=4" "TETRA_WB_OVERSAMPLE=2 TETRA_WB_RESAMP_WT=1" > $O/r04d_ab_pipe.txt 2>&1
 AB_ARGS="--demod split" AB_ROUNDS=2 bash tools/ab.sh env "TETRA_TIMING_RING=1" "TETRA_TIMING_RING=2" "TETRA_TIMING_RING=1 TETRA_TIMING_LEAN=0" "TETRA_TIMING_RING=0" > $O/r04d_ab_split.txt 2>&1
 echo done
