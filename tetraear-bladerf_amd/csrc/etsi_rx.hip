@@ -250,7 +250,8 @@ __device__ __forceinline__ float om_all(const float2 *y, int M2, int lane) {
 template <bool SPLIT = false, int RING = 0, bool LEAN = false>
 __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float gain, float soft_scale, float2 *sp,
                                                  float2 *dp, int smax, int lane, int *prog = nullptr,
-                                                 const float *om = nullptr, float2 *ring = nullptr) {
+                                                 const float *om = nullptr, float2 *ring = nullptr,
+                                                 uint32_t *clk = nullptr) {
     TrackOut o{0, 1.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     if (M2 < 16) {
         if constexpr (SPLIT) {
@@ -274,6 +275,7 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
         for (int w = 1; w < 4; ++w) s = s + om_part(y, M2, w, lane);
     }
     s = bfly<4>(s);
+    if (clk && lane == 0) clk[1] = (uint32_t)wall_clock64();   // probe: the Oerder-Meyr pass done
     const float A0 = lane_f(s, 0), A1 = lane_f(s, 1), A2 = lane_f(s, 2), A3 = lane_f(s, 3);
     const float Xr = A0 - A2, Xi = A3 - A1;
     const float p = -0.63661977236758134f * pat2(Xi, Xr);
@@ -493,11 +495,16 @@ __device__ __forceinline__ void timing_decide_sym(const TrackOut &o, const float
     }
 }
 
+// clk (probe, TETRA_TIMING_PROBE=1 with a diag buffer): the wave's wall-clock stamps at its start, after
+// the Oerder-Meyr pass, after the Gardner loop and at its end, in place of the diagnostics
 template <int RING = 0, bool LEAN = false>
 __device__ __forceinline__ void timing_wave(const float2 *y, int M2, float gain, float soft_scale, float2 *sp,
                                             float2 *dp, int8_t *sb, uint8_t *hp, int32_t *nsym_ch, float4 *diag_ch,
-                                            int smax, int lane, float2 *ring = nullptr) {
-    const TrackOut o = timing_track<false, RING, LEAN>(y, M2, gain, soft_scale, sp, dp, smax, lane, nullptr, nullptr, ring);
+                                            int smax, int lane, float2 *ring = nullptr, uint32_t *clk = nullptr) {
+    if (clk && lane == 0) clk[0] = (uint32_t)wall_clock64();
+    const TrackOut o =
+        timing_track<false, RING, LEAN>(y, M2, gain, soft_scale, sp, dp, smax, lane, nullptr, nullptr, ring, clk);
+    if (clk && lane == 0) clk[2] = (uint32_t)wall_clock64();
     __threadfence_block();   // dp / sp written by other lanes is read below
     if constexpr (LEAN)
         timing_decide_sym(o, sp, sb, hp, lane);
@@ -505,7 +512,12 @@ __device__ __forceinline__ void timing_wave(const float2 *y, int M2, float gain,
         timing_decide(o, dp, sb, hp, 0, 1, lane);
     if (lane == 0) {
         *nsym_ch = o.S;
-        if (diag_ch && M2 >= 16) *diag_ch = make_float4(o.base, o.delta, o.rr, o.ri);
+        if (clk) {
+            __builtin_amdgcn_s_waitcnt(0);   // the decision pass's stores issued and done
+            clk[3] = (uint32_t)wall_clock64();
+        } else if (diag_ch && M2 >= 16) {
+            *diag_ch = make_float4(o.base, o.delta, o.rr, o.ri);
+        }
     }
 }
 
@@ -513,19 +525,27 @@ template <int RING, bool LEAN>
 __global__ __launch_bounds__(64) void k_timing(const float2 *__restrict__ yall, int M2, float gain, float soft_scale,
                                                float2 *__restrict__ sym, float2 *__restrict__ dscr,
                                                int8_t *__restrict__ softbits, uint8_t *__restrict__ hard,
-                                               int32_t *__restrict__ nsym, int smax, float4 *__restrict__ diag) {
+                                               int32_t *__restrict__ nsym, int smax, float4 *__restrict__ diag,
+                                               int probe) {
     __shared__ float2 ring[RING ? TRING : 1];
     const int ch = blockIdx.x;
+    uint32_t *clk = probe && diag ? reinterpret_cast<uint32_t *>(diag + ch) : nullptr;
     timing_wave<RING, LEAN>(yall + (size_t)ch * M2, M2, gain, soft_scale, sym + (size_t)ch * smax, dscr + (size_t)ch * smax,
                       softbits + (size_t)ch * 2 * smax, hard + (size_t)ch * smax, nsym + ch, diag ? diag + ch : nullptr,
-                      smax, threadIdx.x, ring);
+                      smax, threadIdx.x, ring, clk);
 }
 // k_timing's form (same-box A/B): TETRA_TIMING_RING = 0 (the Gardner windows read straight from
 // global memory), 1 (one block ahead, default) or 2 (two); TETRA_TIMING_LEAN = 0 keeps om_part per
 // quarter for the Oerder-Meyr pass and the d_j round trip through dscr (default 1: om_all, d_j
 // recomputed from the symbols)
 using timing_fn = void (*)(const float2 *, int, float, float, float2 *, float2 *, int8_t *, uint8_t *, int32_t *, int,
-                           float4 *);
+                           float4 *, int);
+// TETRA_TIMING_PROBE=1: with a diag buffer, each chunk's diag entry holds four 32-bit wall-clock stamps
+// (start, Oerder-Meyr done, Gardner done, end) instead of the diagnostics -- a latency probe
+static int timing_probe() {
+    const char *e = getenv("TETRA_TIMING_PROBE");
+    return e && atoi(e) == 1;
+}
 static timing_fn timing_kernel() {
     const char *r = getenv("TETRA_TIMING_RING"), *o = getenv("TETRA_TIMING_LEAN");
     const int ring = r ? atoi(r) : 1;
@@ -2296,7 +2316,7 @@ int tetra_etsi_timing(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *y, s
     {
         PROF(ctx, "etsi_timing");
         hipLaunchKernelGGL(timing_kernel(), dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yd, (int)M2, P->gain,
-                           P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg);
+                           P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg, timing_probe());
     }
     return st.finish();
 }
@@ -2345,7 +2365,7 @@ int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *i
     {
         PROF(ctx, "etsi_timing");
         hipLaunchKernelGGL(timing_kernel(), dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yb, (int)M2, P->gain,
-                           P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg);
+                           P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg, timing_probe());
     }
     return st.finish();
 }
