@@ -269,10 +269,12 @@ class BenchStep:
                 c.check(c.lib.tetra_synth_etsi(c.handle, n, NT, fs, seed + 7919 * (s0 // S), snr_db, 600.0, _hip.ptr(x),
                                                _hip.ptr(self.cells[s0:]), _hip.ptr(self.kinds[s0:]),
                                                _hip.ptr(self.payload[s0:]), None), "synth")
+                c.synchronize()   # the copies below run on torch's stream, which need not be the context's
                 for k in range(self.chunks):
                     self.iqs[k][s0:s0 + n].copy_(x[:, k * N:(k + 1) * N])
                 del x
         c.check(c.lib.tetra_etsi_set_cells(c.handle, _hip.ptr(self.cells), C), "set_cells")
+        c.synchronize()   # the synthesised batches are read by torch's ops below (SC16 conversion)
         from tetraear.core.etsi import UNKNOWN_CELL
         self.cell_state = torch.full((C,), UNKNOWN_CELL, dtype=torch.int32, device=device)
         if self.fmt == _hip.TETRA_SC16:   # the synth output is on the SC16 grid: exact
@@ -292,6 +294,11 @@ class BenchStep:
         if demod == "split":
             self.y = [torch.empty((C, self.M2, 2), dtype=torch.float32, device=device)]
         self.pipelined = False
+        # buffers made by torch (on torch's stream) are complete before any kernel of the context's
+        # stream -- a context of its own (the tests' _hip.ctx()) runs on a stream that does not wait
+        # for torch's
+        c.synchronize()
+        torch.cuda.current_stream(device).synchronize()
 
     def pipeline(self):
         """Stream the batches through a two-stage software pipeline: the fused demod (HBM-bound

@@ -164,8 +164,10 @@ class BenchStep:
         c.check(c.lib.tetra_synth_wideband(c.handle, self.plan.c, Nw, seed, snr_db, 300.0, _hip.ptr(self.x),
                                            _hip.ptr(cells), _hip.ptr(self.kinds), _hip.ptr(self.payload), None),
                 "synth_wideband")
+        c.synchronize()   # torch's ops below need not share the context's stream
         # every chunk of carrier k uses carrier k's scrambling code
         self.cells = cells.repeat_interleave(self.nchunk).contiguous()
+        torch.cuda.current_stream(device).synchronize()
         c.check(c.lib.tetra_etsi_set_cells(c.handle, _hip.ptr(self.cells), self.C), "set_cells")
         self.y = torch.empty((M, self.nchunk * self.m2, 2), dtype=torch.float32, device=device)
         self.sym = torch.empty((self.C, self.sm, 2), dtype=torch.float32, device=device)
