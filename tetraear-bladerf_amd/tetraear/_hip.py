@@ -189,9 +189,14 @@ class Context:
 
 
 def ctx():
+    """The calling thread's default context.  It runs on the null stream, so its work is ordered with
+    torch's default stream: device tensors torch just made are complete before its kernels read them,
+    and torch's ops see its results (a context of its own -- Context() -- keeps a non-blocking stream
+    of its own, for callers that order their streams themselves, as bench.py and the pipelines do)."""
     c = getattr(_tls, "ctx", None)
     if c is None:
         c = Context()
+        c.check(c.lib.tetra_set_stream(c.handle, None), "tetra_set_stream")
         _tls.ctx = c
     return c
 

@@ -295,8 +295,7 @@ class BenchStep:
             self.y = [torch.empty((C, self.M2, 2), dtype=torch.float32, device=device)]
         self.pipelined = False
         # buffers made by torch (on torch's stream) are complete before any kernel of the context's
-        # stream -- a context of its own (the tests' _hip.ctx()) runs on a stream that does not wait
-        # for torch's
+        # stream -- a Context() of its own runs on a non-blocking stream that does not wait for torch's
         c.synchronize()
         torch.cuda.current_stream(device).synchronize()
 
