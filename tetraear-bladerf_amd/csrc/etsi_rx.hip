@@ -289,7 +289,21 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
     float zr = 0.f, zi = 0.f, am = 0.f;   // CFO sums over this lane's d_j
     int rel = -1;   // SPLIT: progress not yet released (published after the next block's LDS reads)
     float2 pre[4], pre2[4];   // RING: the next block's 256 samples in flight (RING 2: and the one after)
-    auto ld = [&](int n) -> float2 { return n < M2 ? y[n] : make_float2(0.f, 0.f); };
+    // RING: the ring's loads go through a buffer resource over y (past M2 they return 0) and the symbol
+    // stores through one over sp (past smax they are dropped), both without branches: hipcc then
+    // counts the wave's memory operations exactly and waits at a block's ring writes only for the
+    // loads it needs, not (vmcnt(0)) for the previous block's symbol stores as well
+    typedef unsigned u2v __attribute__((ext_vector_type(2)));
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2 *>(y), 0, 8 * M2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t sps = __builtin_amdgcn_make_buffer_rsrc(sp, 0, 8 * smax, 0x00020000);
+    auto ld = [&](int n) -> float2 {
+        if constexpr (RING > 0) {
+            const u2v v = __builtin_amdgcn_raw_buffer_load_b64(yrs, 8 * n, 0, 0);
+            return make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
+        } else {
+            return n < M2 ? y[n] : make_float2(0.f, 0.f);
+        }
+    };
     if constexpr (RING > 0) {
 #pragma unroll
         for (int u = 0; u < 5; ++u) ring[64 * u + lane] = ld(64 * u + lane);
@@ -364,8 +378,12 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
                     am += sqrtf(fmaf(xr, xr, xi * xi));
                 }
             }
-            sp[S + lane] = on;
+            if constexpr (RING == 0) sp[S + lane] = on;
         }
+        // RING: every lane stores (a lane past nv stores 0 at S + lane >= the final S, or nothing past smax)
+        if constexpr (RING > 0)
+            __builtin_amdgcn_raw_buffer_store_b64(u2v{__float_as_uint(on.x), __float_as_uint(on.y)}, sps, 8 * (S + lane),
+                                                  0, 0);
         if (nv > 0) {
             float E = ev, W = pw;
             wave_sum2(E, W);

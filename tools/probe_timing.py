@@ -27,9 +27,8 @@ def main():
     torch.cuda.synchronize(dev)
     C, m2, sm = st.C, st.m2, st.sm
     diag = torch.zeros((C, 4), dtype=torch.float32, device=dev)
-    forms = [("RING=1 LEAN=1", {"TETRA_TIMING_RING": "1", "TETRA_TIMING_LEAN": "1"}),
-             ("RING=1 LEAN=0", {"TETRA_TIMING_RING": "1", "TETRA_TIMING_LEAN": "0"}),
-             ("RING=0 LEAN=1", {"TETRA_TIMING_RING": "0", "TETRA_TIMING_LEAN": "1"})]
+    forms = [(f"RING={r} LEAN={l}", {"TETRA_TIMING_RING": r, "TETRA_TIMING_LEAN": l})
+             for r, l in (("0", "1"), ("1", "1"), ("2", "1"), ("0", "0"))]
     for name, env in forms:
         os.environ.update(env)
         for probe in ("0", "1", "0", "1"):
