@@ -756,7 +756,9 @@ struct ResampUse {
     }
 };
 
-template <int UP, int DOWN, int Q, bool ROT, bool WT = false>
+// POL >= 0: y stored through a buffer resource over the whole output with that cache policy (2 nt,
+// 16 sc1: written through to memory as stored; the host checks 8 M n_keep < 2^31)
+template <int UP, int DOWN, int Q, bool ROT, bool WT = false, int POL = -1>
 __global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict__ Y, int M, int nblk,
                                                         const float *__restrict__ gU, float2 *__restrict__ y,
                                                         int n_keep) {
@@ -834,9 +836,22 @@ __global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict
         for (int o = 0; o < UP; ++o) tile[lane * (OT + 1) + wv * UP + o] = make_float2(acc[o].x, acc[o].y);
         __syncthreads();
         const int k0 = blockIdx.x * RS_C, n0 = blockIdx.y * OT;
-        for (int e = tid; e < RS_C * OT; e += 256) {
-            const int c = e / OT, o = e - c * OT, kk = k0 + c, n = n0 + o;
-            if (kk < M && n < n_keep) y[(size_t)kk * n_keep + n] = tile[c * (OT + 1) + o];
+        if constexpr (POL >= 0) {
+            typedef unsigned u2v __attribute__((ext_vector_type(2)));
+            const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(y, 0, 8 * M * n_keep, 0x00020000);
+            for (int e = tid; e < RS_C * OT; e += 256) {
+                const int c = e / OT, o = e - c * OT, kk = k0 + c, n = n0 + o;
+                if (kk < M && n < n_keep) {
+                    const float2 v = tile[c * (OT + 1) + o];
+                    __builtin_amdgcn_raw_buffer_store_b64(u2v{__float_as_uint(v.x), __float_as_uint(v.y)}, yr,
+                                                          8 * (kk * n_keep + n), 0, POL);
+                }
+            }
+        } else {
+            for (int e = tid; e < RS_C * OT; e += 256) {
+                const int c = e / OT, o = e - c * OT, kk = k0 + c, n = n0 + o;
+                if (kk < M && n < n_keep) y[(size_t)kk * n_keep + n] = tile[c * (OT + 1) + o];
+            }
         }
     }
 }
@@ -1041,9 +1056,19 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
         // TETRA_WB_RESAMP_WT=1: per-wave transposing tiles (k_pfb_resamp_fix WT; same-box A/B)
         const char *de = getenv("TETRA_WB_RESAMP_WT");
         const bool wt = de && atoi(de) == 1;
+        // TETRA_WB_RESAMP_POL=nt|sc1: y stores with that cache policy (same-box A/B)
+        const char *pe = getenv("TETRA_WB_RESAMP_POL");
+        const int pol = !pe || (size_t)M * n_keep * 8 >= ((size_t)1 << 31) ? -1
+                        : (!strcmp(pe, "nt") ? 2 : (!strcmp(pe, "sc1") ? 16 : -1));
         if (fix36 && wt)   // D = M / 2: always the fused analysis, Y rotated there
             hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false, true>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk,
                                gu, yd, (int)n_keep);
+        else if (fix36 && pol == 2)
+            hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false, false, 2>), gr, dim3(256), 0, ctx->stream, u, M,
+                               (int)nblk, gu, yd, (int)n_keep);
+        else if (fix36 && pol == 16)
+            hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false, false, 16>), gr, dim3(256), 0, ctx->stream, u, M,
+                               (int)nblk, gu, yd, (int)n_keep);
         else if (fix36)
             hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk, gu,
                                yd, (int)n_keep);
