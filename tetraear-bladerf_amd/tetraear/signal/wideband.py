@@ -192,7 +192,15 @@ class BenchStep:
         import torch
         dev = self.x.device
         self.back = _hip.Context()
-        self.s_front = torch.cuda.current_stream(dev)
+        # same-box A/B knobs: TETRA_WB_FRONT_PRIO=1 runs the channeliser on a high-priority stream of
+        # its own; TETRA_WB_WF_BACK=1 moves the waterfall rows to the back stream
+        self.wf_back = os.environ.get("TETRA_WB_WF_BACK") == "1"
+        if os.environ.get("TETRA_WB_FRONT_PRIO") == "1":
+            self.s_front = torch.cuda.Stream(device=dev, priority=-1)
+            self.c.check(self.c.lib.tetra_set_stream(self.c.handle, ctypes.c_void_p(self.s_front.cuda_stream)),
+                         "set_stream")
+        else:
+            self.s_front = torch.cuda.current_stream(dev)
         self.s_back = torch.cuda.Stream(device=dev)
         self.back.check(self.back.lib.tetra_set_stream(self.back.handle, ctypes.c_void_p(self.s_back.cuda_stream)),
                         "set_stream")
@@ -209,13 +217,19 @@ class BenchStep:
     def contexts(self):
         return [self.c] + ([self.back] if self.pipelined else [])
 
-    def _front(self, c, y):
+    def _waterfall(self, c):
         c.check(c.lib.tetra_waterfall(c.handle, _hip.ptr(self.x), _hip.TETRA_CF32, 1, self.Nw, 2048, 2048, self.nfr,
                                       _hip.ptr(self.wf)), "waterfall")
+
+    def _front(self, c, y):
+        if not (self.pipelined and self.wf_back):
+            self._waterfall(c)
         c.check(c.lib.tetra_channelize(c.handle, self.plan.c, _hip.ptr(self.x), self.Nw, _hip.ptr(y),
                                        self.nchunk * self.m2), "channelize")
 
     def _back(self, c, y):
+        if self.pipelined and self.wf_back:
+            self._waterfall(c)
         c.check(c.lib.tetra_etsi_timing(c.handle, self.etsi, _hip.ptr(y), self.C, self.m2, _hip.ptr(self.sym),
                                         _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.sm, None),
                 "etsi_timing")
