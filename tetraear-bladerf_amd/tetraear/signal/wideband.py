@@ -184,17 +184,19 @@ class BenchStep:
         self.pipelined = False
 
     def pipeline(self):
-        """Two-stage software pipeline over consecutive captures: waterfall + channeliser of step k+1
-        on the front stream while the per-carrier timing + lower MAC of step k run on a back stream
-        (its own context).  The carrier samples y are what crosses the streams: double-buffered,
+        """Two-stage software pipeline over consecutive captures: the channeliser of step k+1 on the
+        front stream while the waterfall rows and the per-carrier timing + lower MAC of step k run on a
+        back stream (its own context).  The carrier samples y are what crosses the streams: double-buffered,
         each stage waits only on the event that protects its buffer.  Every step still does the
         whole chain."""
         import torch
         dev = self.x.device
         self.back = _hip.Context()
-        # same-box A/B knobs: TETRA_WB_FRONT_PRIO=1 runs the channeliser on a high-priority stream of
-        # its own; TETRA_WB_WF_BACK=1 moves the waterfall rows to the back stream
-        self.wf_back = os.environ.get("TETRA_WB_WF_BACK") == "1"
+        # the waterfall rows go on the back stream, beside the channeliser (the front stream, the longer
+        # of the two): 0.436 against 0.446 ms per step, same box (profiles/r04_ab_wideband_streams.txt);
+        # TETRA_WB_WF_BACK=0 keeps them on the front.  TETRA_WB_FRONT_PRIO=1 runs the channeliser on a
+        # high-priority stream of its own (no gain)
+        self.wf_back = os.environ.get("TETRA_WB_WF_BACK", "1") == "1"
         if os.environ.get("TETRA_WB_FRONT_PRIO") == "1":
             self.s_front = torch.cuda.Stream(device=dev, priority=-1)
             self.c.check(self.c.lib.tetra_set_stream(self.c.handle, ctypes.c_void_p(self.s_front.cuda_stream)),
