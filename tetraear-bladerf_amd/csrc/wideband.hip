@@ -499,7 +499,9 @@ __global__ __launch_bounds__(A2_T, (A2Cfg<P, DM>::WAVES)) void k_pfb_analysis2(c
 // and stages 2-3's twiddles, 52.5 KB (TREG: stage 4's 640 twiddles are four registers per thread, and
 // the VGPRs are held to 168): three workgroups per CU at P <= 5.  !TREG: all twiddles in LDS, 57.6 KB,
 // two workgroups per CU (TETRA_WB_ANALYSIS=3, same-box A/B).
-template <int P, int DM, bool TREG = true>
+// PROBE (timing-only builds, wrong results: TETRA_WB_ANALYSIS_PROBE): 1 the loader issues no global
+// loads (it writes whatever its registers hold), 2 no Y stores -- what each costs of the kernel's time
+template <int P, int DM, bool TREG = true, int PROBE = 0>
 __global__ __launch_bounds__(AN_T, (TREG && P <= 5 ? 3 : 2)) void k_pfb_analysis1(const float4 *__restrict__ x2, int nblk, int JB,
                                                            const float *__restrict__ h,
                                                            const float2 *__restrict__ twg, float2 *__restrict__ Y) {
@@ -534,6 +536,7 @@ __global__ __launch_bounds__(AN_T, (TREG && P <= 5 ? 3 : 2)) void k_pfb_analysis
         int rpos = rwrap<RING / 2>(L / 2 + l);                 // ring pair position for block 1
         float4 sl[AF1][NLD1];
         auto fetch = [&](float4 (&v)[NLD1], int jj) __attribute__((always_inline)) {
+            if constexpr (PROBE == 1) return;
 #pragma unroll
             for (int m = 0; m < NLD1; ++m) {
                 const nt_f4 w = __builtin_amdgcn_raw_buffer_load_b128(xr, vo + 1024 * m, 8 * D * jj, 0);
@@ -553,6 +556,12 @@ __global__ __launch_bounds__(AN_T, (TREG && P <= 5 ? 3 : 2)) void k_pfb_analysis
             __syncthreads();   // after stage 3
         };
         static_assert(AF1 == 4, "loader unroll");
+        if constexpr (PROBE == 1) {
+#pragma unroll
+            for (int a = 0; a < AF1; ++a)
+#pragma unroll
+                for (int m = 0; m < NLD1; ++m) sl[a][m] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
         fetch(sl[0], 1);
         fetch(sl[1], 2);
         fetch(sl[2], 3);
@@ -649,8 +658,11 @@ __global__ __launch_bounds__(AN_T, (TREG && P <= 5 ? 3 : 2)) void k_pfb_analysis
                 const float a = (q & 1) ? v[r].y : v[r].x, b4 = (q & 1) ? -v[r].x : v[r].y;
                 typedef unsigned u2v __attribute__((ext_vector_type(2)));
                 const float2 o = (q & 2) ? make_float2(-a, -b4) : make_float2(a, b4);
-                __builtin_amdgcn_raw_buffer_store_b64(u2v{__float_as_uint(o.x), __float_as_uint(o.y)}, yr, 8 * k, 0,
-                                                      2 /* nt */);
+                if constexpr (PROBE == 2)
+                    asm volatile("" ::"v"(o.x), "v"(o.y));
+                else
+                    __builtin_amdgcn_raw_buffer_store_b64(u2v{__float_as_uint(o.x), __float_as_uint(o.y)}, yr, 8 * k, 0,
+                                                          2 /* nt */);
             }
         }
     }
@@ -1005,6 +1017,15 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
             const int per_cu = treg && P->P <= 5 ? 3 : 2;
             const int jb = std::max<int>(16, (int)((nblk + per_cu * 256 - 1) / (per_cu * 256)));
             const unsigned grid = (unsigned)((nblk + jb - 1) / jb);
+            const char *pe = getenv("TETRA_WB_ANALYSIS_PROBE");
+            const int probe = pe ? atoi(pe) : 0;
+            if (probe == 1 && P->P == 5 && treg)
+                hipLaunchKernelGGL((k_pfb_analysis1<5, 2, true, 1>), dim3(grid), dim3(AN_T), 0, ctx->stream,
+                                   (const float4 *)xd, (int)nblk, jb, taps, (const float2 *)(taps + tw_off), u);
+            else if (probe == 2 && P->P == 5 && treg)
+                hipLaunchKernelGGL((k_pfb_analysis1<5, 2, true, 2>), dim3(grid), dim3(AN_T), 0, ctx->stream,
+                                   (const float4 *)xd, (int)nblk, jb, taps, (const float2 *)(taps + tw_off), u);
+            else
             switch (P->P * 2 + (treg ? 1 : 0)) {
 #define AN(PP, TR) case PP * 2 + TR: hipLaunchKernelGGL((k_pfb_analysis1<PP, 2, TR>), dim3(grid), dim3(AN_T), 0, ctx->stream, (const float4 *)xd, (int)nblk, jb, taps, (const float2 *)(taps + tw_off), u); break;
                 AN(4, 0) AN(5, 0) AN(6, 0) AN(4, 1) AN(5, 1) AN(6, 1)
