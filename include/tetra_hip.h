@@ -283,7 +283,9 @@ int tetra_etsi_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *plan, const void 
 /* Timing recovery + differential decision: y [C][M2] ->
  *   soft [C][smax] cf32 symbol-spaced samples (the ETSI `.symbols`), softbits [C][2*smax] int8
  *   (>0: bit 0), hard [C][smax] dibit symbols 0..3 (count nsym-1), nsym [C],
- *   diag [C][4] (timing phase, final Gardner correction, CFO rotation re/im) or NULL. */
+ *   diag [C][4] (timing phase, final Gardner correction, CFO rotation re/im) or NULL.
+ *   Entries past a channel's nsym (symbols) and nsym-1 (soft bits, dibits) are unspecified.
+ *   TETRA_TIMING_PROBE=1 (diagnostic): diag holds four 32-bit wall-clock stamps per channel instead. */
 int tetra_etsi_timing(tetra_ctx *ctx, const tetra_etsi_plan *plan, const void *y, size_t C, size_t M2,
                       void *soft, int8_t *softbits, uint8_t *hard, int32_t *nsym, size_t smax, float *diag);
 /* Fused demod (chanfilt + timing) over a batch. */

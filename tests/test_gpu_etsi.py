@@ -961,8 +961,14 @@ def test_generic_kernel_equals_fused_at_2400k(fmt):
                  np.zeros(5, np.int32))
             c.check(c.lib.tetra_demod_etsi_fmt(c.handle, p, _hip.ptr(x), f, 5, N, *[_hip.ptr(a) for a in o], sm, None))
             outs.append(o)
-        for a, b in zip(*outs):
-            assert np.array_equal(a, b), N
+        # equal over what the calls define (the symbols [0, nsym), the decisions [0, nsym - 1)): past
+        # nsym the outputs are unspecified (k_timing writes zeros there, the fused tail nothing)
+        assert np.array_equal(outs[0][3], outs[1][3]), N
+        for ch in range(5):
+            n = int(outs[0][3][ch])
+            assert np.array_equal(outs[0][0][ch, :n], outs[1][0][ch, :n]), (N, ch)
+            assert np.array_equal(outs[0][1][ch, :2 * (n - 1)], outs[1][1][ch, :2 * (n - 1)]), (N, ch)
+            assert np.array_equal(outs[0][2][ch, :n - 1], outs[1][2][ch, :n - 1]), (N, ch)
 
 
 def test_unsupported_rate_never_raises_into_the_loop(caplog):
