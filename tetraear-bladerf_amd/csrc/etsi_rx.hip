@@ -636,6 +636,7 @@ struct TimingOut {
     int32_t *nsym;
     float4 *diag;
     int smax;
+    int probe;   // TETRA_TIMING_PROBE: diag holds wall-clock stamps (start, tail start, tracking done, end)
 };
 
 // LDS -> global copy of n bytes by the workgroup's 256 threads, as device-scope (sc1) stores
@@ -684,8 +685,11 @@ struct TailStage {
 // shared by all four waves (the rotation and scale go through LDS, *tro).
 __device__ __forceinline__ void timing_tail(const float2 *ly, float2 *scr, const TimingOut &to, int M2, int ch,
                                             int tid, TrackOut *tro, int *prog, const TailStage *stage = nullptr,
-                                            float *om = nullptr) {
+                                            float *om = nullptr, uint32_t t0 = 0) {
     const size_t so = (size_t)ch * to.smax;
+    const bool probe = to.probe && to.diag;
+    uint32_t t1 = 0, t2 = 0;
+    if (probe && tid == 0) t1 = (uint32_t)wall_clock64();
     if (om && M2 >= 16) om[tid] = om_part(ly, M2, tid >> 6, tid & 63);   // the four Oerder-Meyr parts at once
     if (tid == 0) *prog = 0;
     __syncthreads();
@@ -699,15 +703,24 @@ __device__ __forceinline__ void timing_tail(const float2 *ly, float2 *scr, const
             tro->base = o.base;
             tro->delta = o.delta;
             to.nsym[ch] = o.S;
+            if (probe) t2 = (uint32_t)wall_clock64();
         }
     } else if (tid < 128) {
         cfo_consumer(scr, to.soft_scale, prog, tro, tid & 63);
     }
     __syncthreads();
     const TrackOut o = *tro;
-    if (tid == 0 && to.diag && M2 >= 16) to.diag[ch] = make_float4(o.base, o.delta, o.rr, o.ri);
+    if (tid == 0 && to.diag && M2 >= 16 && !probe) to.diag[ch] = make_float4(o.base, o.delta, o.rr, o.ri);
+    auto stamp = [&]() {
+        if (probe && tid == 0) {
+            __builtin_amdgcn_s_waitcnt(0);
+            const uint32_t t3 = (uint32_t)wall_clock64();
+            to.diag[ch] = make_float4(__uint_as_float(t0), __uint_as_float(t1), __uint_as_float(t2), __uint_as_float(t3));
+        }
+    };
     if (!stage) {
         timing_decide(o, scr, to.softbits + 2 * so, to.hard + so, tid >> 6, 4, tid & 63);
+        stamp();
         return;
     }
     timing_decide(o, scr, stage->sb, stage->hard, tid >> 6, 4, tid & 63);
@@ -717,6 +730,7 @@ __device__ __forceinline__ void timing_tail(const float2 *ly, float2 *scr, const
     copy_out(reinterpret_cast<uint8_t *>(to.softbits + 2 * so), reinterpret_cast<const uint8_t *>(stage->sb), 2 * nd,
              tid);
     copy_out(to.hard + so, stage->hard, nd, tid);
+    stamp();
 }
 
 // SC16 is held to 128 VGPRs: four workgroups per CU (its LDS allows four; at 158-161 VGPRs it ran at
@@ -1276,6 +1290,7 @@ __global__ __launch_bounds__(256, (YG ? 3 : 2)) void k_chanfilt_r(const In *__re
     float2 *lin_all = reinterpret_cast<float2 *>(img_all + 4 * IMGB);          // 4 stage-1 buffers
     float2 *seam = lin_all + 4 * LR;
     const int ch = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const uint32_t t_start = FUSE && to.probe && tid == 0 ? (uint32_t)wall_clock64() : 0u;
     float *yb = YG ? reinterpret_cast<float *>(y + (size_t)ch * M2) : reinterpret_cast<float *>(seam + 3 * SEAM);
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     uint8_t *img = img_all + wv * IMGB;
@@ -1491,7 +1506,7 @@ __global__ __launch_bounds__(256, (YG ? 3 : 2)) void k_chanfilt_r(const In *__re
         const TailStage st{reinterpret_cast<float2 *>(R + o_om + 1024), reinterpret_cast<int8_t *>(R + o_sb), R + o_hd};
         int *prog = reinterpret_cast<int *>(tro + 1);
         timing_tail(reinterpret_cast<const float2 *>(yb), reinterpret_cast<float2 *>(R), to, M2, ch, tid, tro, prog,
-                    &st, reinterpret_cast<float *>(R + o_om));
+                    &st, reinterpret_cast<float *>(R + o_om), t_start);
     } else {
         copy_out(reinterpret_cast<uint8_t *>(y + (size_t)ch * M2), reinterpret_cast<const uint8_t *>(yb), 8 * M2, tid);
     }
@@ -2386,7 +2401,7 @@ int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *i
         float2 *ys = nullptr;   // k_chanfilt<uint2>: y's round trip
         if (fmt == TETRA_SC16 && !per_wave(fmt, M2, N) && !(ys = (float2 *)ws(ctx, S_W3, C * (size_t)M2 * 8)))
             return st.finish();
-        const TimingOut to{P->gain, P->soft_scale, (float2 *)so, sbo, ho, no, (float4 *)dg, (int)smax};
+        const TimingOut to{P->gain, P->soft_scale, (float2 *)so, sbo, ho, no, (float4 *)dg, (int)smax, timing_probe()};
         rc = launch_chanfilt(ctx, P, x, fmt, C, N, M1, M2, ys, &to);
         if (rc) return rc;
         return st.finish();
