@@ -637,8 +637,6 @@ struct TimingOut {
     float4 *diag;
     int smax;
     int probe;   // TETRA_TIMING_PROBE: diag holds wall-clock stamps (start, tail start, tracking done, end)
-    int pf_step; // > 0: during the tail, waves 2-3 read the first pf_bytes of each quarter of channel
-    int pf_bytes;//   ch + pf_step into the caches (the workgroup dispatched after this one)
 };
 
 // LDS -> global copy of n bytes by the workgroup's 256 threads, as device-scope (sc1) stores
@@ -685,15 +683,9 @@ struct TailStage {
 // The fused demod's timing stage for channel ch on y in LDS (ly), after the workgroup's last barrier:
 // the tracking is the serial tail (wave 0, prioritised on its SIMD); the decision pass after it is
 // shared by all four waves (the rotation and scale go through LDS, *tro).
-struct NoExtra {
-    __device__ void operator()(int) const {}
-};
-// extra(tid): run by waves 2-3 while wave 0 tracks and wave 1 sums the CFO (the fused demod's
-// prefetch of the next channel, TETRA_DEMOD_PREFETCH)
-template <typename Extra = NoExtra>
 __device__ __forceinline__ void timing_tail(const float2 *ly, float2 *scr, const TimingOut &to, int M2, int ch,
                                             int tid, TrackOut *tro, int *prog, const TailStage *stage = nullptr,
-                                            float *om = nullptr, uint32_t t0 = 0, const Extra &extra = Extra{}) {
+                                            float *om = nullptr, uint32_t t0 = 0) {
     const size_t so = (size_t)ch * to.smax;
     const bool probe = to.probe && to.diag;
     uint32_t t1 = 0, t2 = 0;
@@ -715,8 +707,6 @@ __device__ __forceinline__ void timing_tail(const float2 *ly, float2 *scr, const
         }
     } else if (tid < 128) {
         cfo_consumer(scr, to.soft_scale, prog, tro, tid & 63);
-    } else {
-        extra(tid);
     }
     __syncthreads();
     const TrackOut o = *tro;
@@ -1515,33 +1505,8 @@ __global__ __launch_bounds__(256, (YG ? 3 : 2)) void k_chanfilt_r(const In *__re
         const int o_sb = (8 * sm + 15) & ~15, o_hd = o_sb + ((2 * sm + 15) & ~15), o_om = o_hd + ((sm + 15) & ~15);
         const TailStage st{reinterpret_cast<float2 *>(R + o_om + 1024), reinterpret_cast<int8_t *>(R + o_sb), R + o_hd};
         int *prog = reinterpret_cast<int *>(tro + 1);
-        // TETRA_DEMOD_PREFETCH (A/B): waves 2-3 are idle while wave 0 tracks; they read the starts of
-        // the quarters of channel ch + pf_step -- the workgroup the hardware dispatches about when
-        // this one retires -- so its stream begins from L2 / MALL instead of HBM
-        auto pre = [&](int t) __attribute__((always_inline)) {
-            const int nx = ch + to.pf_step;
-            if (to.pf_step <= 0 || nx >= (int)gridDim.x) return;
-            const int l = t - 128;   // 0 .. 127: two waves
-            typedef unsigned u4v __attribute__((ext_vector_type(4)));
-            u4v acc = {0u, 0u, 0u, 0u};
-            for (int q = 0; q < nw; ++q) {
-                const long qs = 10L * 10 * min(q * UQ, UT);   // quarter q's first sample
-                const uint8_t *qp = reinterpret_cast<const uint8_t *>(iq) + ((size_t)nx * N + qs) * BPS;
-                const int nb = min(to.pf_bytes, (int)((N - qs) * BPS));
-                const __amdgpu_buffer_rsrc_t pr =
-                    __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(qp), 0, nb, 0x00020000);
-                for (int o0 = 16 * l; o0 < nb; o0 += 16 * 128 * 8) {
-                    u4v v[8];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) v[u] = __builtin_amdgcn_raw_buffer_load_b128(pr, o0 + 16 * 128 * u, 0, 0);
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) acc ^= v[u];
-                }
-            }
-            asm volatile("" ::"v"(acc.x), "v"(acc.y), "v"(acc.z), "v"(acc.w));
-        };
         timing_tail(reinterpret_cast<const float2 *>(yb), reinterpret_cast<float2 *>(R), to, M2, ch, tid, tro, prog,
-                    &st, reinterpret_cast<float *>(R + o_om), t_start, pre);
+                    &st, reinterpret_cast<float *>(R + o_om), t_start);
     } else {
         copy_out(reinterpret_cast<uint8_t *>(y + (size_t)ch * M2), reinterpret_cast<const uint8_t *>(yb), 8 * M2, tid);
     }
@@ -2436,13 +2401,7 @@ int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *i
         float2 *ys = nullptr;   // k_chanfilt<uint2>: y's round trip
         if (fmt == TETRA_SC16 && !per_wave(fmt, M2, N) && !(ys = (float2 *)ws(ctx, S_W3, C * (size_t)M2 * 8)))
             return st.finish();
-        // TETRA_DEMOD_PREFETCH=<KB per quarter> (A/B): the tail prefetch of the next dispatched channel
-        const char *pfe = getenv("TETRA_DEMOD_PREFETCH");
-        const int pfb = pfe ? 1024 * atoi(pfe) : 0;
-        int ncu = 256;
-        if (pfb > 0) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device);
-        const TimingOut to{P->gain, P->soft_scale, (float2 *)so, sbo, ho, no, (float4 *)dg, (int)smax, timing_probe(),
-                           pfb > 0 ? 2 * ncu : 0, pfb};
+        const TimingOut to{P->gain, P->soft_scale, (float2 *)so, sbo, ho, no, (float4 *)dg, (int)smax, timing_probe()};
         rc = launch_chanfilt(ctx, P, x, fmt, C, N, M1, M2, ys, &to);
         if (rc) return rc;
         return st.finish();
