@@ -564,9 +564,11 @@ static int timing_probe() {
     const char *e = getenv("TETRA_TIMING_PROBE");
     return e && atoi(e) == 1;
 }
-static timing_fn timing_kernel() {
+static timing_fn timing_kernel(size_t M2, size_t smax) {
     const char *r = getenv("TETRA_TIMING_RING"), *o = getenv("TETRA_TIMING_LEAN");
-    const int ring = r ? atoi(r) : 1;
+    // the ring form addresses y and the symbols through buffer resources (32-bit byte ranges)
+    const bool fits = 8 * M2 < ((size_t)1 << 31) && 8 * smax < ((size_t)1 << 31);
+    const int ring = !fits ? 0 : (r ? atoi(r) : 1);
     const bool lean = !(o && atoi(o) == 0);
     if (ring <= 0) return lean ? k_timing<0, true> : k_timing<0, false>;
     if (ring == 1) return lean ? k_timing<1, true> : k_timing<1, false>;
@@ -2364,7 +2366,7 @@ int tetra_etsi_timing(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *y, s
     if (!yd || !so || !sbo || !ho || !no || !dscr) return st.finish();
     {
         PROF(ctx, "etsi_timing");
-        hipLaunchKernelGGL(timing_kernel(), dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yd, (int)M2, P->gain,
+        hipLaunchKernelGGL(timing_kernel(M2, smax), dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yd, (int)M2, P->gain,
                            P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg, timing_probe());
     }
     return st.finish();
@@ -2413,7 +2415,7 @@ int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *i
     if (rc) return rc;
     {
         PROF(ctx, "etsi_timing");
-        hipLaunchKernelGGL(timing_kernel(), dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yb, (int)M2, P->gain,
+        hipLaunchKernelGGL(timing_kernel(M2, smax), dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yb, (int)M2, P->gain,
                            P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg, timing_probe());
     }
     return st.finish();
