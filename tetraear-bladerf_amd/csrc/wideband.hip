@@ -317,6 +317,13 @@ template <int R> __device__ __forceinline__ int rwrap(int i) {   // i in (-R, 2R
         return i >= R ? i - R : i;
     }
 }
+template <int R> __device__ __forceinline__ int rwrap_lo(int i) {   // i in (-R, R) -> [0, R)
+    if constexpr ((R & (R - 1)) == 0) {
+        return i & (R - 1);
+    } else {
+        return i < 0 ? i + R : i;
+    }
+}
 
 template <int P, int DM>
 __global__ __launch_bounds__(A2_T, (A2Cfg<P, DM>::WAVES)) void k_pfb_analysis2(const float4 *__restrict__ x2, int nblk,
@@ -325,6 +332,7 @@ __global__ __launch_bounds__(A2_T, (A2Cfg<P, DM>::WAVES)) void k_pfb_analysis2(c
                                                                              float2 *__restrict__ Y) {
     using Cf = A2Cfg<P, DM>;
     constexpr int M = Cf::M, D = Cf::D, L = Cf::L, RING = Cf::RING, NLD = Cf::NLD;
+    static_assert((P - 1) * M + 700 < RING, "a fold read is at most one ring length behind rbase (rwrap_lo)");
     __shared__ float4 ring4[RING / 2];
     __shared__ float2 frb[2][2][AN_FR];   // [block of the pair][ping-pong]
     __shared__ float2 tw[AN_TWN];
@@ -414,7 +422,7 @@ __global__ __launch_bounds__(A2_T, (A2Cfg<P, DM>::WAVES)) void k_pfb_analysis2(c
                 float ar = 0.f, ai = 0.f;
 #pragma unroll
                 for (int p = 0; p < P; ++p) {
-                    const float2 xv = ring[rwrap<RING>(rbase - p * M - 100 * r)];
+                    const float2 xv = ring[rwrap_lo<RING>(rbase - p * M - 100 * r)];
                     ar = fmaf(hr[r][p], xv.x, ar);
                     ai = fmaf(hr[r][p], xv.y, ai);
                 }
@@ -507,6 +515,7 @@ __global__ __launch_bounds__(AN_T, (TREG && P <= 5 ? 3 : 2)) void k_pfb_analysis
                                                            const float2 *__restrict__ twg, float2 *__restrict__ Y) {
     using Cf = A2Cfg<P, DM>;
     constexpr int M = Cf::M, D = Cf::D, L = Cf::L, RING = Cf::RING;
+    static_assert((P - 1) * M + 700 < RING, "a fold read is at most one ring length behind rbase (rwrap_lo)");
     constexpr int NLD1 = (D / 2 + 63) / 64;   // loader float4 loads per lane per block
     constexpr int AF1 = 4;                    // blocks ahead
     __shared__ float4 ring4[RING / 2];
@@ -598,7 +607,7 @@ __global__ __launch_bounds__(AN_T, (TREG && P <= 5 ? 3 : 2)) void k_pfb_analysis
                 float ar = 0.f, ai = 0.f;
 #pragma unroll
                 for (int p = 0; p < P; ++p) {
-                    const float2 xv = ring[rwrap<RING>(rbase - p * M - 100 * r)];
+                    const float2 xv = ring[rwrap_lo<RING>(rbase - p * M - 100 * r)];
                     ar = fmaf(hr[r][p], xv.x, ar);
                     ai = fmaf(hr[r][p], xv.y, ai);
                 }
