@@ -92,12 +92,13 @@ def test_channelize_vs_oracle(capture):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("oversample,form", [(2, "1"), (2, "2"), (2, "3"), (4, "1"), (4, "2")])
+@pytest.mark.parametrize("oversample,form", [(2, "1"), (2, "2"), (2, "3"), (2, "4"), (4, "1"), (4, "2")])
 def test_channelize_every_analysis_form(oversample, form, monkeypatch):
     """Both filter-bank designs (D = M / 2 and M / 4) through each analysis kernel the host can pick
     (TETRA_WB_ANALYSIS: 1 one block per iteration, 2 two blocks, 3 one block with every twiddle in
-    LDS), held to the oracle of that design; a capture long enough for several blocks per workgroup
-    and a ragged tail."""
+    LDS, 4 the fold on three waves), held to the oracle of that design; a capture long enough for
+    several blocks per workgroup and a ragged tail.  Forms 1, 3 and 4 do the same fmas in the same
+    order: their y is also compared with each other bit for bit."""
     from tetraear.signal.wideband import WidebandReceiver, synth_wideband
     monkeypatch.setenv("TETRA_WB_ANALYSIS", form)
     x = synth_wideband(400_037, seed=5, snr_db=20.0, oversample=oversample)[0]
@@ -106,6 +107,20 @@ def test_channelize_every_analysis_form(oversample, form, monkeypatch):
     want = W.channelize(x.astype(np.complex128), d)
     assert y.shape == want.shape
     assert np.abs(y - want).max() <= Y_TOL * np.abs(want).max()
+
+
+@pytest.mark.gpu
+def test_one_block_analysis_forms_bit_identical(monkeypatch):
+    """D = M / 2: the one-block analysis with twiddles in registers (1), in LDS (3), and with the fold
+    on three waves (4) give bit-identical y (same operations, same order)."""
+    from tetraear.signal.wideband import WidebandReceiver, synth_wideband
+    x = synth_wideband(500_003, seed=13, snr_db=20.0, oversample=2)[0]
+    rx = WidebandReceiver(oversample=2)
+    ys = []
+    for form in ("1", "3", "4"):
+        monkeypatch.setenv("TETRA_WB_ANALYSIS", form)
+        ys.append(rx.channelize(x))
+    assert np.array_equal(ys[0], ys[1]) and np.array_equal(ys[0], ys[2])
 
 
 @pytest.mark.gpu

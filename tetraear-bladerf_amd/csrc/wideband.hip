@@ -508,14 +508,19 @@ __global__ __launch_bounds__(A2_T, (A2Cfg<P, DM>::WAVES)) void k_pfb_analysis2(c
 // the VGPRs are held to 168): three workgroups per CU at P <= 5.  !TREG: all twiddles in LDS, 57.6 KB,
 // two workgroups per CU (TETRA_WB_ANALYSIS=3, same-box A/B).
 // PROBE (timing-only builds, wrong results: TETRA_WB_ANALYSIS_PROBE): 1 the loader issues no global
-// loads (it writes whatever its registers hold), 2 no Y stores -- what each costs of the kernel's time
-template <int P, int DM, bool TREG = true, int PROBE = 0>
+// loads (it writes whatever its registers hold), 2 no Y stores -- what each costs of the kernel's time.
+// F3: the fold on all three compute waves (thread t < 192 folds u[t + 192 m], m < 5, into frame X;
+// a barrier; the radix-8 stage reads X) instead of inside the radix-8 butterflies of waves 0-1: stage 1
+// was two thirds of a block's issue time on two of the four SIMDs (profiles/r04_ab_analysis_probe.txt,
+// DESIGN §5.7).  Four barriers per block, fixed frames (X: fold out, stage 2 out; Y: radix-8 out,
+// stage 3 out).  The same fmas in the same order: the same Y.
+template <int P, int DM, bool TREG = true, int PROBE = 0, bool F3 = false>
 __global__ __launch_bounds__(AN_T, (TREG && P <= 5 ? 3 : 2)) void k_pfb_analysis1(const float4 *__restrict__ x2, int nblk, int JB,
                                                            const float *__restrict__ h,
                                                            const float2 *__restrict__ twg, float2 *__restrict__ Y) {
     using Cf = A2Cfg<P, DM>;
     constexpr int M = Cf::M, D = Cf::D, L = Cf::L, RING = Cf::RING;
-    static_assert((P - 1) * M + 700 < RING, "a fold read is at most one ring length behind rbase (rwrap_lo)");
+    static_assert((P - 1) * M + 768 < RING, "a fold read is at most one ring length behind rbase (rwrap_lo)");
     constexpr int NLD1 = (D / 2 + 63) / 64;   // loader float4 loads per lane per block
     constexpr int AF1 = 4;                    // blocks ahead
     __shared__ float4 ring4[RING / 2];
@@ -560,6 +565,7 @@ __global__ __launch_bounds__(AN_T, (TREG && P <= 5 ? 3 : 2)) void k_pfb_analysis
             }
             rpos = rwrap<RING / 2>(rpos + D / 2);
             fetch(v, jj + 1 + AF1);
+            if constexpr (F3) __syncthreads();   // after the fold
             __syncthreads();   // after stage 1
             __syncthreads();   // after stage 2
             __syncthreads();   // after stage 3
@@ -588,19 +594,50 @@ __global__ __launch_bounds__(AN_T, (TREG && P <= 5 ? 3 : 2)) void k_pfb_analysis
         if (jj + 2 < nb) step(sl[2], jj + 2);
         return;
     }
-    float hr[8][P];
-    if (t < 100) {
+    constexpr int NF = F3 ? 5 : 8;   // fold outputs per thread
+    constexpr int TF = F3 ? 192 : 100, SF = F3 ? 192 : 100;   // folding threads, their output stride
+    float hr[NF][P];
+    if (t < TF) {
 #pragma unroll
-        for (int r = 0; r < 8; ++r)
+        for (int r = 0; r < NF; ++r)
 #pragma unroll
-            for (int p = 0; p < P; ++p) hr[r][p] = h[p * M + t + 100 * r];
+            for (int p = 0; p < P; ++p) hr[r][p] = t + SF * r < M ? h[p * M + t + SF * r] : 0.f;
     }
     __syncthreads();
-    int rbase = rwrap<RING>(L - 1 - (t < 100 ? t : 0));   // ring sample of n_j - t, block jj = 0
+    int rbase = rwrap<RING>(L - 1 - (t < TF ? t : 0));   // ring sample of n_j - t, block jj = 0
     for (int j = j0; j < j1; ++j) {
-        float2 *fa = frb[(j - j0) & 1], *fb = frb[((j - j0) & 1) ^ 1];
-        // stage 1 (R = 8, Ns = 1): butterfly t < 100 on u[t + 100 r], folded from the ring
-        if (t < 100) {
+        float2 *fa = F3 ? frb[1] : frb[(j - j0) & 1], *fb = F3 ? frb[0] : frb[((j - j0) & 1) ^ 1];
+        if constexpr (F3) {
+            // the fold: u[i], i = t + 192 r, into fb (X)
+            if (t < 192) {
+#pragma unroll
+                for (int r = 0; r < NF; ++r) {
+                    const int i = t + 192 * r;
+                    if (i < M) {
+                        float ar = 0.f, ai = 0.f;
+#pragma unroll
+                        for (int p = 0; p < P; ++p) {
+                            const float2 xv = ring[rwrap_lo<RING>(rbase - p * M - 192 * r)];
+                            ar = fmaf(hr[r][p], xv.x, ar);
+                            ai = fmaf(hr[r][p], xv.y, ai);
+                        }
+                        fb[an_pad(i)] = make_float2(ar, ai);
+                    }
+                }
+            }
+            rbase = rwrap<RING>(rbase + D);
+            __syncthreads();
+            // stage 1 (R = 8, Ns = 1): butterfly t < 100 on u[t + 100 r] from X, into fa (Y)
+            if (t < 100) {
+                float2 v[8];
+#pragma unroll
+                for (int r = 0; r < 8; ++r) v[r] = fb[an_pad(t + 100 * r)];
+                bdft8(v);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) fa[an_pad(8 * t + r)] = v[r];
+            }
+        } else if (t < 100) {
+            // stage 1 (R = 8, Ns = 1): butterfly t < 100 on u[t + 100 r], folded from the ring
             float2 v[8];
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
@@ -617,7 +654,7 @@ __global__ __launch_bounds__(AN_T, (TREG && P <= 5 ? 3 : 2)) void k_pfb_analysis
 #pragma unroll
             for (int r = 0; r < 8; ++r) fa[an_pad(8 * t + r)] = v[r];
         }
-        rbase = rwrap<RING>(rbase + D);
+        if constexpr (!F3) rbase = rwrap<RING>(rbase + D);
         __syncthreads();
         // stage 2 (R = 4, Ns = 8): 200 butterflies on 192 threads, fa -> fb
 #pragma unroll
@@ -1028,7 +1065,10 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
             const unsigned grid = (unsigned)((nblk + jb - 1) / jb);
             const char *pe = getenv("TETRA_WB_ANALYSIS_PROBE");
             const int probe = pe ? atoi(pe) : 0;
-            if (probe == 1 && P->P == 5 && treg)
+            if (form == 4 && P->P == 5)   // F3: the fold on three waves (same-box A/B)
+                hipLaunchKernelGGL((k_pfb_analysis1<5, 2, true, 0, true>), dim3(grid), dim3(AN_T), 0, ctx->stream,
+                                   (const float4 *)xd, (int)nblk, jb, taps, (const float2 *)(taps + tw_off), u);
+            else if (probe == 1 && P->P == 5 && treg)
                 hipLaunchKernelGGL((k_pfb_analysis1<5, 2, true, 1>), dim3(grid), dim3(AN_T), 0, ctx->stream,
                                    (const float4 *)xd, (int)nblk, jb, taps, (const float2 *)(taps + tw_off), u);
             else if (probe == 2 && P->P == 5 && treg)
