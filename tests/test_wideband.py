@@ -95,10 +95,10 @@ def test_channelize_vs_oracle(capture):
 @pytest.mark.parametrize("oversample,form", [(2, "1"), (2, "2"), (2, "3"), (2, "4"), (4, "1"), (4, "2")])
 def test_channelize_every_analysis_form(oversample, form, monkeypatch):
     """Both filter-bank designs (D = M / 2 and M / 4) through each analysis kernel the host can pick
-    (TETRA_WB_ANALYSIS: 1 one block per iteration, 2 two blocks, 3 one block with every twiddle in
-    LDS, 4 the fold on three waves), held to the oracle of that design; a capture long enough for
-    several blocks per workgroup and a ragged tail.  Forms 1, 3 and 4 do the same fmas in the same
-    order: their y is also compared with each other bit for bit."""
+    (TETRA_WB_ANALYSIS: 1 one block per iteration with the fold on three waves, 2 two blocks, 3 one
+    block with every twiddle in LDS, 4 one block with the fold inside the radix-8 butterflies), held
+    to the oracle of that design; a capture long enough for several blocks per workgroup and a ragged
+    tail."""
     from tetraear.signal.wideband import WidebandReceiver, synth_wideband
     monkeypatch.setenv("TETRA_WB_ANALYSIS", form)
     x = synth_wideband(400_037, seed=5, snr_db=20.0, oversample=oversample)[0]
@@ -111,8 +111,9 @@ def test_channelize_every_analysis_form(oversample, form, monkeypatch):
 
 @pytest.mark.gpu
 def test_one_block_analysis_forms_bit_identical(monkeypatch):
-    """D = M / 2: the one-block analysis with twiddles in registers (1), in LDS (3), and with the fold
-    on three waves (4) give bit-identical y (same operations, same order)."""
+    """D = M / 2: the one-block analysis forms -- the fold on three waves (1, the default), the fold
+    inside the radix-8 butterflies with the twiddles in LDS (3) or in registers (4) -- give
+    bit-identical y (same operations, same order)."""
     from tetraear.signal.wideband import WidebandReceiver, synth_wideband
     x = synth_wideband(500_003, seed=13, snr_db=20.0, oversample=2)[0]
     rx = WidebandReceiver(oversample=2)

@@ -1049,8 +1049,9 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
         PROF(ctx, "wb_analysis");
         // About one round of workgroups when the capture allows, >= 16 blocks each (the L-sample
         // window each workgroup loads first is its overhead).  TETRA_WB_ANALYSIS: 1 one block per
-        // iteration (default), 2 two blocks per iteration (k_pfb_analysis2), 3 (D = M / 2) one block
-        // with every twiddle in LDS -- same-box A/B and the parity tests, which switch it between calls.  The D = M / 2 kernels address the capture
+        // iteration (default), 2 two blocks per iteration (k_pfb_analysis2), 3 / 4 (D = M / 2) one
+        // block with every twiddle in LDS / with the fold inside the radix-8 butterflies -- same-box
+        // A/B and the parity tests, which switch it between calls.  The D = M / 2 kernels address the capture
         // with 32-bit byte offsets.
         const char *fe = getenv("TETRA_WB_ANALYSIS");
         const int form = fe ? atoi(fe) : 1;
@@ -1065,10 +1066,16 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
             const unsigned grid = (unsigned)((nblk + jb - 1) / jb);
             const char *pe = getenv("TETRA_WB_ANALYSIS_PROBE");
             const int probe = pe ? atoi(pe) : 0;
-            if (form == 4 && P->P == 5)   // F3: the fold on three waves (same-box A/B)
-                hipLaunchKernelGGL((k_pfb_analysis1<5, 2, true, 0, true>), dim3(grid), dim3(AN_T), 0, ctx->stream,
-                                   (const float4 *)xd, (int)nblk, jb, taps, (const float2 *)(taps + tw_off), u);
-            else if (probe == 1 && P->P == 5 && treg)
+            // the default: twiddles in registers and the fold on three waves (F3); 4: without F3, 3:
+            // without either (same-box A/B, profiles/r04_ab_analysis_f3_*.txt)
+            const bool f3 = form != 3 && form != 4;
+            if (f3 && probe == 0) {
+                switch (P->P) {
+#define AN(PP) case PP: hipLaunchKernelGGL((k_pfb_analysis1<PP, 2, true, 0, true>), dim3(grid), dim3(AN_T), 0, ctx->stream, (const float4 *)xd, (int)nblk, jb, taps, (const float2 *)(taps + tw_off), u); break;
+                    AN(4) AN(5) AN(6)
+#undef AN
+                }
+            } else if (probe == 1 && P->P == 5 && treg)
                 hipLaunchKernelGGL((k_pfb_analysis1<5, 2, true, 1>), dim3(grid), dim3(AN_T), 0, ctx->stream,
                                    (const float4 *)xd, (int)nblk, jb, taps, (const float2 *)(taps + tw_off), u);
             else if (probe == 2 && P->P == 5 && treg)
