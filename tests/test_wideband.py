@@ -143,6 +143,10 @@ def test_resampler_wave_tiles_equal(oversample, monkeypatch):
     for pol in ("nt", "sc1"):   # the store's cache policy (D = M / 2 kernel): same values
         monkeypatch.setenv("TETRA_WB_RESAMP_POL", pol)
         assert np.array_equal(rx.channelize(x), y0) and np.array_equal(rx.channelize(x, 1001), y0[:, :1001]), pol
+    monkeypatch.delenv("TETRA_WB_RESAMP_POL")
+    if oversample == 2:   # rows loaded in two batches of 24 instead of three of 17: same values
+        monkeypatch.setenv("TETRA_WB_RESAMP_RB1", "1")
+        assert np.array_equal(rx.channelize(x), y0) and np.array_equal(rx.channelize(x, 1001), y0[:, :1001])
 
 
 @pytest.mark.gpu

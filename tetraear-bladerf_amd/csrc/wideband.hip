@@ -816,7 +816,8 @@ struct ResampUse {
 
 // POL >= 0: y stored through a buffer resource over the whole output with that cache policy (2 nt,
 // 16 sc1: written through to memory as stored; the host checks 8 M n_keep < 2^31)
-template <int UP, int DOWN, int Q, bool ROT, bool WT = false, int POL = -1>
+// RB: rows loaded per batch (17: three dependent batches per group at UP = 36; RB >= ROWS: one)
+template <int UP, int DOWN, int Q, bool ROT, bool WT = false, int POL = -1, int RB = 17>
 __global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict__ Y, int M, int nblk,
                                                         const float *__restrict__ gU, float2 *__restrict__ y,
                                                         int n_keep) {
@@ -841,7 +842,6 @@ __global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict
     pf2 acc[UP];
 #pragma unroll
     for (int o = 0; o < UP; ++o) acc[o] = pf2{0.f, 0.f};
-    constexpr int RB = 17;   // rows in flight per batch
 #pragma unroll
     for (int i0 = 0; i0 < ROWS; i0 += RB) {
         float2 v[RB];
@@ -1140,6 +1140,9 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
         if (fix36 && wt)   // D = M / 2: always the fused analysis, Y rotated there
             hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false, true>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk,
                                gu, yd, (int)n_keep);
+        else if (fix36 && getenv("TETRA_WB_RESAMP_RB1") && atoi(getenv("TETRA_WB_RESAMP_RB1")) == 1)   // A/B: rows in two batches
+            hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false, false, -1, 24>), gr, dim3(256), 0, ctx->stream, u, M,
+                               (int)nblk, gu, yd, (int)n_keep);
         else if (fix36 && pol == 2)
             hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false, false, 2>), gr, dim3(256), 0, ctx->stream, u, M,
                                (int)nblk, gu, yd, (int)n_keep);
