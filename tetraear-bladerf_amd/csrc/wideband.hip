@@ -817,7 +817,8 @@ struct ResampUse {
 // POL >= 0: y stored through a buffer resource over the whole output with that cache policy (2 nt,
 // 16 sc1: written through to memory as stored; the host checks 8 M n_keep < 2^31)
 // RB: rows loaded per batch (17: three dependent batches per group at UP = 36; RB >= ROWS: one)
-template <int UP, int DOWN, int Q, bool ROT, bool WT = false, int POL = -1, int RB = 17>
+// PRB (timing-only build, TETRA_WB_RESAMP_PROBE=1): no y stores -- what the write-out costs
+template <int UP, int DOWN, int Q, bool ROT, bool WT = false, int POL = -1, int RB = 17, int PRB = 0>
 __global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict__ Y, int M, int nblk,
                                                         const float *__restrict__ gU, float2 *__restrict__ y,
                                                         int n_keep) {
@@ -908,7 +909,12 @@ __global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict
         } else {
             for (int e = tid; e < RS_C * OT; e += 256) {
                 const int c = e / OT, o = e - c * OT, kk = k0 + c, n = n0 + o;
-                if (kk < M && n < n_keep) y[(size_t)kk * n_keep + n] = tile[c * (OT + 1) + o];
+                if constexpr (PRB == 1) {
+                    const float2 v = tile[c * (OT + 1) + o];
+                    asm volatile("" ::"v"(v.x), "v"(v.y));
+                } else if (kk < M && n < n_keep) {
+                    y[(size_t)kk * n_keep + n] = tile[c * (OT + 1) + o];
+                }
             }
         }
     }
@@ -1140,6 +1146,9 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
         if (fix36 && wt)   // D = M / 2: always the fused analysis, Y rotated there
             hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false, true>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk,
                                gu, yd, (int)n_keep);
+        else if (fix36 && getenv("TETRA_WB_RESAMP_PROBE") && atoi(getenv("TETRA_WB_RESAMP_PROBE")) == 1)
+            hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false, false, -1, 17, 1>), gr, dim3(256), 0, ctx->stream, u, M,
+                               (int)nblk, gu, yd, (int)n_keep);
         else if (fix36 && getenv("TETRA_WB_RESAMP_RB1") && atoi(getenv("TETRA_WB_RESAMP_RB1")) == 1)   // A/B: rows in two batches
             hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false, false, -1, 24>), gr, dim3(256), 0, ctx->stream, u, M,
                                (int)nblk, gu, yd, (int)n_keep);
