@@ -540,6 +540,22 @@ __global__ __launch_bounds__(AN_T, (TREG && P <= 5 ? 3 : 2)) void k_pfb_analysis
     const long pr0 = (long)j0 * (D / 2);                      // ring pair 0 = x[j0 D]
     for (int q = t; q < L / 2; q += AN_T)                     // the first block's window
         if (pr0 + q < npr) ring4[q] = x2[pr0 + q];
+    // stage 2's radix-4 butterfly b on the fixed F3 frames (Y -> X); with F3 the loader wave's lanes
+    // 0-7 take butterflies 192-199, so no compute wave runs two
+    auto s2f3 = [&](int b) __attribute__((always_inline)) {
+        const float2 *fa = frb[1];
+        float2 *fb = frb[0];
+        float2 v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fa[an_pad(b + 200 * r)];
+        const int m = b & 7;
+#pragma unroll
+        for (int r = 1; r < 4; ++r) v[r] = c_mul(v[r], tw[AN_TW2 + (r - 1) * 8 + m]);
+        bdft4(v[0], v[1], v[2], v[3]);
+        const int base = (b >> 3) * 32 + m;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) fb[an_pad(base + 8 * r)] = v[r];
+    };
     if (wv == 3) {
         // block jj (>= 1) adds x[L + (j0 + jj - 1) D, + D): D / 2 pairs from relative pair
         // (L + (jj - 1) D) / 2; written during block jj - 1's stage 1 (disjoint from its window)
@@ -567,6 +583,9 @@ __global__ __launch_bounds__(AN_T, (TREG && P <= 5 ? 3 : 2)) void k_pfb_analysis
             fetch(v, jj + 1 + AF1);
             if constexpr (F3) __syncthreads();   // after the fold
             __syncthreads();   // after stage 1
+            if constexpr (F3) {
+                if (l < 8) s2f3(192 + l);
+            }
             __syncthreads();   // after stage 2
             __syncthreads();   // after stage 3
         };
@@ -656,7 +675,10 @@ __global__ __launch_bounds__(AN_T, (TREG && P <= 5 ? 3 : 2)) void k_pfb_analysis
         }
         if constexpr (!F3) rbase = rwrap<RING>(rbase + D);
         __syncthreads();
-        // stage 2 (R = 4, Ns = 8): 200 butterflies on 192 threads, fa -> fb
+        // stage 2 (R = 4, Ns = 8): 200 butterflies on 192 threads, fa -> fb (F3: 192 here, 8 on the loader)
+        if constexpr (F3) {
+            if (t < 192) s2f3(t);
+        } else
 #pragma unroll
         for (int h2 = 0; h2 < 2; ++h2) {
             const int b = t + 192 * h2;
