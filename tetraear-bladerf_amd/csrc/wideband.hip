@@ -634,9 +634,13 @@ __global__ __launch_bounds__(AN_T, (TREG && P <= 5 ? 3 : 2)) void k_pfb_analysis
                     const int i = t + 192 * r;
                     if (i < M) {
                         float ar = 0.f, ai = 0.f;
+                        // e - p M wraps (+ RING) exactly when it is negative: pick the base, then
+                        // subtract (one compare, one select, one subtract per tap)
+                        const int e = rbase - 192 * r;                       // in (-768, RING)
+                        const float2 *ba = ring + e, *bb = ring + e + RING;
 #pragma unroll
                         for (int p = 0; p < P; ++p) {
-                            const float2 xv = ring[rwrap_lo<RING>(rbase - p * M - 192 * r)];
+                            const float2 xv = (e >= p * M ? ba : bb)[-p * M];
                             ar = fmaf(hr[r][p], xv.x, ar);
                             ai = fmaf(hr[r][p], xv.y, ai);
                         }
