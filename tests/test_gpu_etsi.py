@@ -420,31 +420,6 @@ def test_demod_lengths_vs_oracle(N, fmt):
         assert np.array_equal(soft[ch, :2 * max(n - 1, 0)], sbo)
 
 
-@pytest.mark.parametrize("N", [131072, 100000, 262140])
-def test_sc16_global_y_form_bit_exact(N, monkeypatch):
-    """TETRA_SC16_YG=1 (the fused SC16 kernel with y in a global scratch, three workgroups per CU) gives
-    the same symbols, soft bits and hard dibits as the default form and as the oracle; many channels
-    (more than one round of workgroups) and chunk lengths whose wave quarters end mid-tile."""
-    from tetraear.signal.etsi import synth, EtsiReceiver
-    C = 800
-    iq = synth(C, N, seed=21, snr_db=18.0)[0]
-    inp = np.stack([np.round(iq.real * 32768), np.round(iq.imag * 32768)], -1).clip(-32768, 32767).astype(np.int16)
-    monkeypatch.setenv("TETRA_SC16_YG", "0")
-    a = EtsiReceiver().demod_batch(inp)
-    monkeypatch.setenv("TETRA_SC16_YG", "1")
-    b = EtsiReceiver().demod_batch(inp)
-    for u, v in zip(a, b):
-        assert np.array_equal(u, v)
-    hard, soft, sym, ns = b
-    rx = E.Receiver()
-    xs = (inp[..., 0].astype(np.float32) / 32768 + 1j * (inp[..., 1].astype(np.float32) / 32768)).astype(np.complex64)
-    for ch in (0, 401, C - 1):
-        so, sbo, ho, _ = rx.demod(xs[ch])
-        n = int(ns[ch])
-        assert n == len(so) and np.array_equal(sym[ch, :n], so) and np.array_equal(hard[ch, :n - 1], ho)
-        assert np.array_equal(soft[ch, :2 * (n - 1)], sbo)
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("N", [0, 1, 2, 47, 48, 400, 3300, 3301, 3500])
 def test_process_edge_lengths(N):

@@ -125,31 +125,6 @@ def test_one_block_analysis_forms_bit_identical(monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("oversample", [2, 4])
-def test_resampler_wave_tiles_equal(oversample, monkeypatch):
-    """TETRA_WB_RESAMP_WT=1 (per-wave transposing tiles) and TETRA_WB_RESAMP_POL (the stores' cache
-    policy) change only how the resampler's outputs are stored: y is bit-identical to the default
-    form, ragged capture length included."""
-    from tetraear.signal.wideband import WidebandReceiver, synth_wideband
-    x = synth_wideband(300_011, seed=9, snr_db=20.0, oversample=oversample)[0]
-    rx = WidebandReceiver(oversample=oversample)
-    monkeypatch.setenv("TETRA_WB_RESAMP_WT", "0")
-    y0 = rx.channelize(x)
-    monkeypatch.setenv("TETRA_WB_RESAMP_WT", "1")
-    y1 = rx.channelize(x)
-    y2 = rx.channelize(x, 1001)
-    assert np.array_equal(y0, y1) and np.array_equal(y2, y0[:, :1001])
-    monkeypatch.setenv("TETRA_WB_RESAMP_WT", "0")
-    for pol in ("nt", "sc1"):   # the store's cache policy (D = M / 2 kernel): same values
-        monkeypatch.setenv("TETRA_WB_RESAMP_POL", pol)
-        assert np.array_equal(rx.channelize(x), y0) and np.array_equal(rx.channelize(x, 1001), y0[:, :1001]), pol
-    monkeypatch.delenv("TETRA_WB_RESAMP_POL")
-    if oversample == 2:   # rows loaded in two batches of 24 instead of three of 17: same values
-        monkeypatch.setenv("TETRA_WB_RESAMP_RB1", "1")
-        assert np.array_equal(rx.channelize(x), y0) and np.array_equal(rx.channelize(x, 1001), y0[:, :1001])
-
-
-@pytest.mark.gpu
 def test_wideband_timing_bit_exact(capture):
     """From y on the chain is the ETSI one: the GPU timing on the channeliser's own output equals
     oracle/etsi.py on the same y, carrier by carrier."""

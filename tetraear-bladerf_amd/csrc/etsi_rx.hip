@@ -1272,28 +1272,27 @@ __device__ __forceinline__ void fmac_rows(float &ar, float &ai, const float *xr,
     }
 }
 
-// YG (SC16 A/B, TETRA_SC16_YG=1): y goes to a global scratch row (the launch passes it, padded 512
-// samples on both sides for the tail's out-of-range window reads) instead of LDS, and one input tile
-// is prefetched instead of two: 42 KB of LDS and <= 168 VGPRs, three workgroups per CU
-template <typename In, bool FUSE, bool YG = false>
-__global__ __launch_bounds__(256, (YG ? 3 : 2)) void k_chanfilt_r(const In *__restrict__ iq, long N, int M1, int M2,
+// (Round 4 measured and removed a form with y in a global scratch, one tile prefetched and three
+// workgroups per CU for SC16: 0.938 -> 1.05 ms)
+template <typename In, bool FUSE>
+__global__ __launch_bounds__(256, 2) void k_chanfilt_r(const In *__restrict__ iq, long N, int M1, int M2,
                                                        const float *__restrict__ h1, const float *__restrict__ afrag,
                                                        float2 *__restrict__ y, TimingOut to) {
     constexpr bool SC16 = std::is_same<In, uint4>::value;
-    constexpr int BPS = RCfg<In>::bps, PF = YG ? 1 : RCfg<In>::pf, NCH = r_chunks<In>(), NL = (NCH + 63) / 64;
+    constexpr int BPS = RCfg<In>::bps, PF = RCfg<In>::pf, NCH = r_chunks<In>(), NL = (NCH + 63) / 64;
     constexpr int NB = RCfg<In>::nb, TK = r_tk<In>(), TIN = 10 * TK, LR = RCfg<In>::wlr;
     constexpr int ROWK = NB == 1 ? 12 : 28;    // outputs per 16-lane row
     constexpr int RH16 = RHALO * BPS / 16;     // 16-B chunks per halo
     constexpr int IMGB = r_img16<In>() * 16;   // image bytes per wave
     using Pair = typename std::conditional<SC16, uint2, float4>::type;   // two samples
-    __shared__ float4 smem[r_smem4<In>() - (YG ? YLDS / 2 : 0)];
+    __shared__ float4 smem[r_smem4<In>()];
     TrackOut *tro = reinterpret_cast<TrackOut *>(smem);                        // + prog: 2 float4
     uint8_t *img_all = reinterpret_cast<uint8_t *>(smem + 2);                  // 4 wave images
     float2 *lin_all = reinterpret_cast<float2 *>(img_all + 4 * IMGB);          // 4 stage-1 buffers
     float2 *seam = lin_all + 4 * LR;
     const int ch = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const uint32_t t_start = FUSE && to.probe && tid == 0 ? (uint32_t)wall_clock64() : 0u;
-    float *yb = YG ? reinterpret_cast<float *>(y + (size_t)ch * M2) : reinterpret_cast<float *>(seam + 3 * SEAM);
+    float *yb = reinterpret_cast<float *>(seam + 3 * SEAM);
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     uint8_t *img = img_all + wv * IMGB;
     float2 *lin = lin_all + wv * LR;
@@ -2227,15 +2226,6 @@ static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void 
         ctx->coef_etsi_dev = coef;
     }
     const CfKernel kind = chanfilt_kernel(fmt, M2, N, fused != nullptr);
-    // TETRA_SC16_YG=1 (same-box A/B): the fused SC16 kernel with y in a global scratch, three
-    // workgroups per CU; the scratch is padded 512 samples on both sides (the tail's window reads)
-    const char *yge = getenv("TETRA_SC16_YG");
-    float2 *yg = nullptr;
-    if (kind == CF_R_FUSED && fmt == TETRA_SC16 && yge && atoi(yge) == 1) {
-        yg = (float2 *)ws(ctx, S_W3, (C * (size_t)M2 + 1024) * 8);
-        if (!yg) return TETRA_E_NOMEM;
-        yg += 512;
-    }
     PROF(ctx, fused ? "etsi_demod" : "etsi_chanfilt");
     const TimingOut to = fused ? *fused : TimingOut{};
     const dim3 g((unsigned)C), b(256);
@@ -2244,9 +2234,6 @@ static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void 
         if (fmt == TETRA_CF32)
             hipLaunchKernelGGL((k_chanfilt_r<float4, true>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1,
                                (int)M2, coef, coef + 128, y, to);
-        else if (yg)
-            hipLaunchKernelGGL((k_chanfilt_r<uint4, true, true>), g, b, 0, ctx->stream, (const uint4 *)x, (long)N,
-                               (int)M1, (int)M2, coef + 64, coef + 128, yg, to);
         else
             hipLaunchKernelGGL((k_chanfilt_r<uint4, true>), g, b, 0, ctx->stream, (const uint4 *)x, (long)N, (int)M1,
                                (int)M2, coef + 64, coef + 128, y, to);

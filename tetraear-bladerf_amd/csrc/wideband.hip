@@ -821,11 +821,9 @@ __global__ __launch_bounds__(256) void k_pfb_resamp(const float2 *__restrict__ Y
 // Position of tap (row i, output o) in the use-ordered tap table gU (rows ascending, outputs
 // ascending within a row): the n-th FMA of a group reads tap n.  The table sits in LDS (810
 // floats): as scalar loads the compiler hoisted hundreds of taps and spilled SGPRs to VGPR lanes.
-// WT (wave tiles): each wave transposes its own 64 x UP outputs through a 64 x (UP / NS + 1) tile, one
-// part at a time (NS = 3 at UP = 36), and stores them -- 4 x 6.7 KB of LDS instead of the 74 KB
-// workgroup tile, so the VGPRs (116 at UP = 36) set the occupancy: 4 workgroups per CU instead of 2.
-// (Without the workgroup barrier after the FMAs -- or storing straight from registers -- hipcc hoists
-// every tap read of the group and spills.)
+// Measured and removed in round 4: per-wave transposing tiles (4 waves per SIMD instead
+// of 2: no faster), nt / sc1 stores of y (slower), rows in two batches instead of three (noise).
+// Storing straight from registers makes hipcc hoist every tap read of the group and spill.
 template <int UP, int DOWN, int Q>
 struct ResampUse {
     static constexpr int ROWS = (DOWN * (UP - 1)) / UP + Q;
@@ -840,11 +838,8 @@ struct ResampUse {
     }
 };
 
-// POL >= 0: y stored through a buffer resource over the whole output with that cache policy (2 nt,
-// 16 sc1: written through to memory as stored; the host checks 8 M n_keep < 2^31)
-// RB: rows loaded per batch (17: three dependent batches per group at UP = 36; RB >= ROWS: one)
 // PRB (timing-only build, TETRA_WB_RESAMP_PROBE=1): no y stores -- what the write-out costs
-template <int UP, int DOWN, int Q, bool ROT, bool WT = false, int POL = -1, int RB = 17, int PRB = 0>
+template <int UP, int DOWN, int Q, bool ROT, int PRB = 0>
 __global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict__ Y, int M, int nblk,
                                                         const float *__restrict__ gU, float2 *__restrict__ y,
                                                         int n_keep) {
@@ -852,8 +847,8 @@ __global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict
     constexpr U use{};
     constexpr int ROWS = U::ROWS;                       // rows of one output group
     constexpr int OT = 4 * UP;                          // outputs per workgroup (4 waves x one group)
-    constexpr int NS = UP % 3 == 0 && UP > 18 ? 3 : 2, UH = UP / NS;   // WT: parts, outputs per part
-    __shared__ float2 tile[WT ? 4 * RS_C * (UH + 1) : RS_C * (OT + 1)];
+    constexpr int RB = 17;                              // rows in flight per batch
+    __shared__ float2 tile[RS_C * (OT + 1)];
     __shared__ float tapL[use.n];   // taps in use order: each read is a same-address LDS broadcast
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -900,48 +895,17 @@ __global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict
             }
         }
     }
-    if constexpr (WT) {
-        static_assert(UP % NS == 0, "WT splits the group in equal parts");
-        float2 *wt = tile + wv * RS_C * (UH + 1);
-        const int k0 = blockIdx.x * RS_C, n0 = UP * m;
-        __syncthreads();
 #pragma unroll
-        for (int h = 0; h < NS; ++h) {
-#pragma unroll
-            for (int o = 0; o < UH; ++o) wt[lane * (UH + 1) + o] = make_float2(acc[h * UH + o].x, acc[h * UH + o].y);
-            __builtin_amdgcn_wave_barrier();
-            for (int e = lane; e < RS_C * UH; e += 64) {
-                const int c = e / UH, o = e - c * UH, kk = k0 + c, n = n0 + h * UH + o;
-                if (kk < M && n < n_keep) y[(size_t)kk * n_keep + n] = wt[c * (UH + 1) + o];
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-    } else {
-#pragma unroll
-        for (int o = 0; o < UP; ++o) tile[lane * (OT + 1) + wv * UP + o] = make_float2(acc[o].x, acc[o].y);
-        __syncthreads();
-        const int k0 = blockIdx.x * RS_C, n0 = blockIdx.y * OT;
-        if constexpr (POL >= 0) {
-            typedef unsigned u2v __attribute__((ext_vector_type(2)));
-            const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(y, 0, 8 * M * n_keep, 0x00020000);
-            for (int e = tid; e < RS_C * OT; e += 256) {
-                const int c = e / OT, o = e - c * OT, kk = k0 + c, n = n0 + o;
-                if (kk < M && n < n_keep) {
-                    const float2 v = tile[c * (OT + 1) + o];
-                    __builtin_amdgcn_raw_buffer_store_b64(u2v{__float_as_uint(v.x), __float_as_uint(v.y)}, yr,
-                                                          8 * (kk * n_keep + n), 0, POL);
-                }
-            }
-        } else {
-            for (int e = tid; e < RS_C * OT; e += 256) {
-                const int c = e / OT, o = e - c * OT, kk = k0 + c, n = n0 + o;
-                if constexpr (PRB == 1) {
-                    const float2 v = tile[c * (OT + 1) + o];
-                    asm volatile("" ::"v"(v.x), "v"(v.y));
-                } else if (kk < M && n < n_keep) {
-                    y[(size_t)kk * n_keep + n] = tile[c * (OT + 1) + o];
-                }
-            }
+    for (int o = 0; o < UP; ++o) tile[lane * (OT + 1) + wv * UP + o] = make_float2(acc[o].x, acc[o].y);
+    __syncthreads();
+    const int k0 = blockIdx.x * RS_C, n0 = blockIdx.y * OT;
+    for (int e = tid; e < RS_C * OT; e += 256) {
+        const int c = e / OT, o = e - c * OT, kk = k0 + c, n = n0 + o;
+        if constexpr (PRB == 1) {
+            const float2 v = tile[c * (OT + 1) + o];
+            asm volatile("" ::"v"(v.x), "v"(v.y));
+        } else if (kk < M && n < n_keep) {
+            y[(size_t)kk * n_keep + n] = tile[c * (OT + 1) + o];
         }
     }
 }
@@ -1162,35 +1126,15 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
         PROF(ctx, "wb_resamp");
         const dim3 gr((unsigned)((M + RS_C - 1) / RS_C), (unsigned)((n_keep + 4 * P->up - 1) / (4 * P->up)));
         const float *gu = taps + L + P->up * RS_QP;
-        // TETRA_WB_RESAMP_WT=1: per-wave transposing tiles (k_pfb_resamp_fix WT; same-box A/B)
-        const char *de = getenv("TETRA_WB_RESAMP_WT");
-        const bool wt = de && atoi(de) == 1;
-        // TETRA_WB_RESAMP_POL=nt|sc1: y stores with that cache policy (same-box A/B)
-        const char *pe = getenv("TETRA_WB_RESAMP_POL");
-        const int pol = !pe || (size_t)M * n_keep * 8 >= ((size_t)1 << 31) ? -1
-                        : (!strcmp(pe, "nt") ? 2 : (!strcmp(pe, "sc1") ? 16 : -1));
-        if (fix36 && wt)   // D = M / 2: always the fused analysis, Y rotated there
-            hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false, true>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk,
+        // TETRA_WB_RESAMP_PROBE=1 (timing-only, wrong y): the D = M / 2 resampler without its stores
+        const char *pe = getenv("TETRA_WB_RESAMP_PROBE");
+        if (fix36 && pe && atoi(pe) == 1)
+            hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false, 1>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk,
                                gu, yd, (int)n_keep);
-        else if (fix36 && getenv("TETRA_WB_RESAMP_PROBE") && atoi(getenv("TETRA_WB_RESAMP_PROBE")) == 1)
-            hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false, false, -1, 17, 1>), gr, dim3(256), 0, ctx->stream, u, M,
-                               (int)nblk, gu, yd, (int)n_keep);
-        else if (fix36 && getenv("TETRA_WB_RESAMP_RB1") && atoi(getenv("TETRA_WB_RESAMP_RB1")) == 1)   // A/B: rows in two batches
-            hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false, false, -1, 24>), gr, dim3(256), 0, ctx->stream, u, M,
-                               (int)nblk, gu, yd, (int)n_keep);
-        else if (fix36 && pol == 2)
-            hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false, false, 2>), gr, dim3(256), 0, ctx->stream, u, M,
-                               (int)nblk, gu, yd, (int)n_keep);
-        else if (fix36 && pol == 16)
-            hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false, false, 16>), gr, dim3(256), 0, ctx->stream, u, M,
-                               (int)nblk, gu, yd, (int)n_keep);
-        else if (fix36)
+        else if (fix36)   // D = M / 2: always the fused analysis, Y rotated there
             hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk, gu,
                                yd, (int)n_keep);
-        else if (fused && wt)   // Y already carries the mixer rotation
-            hipLaunchKernelGGL((k_pfb_resamp_fix<18, 25, 45, false, true>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk,
-                               gu, yd, (int)n_keep);
-        else if (fused)
+        else if (fused)   // Y already carries the mixer rotation
             hipLaunchKernelGGL((k_pfb_resamp_fix<18, 25, 45, false>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk, gu,
                                yd, (int)n_keep);
         else
