@@ -288,6 +288,15 @@ int tetra_etsi_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *plan, const void 
  *   TETRA_TIMING_PROBE=1 (diagnostic): diag holds four 32-bit wall-clock stamps per channel instead. */
 int tetra_etsi_timing(tetra_ctx *ctx, const tetra_etsi_plan *plan, const void *y, size_t C, size_t M2,
                       void *soft, int8_t *softbits, uint8_t *hard, int32_t *nsym, size_t smax, float *diag);
+/* tetra_etsi_timing for the wideband chain's chunks, with the Oerder-Meyr class sums formed from
+ * the resampler's group partials om (tetra_channelize_om) instead of a pass over y: y [C][M2] is
+ * C / nchunk carrier rows of nchunk consecutive chunks, om [C / nchunk][ngrp] float4 the rows'
+ * partials over groups of U outputs (U a multiple of 4, <= 64; ngrp U >= nchunk M2; M2 a multiple
+ * of 4).  The class sums follow oracle/etsi_oracle.c eo_om_grouped (a summation order of the same
+ * |y|^2 class sums; same outputs as tetra_etsi_timing otherwise; no reference counterpart). */
+int tetra_etsi_timing_om(tetra_ctx *ctx, const tetra_etsi_plan *plan, const void *y, size_t C, size_t M2,
+                         const void *om, size_t nchunk, size_t ngrp, int U, void *soft, int8_t *softbits,
+                         uint8_t *hard, int32_t *nsym, size_t smax, float *diag);
 /* Fused demod (chanfilt + timing) over a batch. */
 int tetra_demod_etsi(tetra_ctx *ctx, const tetra_etsi_plan *plan, const void *iq, size_t C, size_t N,
                      void *soft, int8_t *softbits, uint8_t *hard, int32_t *nsym, size_t smax, float *diag);
@@ -370,6 +379,11 @@ int tetra_wb_lengths(const tetra_wb_plan *plan, size_t Nw, int64_t *nblk, int64_
 /* x [Nw] cf32 -> y [M][n_keep] cf32 at 72 kHz (first n_keep <= n72 outputs of each carrier; a
  * carrier's row is then n_keep / M2 timing chunks of M2 samples for tetra_etsi_timing). */
 int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *plan, const void *x, size_t Nw, void *y, size_t n_keep);
+/* tetra_channelize that also leaves om [M][ceil(n_keep / up)] float4: per carrier and group of up
+ * consecutive outputs, the Oerder-Meyr class partials (sum over o = c mod 4 of |y[up g + o]|^2, o
+ * ascending; oracle eo_om_group_partials) for tetra_etsi_timing_om.  D = M / 2 plan (up = 36) only. */
+int tetra_channelize_om(tetra_ctx *ctx, const tetra_wb_plan *plan, const void *x, size_t Nw, void *y, size_t n_keep,
+                        void *om);
 /* Synthetic wideband capture: M carriers of tetra_synth_etsi bursts at fs/D, filter-bank
  * synthesised to fs, plus AWGN at per-carrier Es/N0 = snr_db.  Outputs as tetra_synth_etsi with
  * C = M and N = Nw / D + 1 (carrier k at +k fs / M, i.e. FFT bin k). */

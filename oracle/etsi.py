@@ -54,6 +54,12 @@ def lib():
         L.eo_timing.argtypes = [f32p, ctypes.c_int, ctypes.c_float, ctypes.c_float, f32p, f32p, i8p, u8p,
                                 ctypes.c_int, f32p]
         L.eo_timing.restype = ctypes.c_int
+        L.eo_timing_om.argtypes = [f32p, ctypes.c_int, f32p, ctypes.c_float, ctypes.c_float, f32p, f32p, i8p, u8p,
+                                   ctypes.c_int, f32p]
+        L.eo_timing_om.restype = ctypes.c_int
+        L.eo_om_quarters.argtypes = [f32p, ctypes.c_int, f32p]
+        L.eo_om_group_partials.argtypes = [f32p, ctypes.c_long, ctypes.c_int, f32p]
+        L.eo_om_grouped.argtypes = [f32p, ctypes.c_long, ctypes.c_int, ctypes.c_int, f32p, f32p]
         L.eo_sync.argtypes = [u8p, ctypes.c_int, i32p, i32p, ctypes.c_int]
         L.eo_sync.restype = ctypes.c_int
         L.eo_decide.argtypes = [f32p, ctypes.c_int, u8p]
@@ -230,7 +236,9 @@ class Receiver:
         M2 = lib().eo_chanfilt(x, N, d["h1"], d["L1"], d["q1"], d["hp"], d["Lp"], d["up"], d["down"], x240, y)
         return y[:2 * M2].view(np.complex64).copy()
 
-    def timing(self, y):
+    def timing(self, y, om=None):
+        """Timing + decision on one chunk y; om: its Oerder-Meyr class sums A[4] (om_grouped), or
+        None for the fused demod's quarter order (om_quarters)."""
         d = self.d
         yv = np.ascontiguousarray(np.asarray(y, np.complex64)).view(np.float32)
         M2 = len(yv) // 2
@@ -240,12 +248,44 @@ class Receiver:
         soft = np.zeros(2 * smax, np.int8)
         hard = np.zeros(smax, np.uint8)
         diag = np.zeros(4, np.float32)
-        S = lib().eo_timing(yv, M2, d["gain"], d["soft_scale"], sym, dscr, soft, hard, smax, diag)
+        if om is None:
+            S = lib().eo_timing(yv, M2, d["gain"], d["soft_scale"], sym, dscr, soft, hard, smax, diag)
+        else:
+            S = lib().eo_timing_om(yv, M2, np.ascontiguousarray(om, np.float32), d["gain"], d["soft_scale"], sym,
+                                   dscr, soft, hard, smax, diag)
         return (sym[:2 * S].view(np.complex64).copy(), soft[:2 * max(S - 1, 0)].copy(),
                 hard[:max(S - 1, 0)].copy(), diag)
 
     def demod(self, x):
         return self.timing(self.chanfilt(x))
+
+    @staticmethod
+    def om_quarters(y):
+        """Oerder-Meyr class sums of one chunk in the fused demod's order (eo_om_quarters)."""
+        yv = np.ascontiguousarray(np.asarray(y, np.complex64)).view(np.float32)
+        A = np.zeros(4, np.float32)
+        lib().eo_om_quarters(yv, len(yv) // 2, A)
+        return A
+
+    @staticmethod
+    def om_group_partials(row, U):
+        """The wideband resampler's per-group class partials of a carrier row: [ceil(n / U), 4]."""
+        rv = np.ascontiguousarray(np.asarray(row, np.complex64)).view(np.float32)
+        n = len(rv) // 2
+        P = np.zeros(4 * (-(-n // U)), np.float32)
+        lib().eo_om_group_partials(rv, n, U, P)
+        return P.reshape(-1, 4)
+
+    @staticmethod
+    def om_grouped(row, s, M2, U, P=None):
+        """Oerder-Meyr class sums of the chunk row[s, s + M2) in the wideband grouped order
+        (eo_om_grouped) from the group partials P (computed from the row if None)."""
+        rv = np.ascontiguousarray(np.asarray(row, np.complex64)).view(np.float32)
+        if P is None:
+            P = Receiver.om_group_partials(row, U)
+        A = np.zeros(4, np.float32)
+        lib().eo_om_grouped(rv, s, M2, U, np.ascontiguousarray(P, np.float32).reshape(-1), A)
+        return A
 
     @staticmethod
     def decide(symbols):

@@ -268,13 +268,13 @@ static void csqrt_p(float x, float y, float *a, float *b)
  *   soft_sym [smax] cf32 symbol-spaced samples; softbits [2*smax] int8; hard [smax] dibit symbols.
  *   diag[0..3] = base, final delta, cfo rotation angle proxy (rot re, rot im).
  *   Returns S = number of soft symbols (dibits = S-1). */
-int eo_timing(const float *y, int M2, float gain, float soft_scale, float *soft_sym, float *dscr, int8_t *softbits,
-              uint8_t *hard, int smax, float *diag)
+/* Oerder-Meyr class sums A[c] = sum of |y[n]|^2 over n = c mod 4 of one chunk, in the fused
+ * demod's order: lane l accumulates n = l, l+64, ... (class n mod 4 = l mod 4), as four partial
+ * sums over quarters of the 64-sample blocks (part w: blocks [w q4, (w+1) q4), q4 = ceil(nb / 4))
+ * added in order -- the GPU computes the parts on four waves at once -- then a butterfly over
+ * xor 32, 16, 8, 4 (lane c holds class c). */
+void eo_om_quarters(const float *y, int M2, float A[4])
 {
-    if (M2 < 16) return 0;
-    /* Oerder-Meyr: lane l accumulates |y[n]|^2 for n = l, l+64, ... (class n mod 4 = l mod 4), as
-     * four partial sums over quarters of the 64-sample blocks (part w: blocks [w q4, (w+1) q4),
-     * q4 = ceil(nb / 4)) added in order -- the GPU computes the parts on four waves at once */
     float acc[64];
     const int nb = (M2 + 63) / 64, q4 = (nb + 3) / 4;
     for (int l = 0; l < 64; ++l) {
@@ -290,14 +290,67 @@ int eo_timing(const float *y, int M2, float gain, float soft_scale, float *soft_
         }
         acc[l] = s;
     }
-    /* class sums: butterfly over xor 32,16,8,4 */
-    {
-        float t[64];
-        for (int off = 32; off >= 4; off >>= 1) {
-            for (int l = 0; l < 64; ++l) t[l] = acc[l] + acc[l ^ off];
-            memcpy(acc, t, sizeof t);
-        }
+    float t[64];
+    for (int off = 32; off >= 4; off >>= 1) {
+        for (int l = 0; l < 64; ++l) t[l] = acc[l] + acc[l ^ off];
+        memcpy(acc, t, sizeof t);
     }
+    for (int c = 0; c < 4; ++c) A[c] = acc[c];
+}
+
+/* The same class sums in the wideband chain's grouped order (the resampler forms them while it
+ * writes y; csrc/wideband.hip k_pfb_resamp_fix OM, etsi_rx.hip k_timing OMG).  The chunk is
+ * row[s, s + M2) of a carrier's 72 kHz row, s and M2 multiples of 4 and U (the resampler's output
+ * group) a multiple of 4, so class c is n mod 4 in row positions too.
+ *   group partials P[g][c] = sum over o = c mod 4 in [0, U), ascending, of |row[U g + o]|^2;
+ *   G[c]: lane l (0..63) sums P[g][c] over the chunk's whole groups g = g0 + l, g0 + l + 64, ...
+ *         ascending (g0 = ceil(s / U), g1 = floor((s + M2) / U)), then the xor 32..1 butterfly;
+ *   head / tail: the samples before U g0 / from U g1 on, class by class in ascending n;
+ *   A[c] = (head[c] + G[c]) + tail[c]. */
+void eo_om_group_partials(const float *row, long n, int U, float *P)
+{
+    for (long g = 0; g * U < n; ++g)
+        for (int c = 0; c < 4; ++c) {
+            float p = 0.f;
+            for (int o = c; o < U; o += 4) {
+                long i = g * U + o;
+                if (i < n) p += fmaf(row[2 * i], row[2 * i], row[2 * i + 1] * row[2 * i + 1]);
+            }
+            P[4 * g + c] = p;
+        }
+}
+
+void eo_om_grouped(const float *row, long s, int M2, int U, const float *P, float A[4])
+{
+    const long g0 = (s + U - 1) / U, g1 = (s + M2) / U;
+    float v[4][64];
+    for (int c = 0; c < 4; ++c)
+        for (int l = 0; l < 64; ++l) {
+            float a = 0.f;
+            for (long g = g0 + l; g < g1; g += 64) a = a + P[4 * g + c];
+            v[c][l] = a;
+        }
+    const long hend = U * g0 < s + M2 ? U * g0 : s + M2, tbeg = U * g1 > hend ? U * g1 : hend;
+    for (int c = 0; c < 4; ++c) {
+        float h = 0.f, t = 0.f;
+        for (long i = s + c; i < hend; i += 4)
+            h = h + fmaf(row[2 * i], row[2 * i], row[2 * i + 1] * row[2 * i + 1]);
+        for (long i = tbeg + c; i < s + M2; i += 4)
+            t = t + fmaf(row[2 * i], row[2 * i], row[2 * i + 1] * row[2 * i + 1]);
+        A[c] = (h + wave_sum(v[c])) + t;
+    }
+}
+
+/* eo_timing with the Oerder-Meyr class sums given (om != NULL) or computed in the quarter order. */
+int eo_timing_om(const float *y, int M2, const float *om, float gain, float soft_scale, float *soft_sym, float *dscr,
+                 int8_t *softbits, uint8_t *hard, int smax, float *diag)
+{
+    if (M2 < 16) return 0;
+    float acc[4];
+    if (om)
+        memcpy(acc, om, sizeof acc);
+    else
+        eo_om_quarters(y, M2, acc);
     float Xr = acc[0] - acc[2], Xi = acc[3] - acc[1];
     float p = -0.63661977236758134f * pat2(Xi, Xr);   /* -(2/pi) arg X */
     float base = p < 0.0f ? p + 4.0f : p;
@@ -390,6 +443,12 @@ int eo_timing(const float *y, int M2, float gain, float soft_scale, float *soft_
     }
     if (diag) { diag[0] = base; diag[1] = delta; diag[2] = rr; diag[3] = ri; }
     return S;
+}
+
+int eo_timing(const float *y, int M2, float gain, float soft_scale, float *soft_sym, float *dscr, int8_t *softbits,
+              uint8_t *hard, int smax, float *diag)
+{
+    return eo_timing_om(y, M2, NULL, gain, soft_scale, soft_sym, dscr, softbits, hard, smax, diag);
 }
 
 /* ------------------------------------------------------------------------- burst sync */

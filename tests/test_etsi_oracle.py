@@ -145,3 +145,35 @@ def test_iq_round_trip_other_rates(fs):
     res = rx.lower_mac(soft, hard, cell)
     sent = [tuple(t) for _, jj in jobs for _, t in jj]
     assert len(res) >= 2 and all(ok and tuple(t1) in sent for _, _, dec in res for _, t1, ok in dec)
+
+
+def test_timing_with_given_class_sums_equals_quarter_order():
+    """eo_timing_om with the quarter-order class sums handed in is eo_timing (the O-M split is a pure
+    refactor), and the wideband grouped order gives the same class sums to float rounding."""
+    rng = np.random.default_rng(7)
+    ora = E.Receiver()
+    bits = rng.integers(0, 2, 2 * 1200).astype(np.uint8)
+    y = E.modulate(bits, 4 * 1100, fs=72000.0, t0=0.37, cfo=40.0, snr_db=15.0, rng=rng)
+    a = ora.timing(y)
+    b = ora.timing(y, om=ora.om_quarters(y))
+    for u, v in zip(a, b):
+        assert np.array_equal(u, v)
+    p = np.abs(y.astype(np.complex128)) ** 2
+    exact = np.array([p[c::4].sum() for c in range(4)])
+    for U in (4, 36, 64):
+        A = ora.om_grouped(y, 0, len(y), U)
+        assert np.allclose(A, exact, rtol=2e-6), U
+    assert np.allclose(ora.om_quarters(y), exact, rtol=2e-6)
+
+
+@pytest.mark.parametrize("s,M2,U", [(0, 3932, 36), (3932, 3932, 36), (7864, 3932, 36), (36, 1000, 36),
+                                    (8, 24, 36), (4, 60, 36), (40, 8000, 36), (0, 512, 4), (12, 4096, 64)])
+def test_grouped_class_sums_cover_each_sample_once(s, M2, U):
+    """The grouped order (head, whole groups, tail) counts every sample of row[s, s + M2) exactly
+    once in its class: with integer-valued powers the sums are exact in float32."""
+    rng = np.random.default_rng(s + M2 + U)
+    n = s + M2 + 2 * U
+    row = (rng.integers(0, 8, n) + 1j * rng.integers(0, 8, n)).astype(np.complex64)
+    A = E.Receiver.om_grouped(row, s, M2, U)
+    p = np.abs(row[s:s + M2].astype(np.complex128)) ** 2
+    assert np.array_equal(A, np.array([p[c::4].sum() for c in range(4)], np.float32))

@@ -125,11 +125,13 @@ def test_one_block_analysis_forms_bit_identical(monkeypatch):
 
 
 @pytest.mark.gpu
-def test_wideband_timing_bit_exact(capture):
+def test_wideband_timing_bit_exact(capture, monkeypatch):
     """From y on the chain is the ETSI one: the GPU timing on the channeliser's own output equals
-    oracle/etsi.py on the same y, carrier by carrier."""
+    oracle/etsi.py on the same y, carrier by carrier (TETRA_WB_OM=0: the timing's own Oerder-Meyr
+    pass over y, the ETSI chain's order; the grouped form: test_wideband_timing_om_bit_exact)."""
     import etsi as E
     from tetraear.signal.wideband import WidebandReceiver
+    monkeypatch.setenv("TETRA_WB_OM", "0")
     x = capture[0]
     rx = WidebandReceiver()
     hard, soft, sym, ns = rx.demod(x)
@@ -197,3 +199,56 @@ def test_bench_wideband_pipeline_matches_serial():
         assert st.quality()["crc_ok"] > 0
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
+
+
+@pytest.fixture(scope="module")
+def capture3():
+    from tetraear.signal.wideband import synth_wideband
+    return synth_wideband(3_300_000, seed=17, snr_db=25.0, cfo_max=300.0)   # three timing chunks per carrier
+
+
+@pytest.mark.gpu
+def test_resampler_om_partials_bit_exact(capture3):
+    """tetra_channelize_om: y is tetra_channelize's, and every whole group's Oerder-Meyr class partials
+    equal oracle eo_om_group_partials on that y."""
+    import etsi as E
+    from tetraear.signal.wideband import WidebandReceiver, chunking
+    x = capture3[0]
+    rx = WidebandReceiver()
+    nchunk, m2 = chunking(rx.plan, len(x), rx.m2)
+    n_keep = nchunk * m2
+    y, om = rx.channelize_om(x, n_keep)
+    assert np.array_equal(y, rx.channelize(x, n_keep))
+    U = rx.plan.c.up
+    whole = n_keep // U
+    for k in (0, 1, 255, 400, 799):
+        P = E.Receiver.om_group_partials(y[k], U)
+        assert np.array_equal(om[k, :whole], P[:whole]), k
+
+
+@pytest.mark.gpu
+def test_wideband_timing_om_bit_exact(capture3):
+    """The wideband timing on the resampler's class sums (tetra_etsi_timing_om) equals the oracle's
+    timing with the grouped Oerder-Meyr order, chunk by chunk -- chunks whose start is not on a
+    resampler group (heads and tails) included -- and decodes as the pass-over-y form does."""
+    import etsi as E
+    from tetraear.signal.wideband import WidebandReceiver, chunking
+    x = capture3[0]
+    rx = WidebandReceiver()
+    assert rx.grouped_om()
+    nchunk, m2 = chunking(rx.plan, len(x), rx.m2)
+    assert nchunk == 3
+    hard, soft, sym, ns = rx.demod(x)
+    y, _ = rx.channelize_om(x, nchunk * m2)
+    U = rx.plan.c.up
+    ora = E.Receiver()
+    for k in (0, 3, 399, 400, 798):
+        P = E.Receiver.om_group_partials(y[k], U)
+        for ci in range(nchunk):
+            s = ci * m2
+            A = E.Receiver.om_grouped(y[k], s, m2, U, P)
+            so, sbo, ho, _ = ora.timing(y[k, s:s + m2], om=A)
+            n = int(ns[k, ci])
+            assert n == len(so), (k, ci)
+            assert np.array_equal(sym[k, ci, :n], so) and np.array_equal(hard[k, ci, :n - 1], ho), (k, ci)
+            assert np.array_equal(soft[k, ci, :2 * (n - 1)], sbo), (k, ci)

@@ -247,11 +247,13 @@ __device__ __forceinline__ float om_all(const float2 *y, int M2, int lane) {
 // blocks' loads in flight in registers (pre, pre2: the ring's contents at every block are the same).
 // LEAN (k_timing): the Oerder-Meyr pass by om_all (all quarters' loads together) instead of om_part per
 // quarter, and no d_j stores -- the decision pass recomputes d_j from the stored symbols (timing_decide_sym).
-template <bool SPLIT = false, int RING = 0, bool LEAN = false>
+// OMC (k_timing's OMG form): the Oerder-Meyr class sums are given (omc = A0..A3, wave-uniform) --
+// the wideband resampler formed their group partials -- and the pass over y is skipped.
+template <bool SPLIT = false, int RING = 0, bool LEAN = false, bool OMC = false>
 __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float gain, float soft_scale, float2 *sp,
                                                  float2 *dp, int smax, int lane, int *prog = nullptr,
                                                  const float *om = nullptr, float2 *ring = nullptr,
-                                                 uint32_t *clk = nullptr) {
+                                                 uint32_t *clk = nullptr, float4 omc = float4{}) {
     TrackOut o{0, 1.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     if (M2 < 16) {
         if constexpr (SPLIT) {
@@ -262,21 +264,32 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
     // Oerder-Meyr: class sums of |y|^2 over n mod 4, per lane as four partial sums over quarters of
     // the blocks added in order (om_part; the oracle's order) -- precomputed by four waves (om)
     // or computed here one after the other
-    float s;
-    if (om) {
-        s = om[lane];
-#pragma unroll
-        for (int w = 1; w < 4; ++w) s = s + om[64 * w + lane];
-    } else if constexpr (LEAN) {
-        s = om_all(y, M2, lane);
+    float A0, A1, A2, A3;
+    if constexpr (OMC) {
+        A0 = omc.x;
+        A1 = omc.y;
+        A2 = omc.z;
+        A3 = omc.w;
     } else {
-        s = om_part(y, M2, 0, lane);
+        float s;
+        if (om) {
+            s = om[lane];
 #pragma unroll
-        for (int w = 1; w < 4; ++w) s = s + om_part(y, M2, w, lane);
+            for (int w = 1; w < 4; ++w) s = s + om[64 * w + lane];
+        } else if constexpr (LEAN) {
+            s = om_all(y, M2, lane);
+        } else {
+            s = om_part(y, M2, 0, lane);
+#pragma unroll
+            for (int w = 1; w < 4; ++w) s = s + om_part(y, M2, w, lane);
+        }
+        s = bfly<4>(s);
+        A0 = lane_f(s, 0);
+        A1 = lane_f(s, 1);
+        A2 = lane_f(s, 2);
+        A3 = lane_f(s, 3);
     }
-    s = bfly<4>(s);
     if (clk && lane == 0) clk[1] = (uint32_t)wall_clock64();   // probe: the Oerder-Meyr pass done
-    const float A0 = lane_f(s, 0), A1 = lane_f(s, 1), A2 = lane_f(s, 2), A3 = lane_f(s, 3);
     const float Xr = A0 - A2, Xi = A3 - A1;
     const float p = -0.63661977236758134f * pat2(Xi, Xr);
     float base = p < 0.0f ? p + 4.0f : p;
@@ -515,13 +528,14 @@ __device__ __forceinline__ void timing_decide_sym(const TrackOut &o, const float
 
 // clk (probe, TETRA_TIMING_PROBE=1 with a diag buffer): the wave's wall-clock stamps at its start, after
 // the Oerder-Meyr pass, after the Gardner loop and at its end, in place of the diagnostics
-template <int RING = 0, bool LEAN = false>
+template <int RING = 0, bool LEAN = false, bool OMC = false>
 __device__ __forceinline__ void timing_wave(const float2 *y, int M2, float gain, float soft_scale, float2 *sp,
                                             float2 *dp, int8_t *sb, uint8_t *hp, int32_t *nsym_ch, float4 *diag_ch,
-                                            int smax, int lane, float2 *ring = nullptr, uint32_t *clk = nullptr) {
-    if (clk && lane == 0) clk[0] = (uint32_t)wall_clock64();
-    const TrackOut o =
-        timing_track<false, RING, LEAN>(y, M2, gain, soft_scale, sp, dp, smax, lane, nullptr, nullptr, ring, clk);
+                                            int smax, int lane, float2 *ring = nullptr, uint32_t *clk = nullptr,
+                                            float4 omc = float4{}) {
+    if (!OMC && clk && lane == 0) clk[0] = (uint32_t)wall_clock64();   // OMC: stamped before the class sums
+    const TrackOut o = timing_track<false, RING, LEAN, OMC>(y, M2, gain, soft_scale, sp, dp, smax, lane, nullptr,
+                                                            nullptr, ring, clk, omc);
     if (clk && lane == 0) clk[2] = (uint32_t)wall_clock64();
     __threadfence_block();   // dp / sp written by other lanes is read below
     if constexpr (LEAN)
@@ -539,37 +553,80 @@ __device__ __forceinline__ void timing_wave(const float2 *y, int M2, float gain,
     }
 }
 
-template <int RING, bool LEAN>
+// The Oerder-Meyr class sums of chunk ch in the wideband grouped order (oracle eo_om_grouped): the
+// chunk is row[s, s + M2) of its carrier's row of nchunk chunks, s = (ch mod nchunk) M2; om holds the
+// row's resampler group partials (ngrp float4 per carrier, U outputs per group).  Lane l sums the
+// whole groups g0 + l, g0 + l + 64, ... then a wave butterfly; the head [s, U g0) and the tail
+// [U g1, s + M2) (each < U <= 64 samples, one per lane) are summed class by class in ascending n.
+__device__ __forceinline__ float4 om_grouped(const float2 *__restrict__ yall, const float4 *__restrict__ om, int ch,
+                                             int M2, int nchunk, int ngrp, int U, int lane) {
+    const int k = ch / nchunk;
+    const long s = (long)(ch - k * nchunk) * M2, e = s + M2;
+    const float2 *row = yall + (size_t)k * nchunk * M2;
+    const float4 *P = om + (size_t)k * ngrp;
+    const long g0 = (s + U - 1) / U, g1 = e / U;
+    const long hend = min((long)U * g0, e), tbeg = max((long)U * g1, hend);
+    // head and tail samples first (their loads in flight with the partials')
+    const long hi = s + lane, ti = tbeg + lane;
+    const float2 hv = hi < hend ? row[hi] : make_float2(0.f, 0.f);
+    const float2 tv = ti < e ? row[ti] : make_float2(0.f, 0.f);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (long g = g0 + lane; g < g1; g += 64) {
+        const float4 p = P[g];
+        v.x = v.x + p.x;
+        v.y = v.y + p.y;
+        v.z = v.z + p.z;
+        v.w = v.w + p.w;
+    }
+    // a lane past the head / tail holds 0, and adding +0 to a sum of squares leaves it unchanged
+    const float ph = fmaf(hv.x, hv.x, hv.y * hv.y), pt = fmaf(tv.x, tv.x, tv.y * tv.y);
+    wave_sum2(v.x, v.y);
+    wave_sum2(v.z, v.w);
+    float h[4] = {0.f, 0.f, 0.f, 0.f}, t[4] = {0.f, 0.f, 0.f, 0.f};
+    const int nh = (int)(hend - s), nt = (int)(e - tbeg);   // < U <= 64
+    for (int i = 0; i < nh; ++i) h[i & 3] = h[i & 3] + lane_f(ph, i);
+    for (int i = 0; i < nt; ++i) t[i & 3] = t[i & 3] + lane_f(pt, i);
+    return make_float4((h[0] + v.x) + t[0], (h[1] + v.y) + t[1], (h[2] + v.z) + t[2], (h[3] + v.w) + t[3]);
+}
+
+// OMG (tetra_etsi_timing_om): the Oerder-Meyr class sums from the resampler's group partials
+template <int RING, bool LEAN, bool OMG = false>
 __global__ __launch_bounds__(64) void k_timing(const float2 *__restrict__ yall, int M2, float gain, float soft_scale,
                                                float2 *__restrict__ sym, float2 *__restrict__ dscr,
                                                int8_t *__restrict__ softbits, uint8_t *__restrict__ hard,
                                                int32_t *__restrict__ nsym, int smax, float4 *__restrict__ diag,
-                                               int probe) {
+                                               int probe, const float4 *__restrict__ om, int nchunk, int ngrp, int U) {
     __shared__ float2 ring[RING ? TRING : 1];
     const int ch = blockIdx.x;
     uint32_t *clk = probe && diag ? reinterpret_cast<uint32_t *>(diag + ch) : nullptr;
-    timing_wave<RING, LEAN>(yall + (size_t)ch * M2, M2, gain, soft_scale, sym + (size_t)ch * smax, dscr + (size_t)ch * smax,
-                      softbits + (size_t)ch * 2 * smax, hard + (size_t)ch * smax, nsym + ch, diag ? diag + ch : nullptr,
-                      smax, threadIdx.x, ring, clk);
+    float4 omc = float4{};
+    if constexpr (OMG) {
+        if (clk && threadIdx.x == 0) clk[0] = (uint32_t)wall_clock64();
+        omc = om_grouped(yall, om, ch, M2, nchunk, ngrp, U, threadIdx.x);
+    }
+    timing_wave<RING, LEAN, OMG>(yall + (size_t)ch * M2, M2, gain, soft_scale, sym + (size_t)ch * smax,
+                                 dscr + (size_t)ch * smax, softbits + (size_t)ch * 2 * smax, hard + (size_t)ch * smax,
+                                 nsym + ch, diag ? diag + ch : nullptr, smax, threadIdx.x, ring, clk, omc);
 }
 // k_timing's form (same-box A/B): TETRA_TIMING_RING = 0 (the Gardner windows read straight from
 // global memory), 1 (one block ahead, default) or 2 (two); TETRA_TIMING_LEAN = 0 keeps om_part per
 // quarter for the Oerder-Meyr pass and the d_j round trip through dscr (default 1: om_all, d_j
 // recomputed from the symbols)
 using timing_fn = void (*)(const float2 *, int, float, float, float2 *, float2 *, int8_t *, uint8_t *, int32_t *, int,
-                           float4 *, int);
+                           float4 *, int, const float4 *, int, int, int);
 // TETRA_TIMING_PROBE=1: with a diag buffer, each chunk's diag entry holds four 32-bit wall-clock stamps
 // (start, Oerder-Meyr done, Gardner done, end) instead of the diagnostics -- a latency probe
 static int timing_probe() {
     const char *e = getenv("TETRA_TIMING_PROBE");
     return e && atoi(e) == 1;
 }
-static timing_fn timing_kernel(size_t M2, size_t smax) {
+static timing_fn timing_kernel(size_t M2, size_t smax, bool omg = false) {
     const char *r = getenv("TETRA_TIMING_RING"), *o = getenv("TETRA_TIMING_LEAN");
     // the ring form addresses y and the symbols through buffer resources (32-bit byte ranges)
     const bool fits = 8 * M2 < ((size_t)1 << 31) && 8 * smax < ((size_t)1 << 31);
     const int ring = !fits ? 0 : (r ? atoi(r) : 1);
     const bool lean = !(o && atoi(o) == 0);
+    if (omg) return ring <= 0 ? k_timing<0, true, true> : k_timing<1, true, true>;
     if (ring <= 0) return lean ? k_timing<0, true> : k_timing<0, false>;
     if (ring == 1) return lean ? k_timing<1, true> : k_timing<1, false>;
     return lean ? k_timing<2, true> : k_timing<2, false>;
@@ -2354,7 +2411,34 @@ int tetra_etsi_timing(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *y, s
     {
         PROF(ctx, "etsi_timing");
         hipLaunchKernelGGL(timing_kernel(M2, smax), dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yd, (int)M2, P->gain,
-                           P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg, timing_probe());
+                           P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg, timing_probe(),
+                           nullptr, 0, 0, 0);
+    }
+    return st.finish();
+}
+
+int tetra_etsi_timing_om(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *y, size_t C, size_t M2,
+                         const void *om, size_t nchunk, size_t ngrp, int U, void *soft, int8_t *softbits,
+                         uint8_t *hard, int32_t *nsym, size_t smax, float *diag) {
+    if (!ctx || !P || C == 0 || !om) return TETRA_E_INVALID;
+    if (nchunk == 0 || C % nchunk || M2 % 4 || U < 4 || U > 64 || U % 4 || ngrp * (size_t)U < nchunk * M2 ||
+        M2 < 16 || nchunk * M2 * 8 >= ((size_t)1 << 31))
+        return tetra_fail(ctx, TETRA_E_INVALID, "timing_om: C a multiple of nchunk, M2 >= 16 a multiple of 4, "
+                                                "4 <= U <= 64 a multiple of 4, ngrp U >= nchunk M2");
+    Staging st(ctx);
+    const void *yd = st.in(y, C * M2 * 8);
+    const void *omd = st.in(om, C / nchunk * ngrp * 16);
+    void *so = st.out(soft, C * smax * 8);
+    int8_t *sbo = (int8_t *)st.out(softbits, C * smax * 2);
+    uint8_t *ho = (uint8_t *)st.out(hard, C * smax);
+    int32_t *no = (int32_t *)st.out(nsym, C * 4);
+    float *dg = diag ? (float *)st.out(diag, C * 16) : nullptr;
+    if (!yd || !omd || !so || !sbo || !ho || !no) return st.finish();
+    {
+        PROF(ctx, "etsi_timing");
+        hipLaunchKernelGGL(timing_kernel(M2, smax, true), dim3((unsigned)C), dim3(64), 0, ctx->stream,
+                           (const float2 *)yd, (int)M2, P->gain, P->soft_scale, (float2 *)so, nullptr, sbo, ho, no,
+                           (int)smax, (float4 *)dg, timing_probe(), (const float4 *)omd, (int)nchunk, (int)ngrp, U);
     }
     return st.finish();
 }
@@ -2403,7 +2487,8 @@ int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *i
     {
         PROF(ctx, "etsi_timing");
         hipLaunchKernelGGL(timing_kernel(M2, smax), dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yb, (int)M2, P->gain,
-                           P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg, timing_probe());
+                           P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg, timing_probe(),
+                           nullptr, 0, 0, 0);
     }
     return st.finish();
 }

@@ -838,11 +838,16 @@ struct ResampUse {
     }
 };
 
-// PRB (timing-only build, TETRA_WB_RESAMP_PROBE=1): no y stores -- what the write-out costs
-template <int UP, int DOWN, int Q, bool ROT, int PRB = 0>
+// PRB (timing-only build, TETRA_WB_RESAMP_PROBE=1): no y stores -- what the write-out costs.
+// OM (tetra_channelize_om; UP a multiple of 4): each lane also leaves its group's Oerder-Meyr class
+// partials om[k][m] = (P0, P1, P2, P3), P_c = sum over o = c mod 4, ascending, of |y[UP m + o]|^2 --
+// from the registers the group's outputs are stored from, so k_timing's OMG form needs no pass over y
+// before its Gardner loop (oracle/etsi_oracle.c eo_om_group_partials).
+template <int UP, int DOWN, int Q, bool ROT, int PRB = 0, bool OM = false>
 __global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict__ Y, int M, int nblk,
                                                         const float *__restrict__ gU, float2 *__restrict__ y,
-                                                        int n_keep) {
+                                                        int n_keep, float4 *__restrict__ om = nullptr,
+                                                        int ngrp = 0) {
     using U = ResampUse<UP, DOWN, Q>;
     constexpr U use{};
     constexpr int ROWS = U::ROWS;                       // rows of one output group
@@ -897,6 +902,15 @@ __global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict
     }
 #pragma unroll
     for (int o = 0; o < UP; ++o) tile[lane * (OT + 1) + wv * UP + o] = make_float2(acc[o].x, acc[o].y);
+    if constexpr (OM) {
+        static_assert(UP % 4 == 0, "class partials need whole classes per group");
+        if (blockIdx.x * RS_C + lane < M && m * UP < n_keep) {
+            float p[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int o = 0; o < UP; ++o) p[o & 3] = p[o & 3] + fmaf(acc[o].x, acc[o].x, acc[o].y * acc[o].y);
+            om[(size_t)k * ngrp + m] = make_float4(p[0], p[1], p[2], p[3]);
+        }
+    }
     __syncthreads();
     const int k0 = blockIdx.x * RS_C, n0 = blockIdx.y * OT;
     for (int e = tid; e < RS_C * OT; e += 256) {
@@ -971,7 +985,8 @@ int tetra_wb_lengths(const tetra_wb_plan *P, size_t Nw, int64_t *nblk, int64_t *
     return TETRA_OK;
 }
 
-int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size_t Nw, void *y, size_t n_keep) {
+namespace {
+int channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size_t Nw, void *y, size_t n_keep, void *om) {
     if (!ctx) return TETRA_E_INVALID;
     int rc = wb_check(ctx, P);
     if (rc) return rc;
@@ -980,18 +995,22 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
     if (n72 <= 0 || n_keep == 0 || (int64_t)n_keep > n72)
         return tetra_fail(ctx, TETRA_E_INVALID, "n_keep must be in [1, %ld] for %zu samples", (long)n72, Nw);
     const int M = P->M, L = M * P->P, Q = P->Lg / P->up;
-    Staging st(ctx);
-    const float2 *xd = (const float2 *)st.in(x, Nw * 8);
-    float2 *yd = (float2 *)st.out(y, (size_t)M * n_keep * 8);
-    float2 *u = (float2 *)ws(ctx, S_W8, (size_t)nblk * M * 8);
     const int DM = 4 * P->D / M;   // 1: carriers at 4x, 2: at 2x the carrier spacing
     if (Q != 45 && Q != 23) return tetra_fail(ctx, TETRA_E_INVALID, "resampler built for Lg / up = 45 or 23 taps");
     if (P->up > RS_QP) return tetra_fail(ctx, TETRA_E_INVALID, "resampler up %d > %d", P->up, RS_QP);
     // the compiled-in rate pairs: 100 kHz -> 72 kHz (D = M / 4) and 50 kHz -> 72 kHz (D = M / 2)
     const bool fix18 = P->up == 18 && P->down == 25 && Q == 45, fix36 = P->up == 36 && P->down == 25 && Q == 23;
     const bool fixed = fix18 || fix36;
+    if (om && !fix36)
+        return tetra_fail(ctx, TETRA_E_INVALID, "Oerder-Meyr group partials need the D = M / 2 resampler (36 / 25)");
+    const int ngrp = (int)((n_keep + P->up - 1) / P->up);
+    Staging st(ctx);
+    const float2 *xd = (const float2 *)st.in(x, Nw * 8);
+    float2 *yd = (float2 *)st.out(y, (size_t)M * n_keep * 8);
+    float4 *omd = om ? (float4 *)st.out(om, (size_t)M * ngrp * 16) : nullptr;
+    float2 *u = (float2 *)ws(ctx, S_W8, (size_t)nblk * M * 8);
     float *taps = (float *)ws(ctx, S_W9, (size_t)(L + P->up * RS_QP + P->Lg + 2 + 2 * AN_TWN) * 4);
-    if (!xd || !yd || !u || !taps) return st.finish();
+    if (!xd || !yd || !u || !taps || (om && !omd)) return st.finish();
     // h, then g phase-major: gT[rho][q] = g[rho + up q] (zero-padded to RS_QP), then g as given
     ctx->taps_wb.assign(P->h, P->h + L);
     ctx->taps_wb.resize((size_t)L + P->up * RS_QP, 0.f);
@@ -1131,6 +1150,9 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
         if (fix36 && pe && atoi(pe) == 1)
             hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false, 1>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk,
                                gu, yd, (int)n_keep);
+        else if (fix36 && omd)   // + the Oerder-Meyr group partials
+            hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false, 0, true>), gr, dim3(256), 0, ctx->stream, u, M,
+                               (int)nblk, gu, yd, (int)n_keep, omd, ngrp);
         else if (fix36)   // D = M / 2: always the fused analysis, Y rotated there
             hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk, gu,
                                yd, (int)n_keep);
@@ -1159,6 +1181,17 @@ int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size
         HIP_TRY(ctx, hipGetLastError());
     }
     return st.finish();
+}
+}  // namespace
+
+int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size_t Nw, void *y, size_t n_keep) {
+    return channelize(ctx, P, x, Nw, y, n_keep, nullptr);
+}
+
+int tetra_channelize_om(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size_t Nw, void *y, size_t n_keep,
+                        void *om) {
+    if (!om) return tetra_fail(ctx, TETRA_E_INVALID, "null om");
+    return channelize(ctx, P, x, Nw, y, n_keep, om);
 }
 
 int tetra_synth_wideband(tetra_ctx *ctx, const tetra_wb_plan *P, size_t Nw, uint64_t seed, float snr_db,

@@ -103,6 +103,8 @@ def _bind(L):
         "tetra_etsi_lengths": (_i32, [ctypes.POINTER(EtsiPlan), _sz, _vp, _vp, _vp]),
         "tetra_etsi_chanfilt": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _sz, _sz, _vp]),
         "tetra_etsi_timing": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _sz, _sz, _vp, _vp, _vp, _vp, _sz, _vp]),
+        "tetra_etsi_timing_om": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _sz, _sz, _vp, _sz, _sz, ctypes.c_int, _vp,
+                                        _vp, _vp, _vp, _sz, _vp]),
         "tetra_demod_etsi": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _sz, _sz, _vp, _vp, _vp, _vp, _sz, _vp]),
         "tetra_etsi_chanfilt_fmt": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _i32, _sz, _sz, _vp]),
         "tetra_demod_etsi_fmt": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _i32, _sz, _sz, _vp, _vp, _vp, _vp, _sz,
@@ -121,6 +123,7 @@ def _bind(L):
         "tetra_afc_gate": (_i32, [_vp, _vp, _i32, _sz, _sz, ctypes.c_double, _vp, _vp, _vp, _vp]),
         "tetra_scan_detect": (_i32, [_vp, _vp, _i32, _sz, _sz, _i32, ctypes.c_uint32, _vp]),
         "tetra_channelize": (_i32, [_vp, ctypes.POINTER(WbPlan), _vp, _sz, _vp, _sz]),
+        "tetra_channelize_om": (_i32, [_vp, ctypes.POINTER(WbPlan), _vp, _sz, _vp, _sz, _vp]),
         "tetra_synth_wideband": (_i32, [_vp, ctypes.POINTER(WbPlan), _sz, ctypes.c_uint64, ctypes.c_float,
                                         ctypes.c_float, _vp, _vp, _vp, _vp, _vp]),
         "tetra_synth_bursts_per_channel": (_i32, [_sz, ctypes.c_double]),

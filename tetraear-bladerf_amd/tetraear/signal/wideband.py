@@ -87,6 +87,13 @@ def chunking(plan, Nw, m2=M2_CHUNK):
     return nchunk, m2
 
 
+def grouped_om(plan, m2=M2_CHUNK):
+    """The wideband timing takes its Oerder-Meyr class sums from the resampler's group partials
+    (tetra_channelize_om + tetra_etsi_timing_om) where the plan's output groups hold whole classes
+    (up a multiple of 4: the D = M / 2 design) and TETRA_WB_OM is not 0."""
+    return plan.c.up % 4 == 0 and plan.c.up <= 64 and m2 % 4 == 0 and os.environ.get("TETRA_WB_OM", "1") != "0"
+
+
 class WidebandReceiver:
     """Channeliser + per-carrier ETSI demod (timing, decision) for host or device arrays."""
 
@@ -105,11 +112,33 @@ class WidebandReceiver:
         c.check(c.lib.tetra_channelize(c.handle, self.plan.c, _hip.ptr(x), len(x), _hip.ptr(y), n_keep), "channelize")
         return y
 
+    def channelize_om(self, x, n_keep=None):
+        """channelize plus the resampler's Oerder-Meyr group partials: (y [M][n_keep] complex64,
+        om [M][ceil(n_keep / up)][4] float32) -- D = M / 2 plan only (tetra_channelize_om)."""
+        c = _hip.ctx()
+        x = np.ascontiguousarray(x, np.complex64)
+        _, n72 = self.plan.lengths(len(x))
+        n_keep = n72 if n_keep is None else n_keep
+        y = np.empty((self.plan.M, n_keep), np.complex64)
+        om = np.empty((self.plan.M, -(-n_keep // self.plan.c.up), 4), np.float32)
+        c.check(c.lib.tetra_channelize_om(c.handle, self.plan.c, _hip.ptr(x), len(x), _hip.ptr(y), n_keep,
+                                          _hip.ptr(om)), "channelize_om")
+        return y, om
+
+    def grouped_om(self):
+        """Whether demod forms the timing's Oerder-Meyr sums in the resampler (the D = M / 2 plan;
+        TETRA_WB_OM=0 keeps the timing's own pass over y, for A/B)."""
+        return grouped_om(self.plan)
+
     def demod(self, x):
         """x [Nw] -> (hard, soft_bits, sym, nsym) per (carrier, chunk): [M, nchunk, smax] uint8,
         [M, nchunk, 2 smax] int8, [M, nchunk, smax] complex64, [M, nchunk] int32."""
         nchunk, m2 = chunking(self.plan, len(x), self.m2)
-        y = self.channelize(x, nchunk * m2)
+        om = None
+        if self.grouped_om():
+            y, om = self.channelize_om(x, nchunk * m2)
+        else:
+            y = self.channelize(x, nchunk * m2)
         c = _hip.ctx()
         C = self.plan.M * nchunk
         sm = m2 // 4 + 2
@@ -117,8 +146,13 @@ class WidebandReceiver:
         soft = np.empty((C, 2 * sm), np.int8)
         hard = np.empty((C, sm), np.uint8)
         ns = np.empty(C, np.int32)
-        c.check(c.lib.tetra_etsi_timing(c.handle, self.etsi, _hip.ptr(y), C, m2, _hip.ptr(sym), _hip.ptr(soft),
-                                        _hip.ptr(hard), _hip.ptr(ns), sm, None), "etsi_timing")
+        if om is not None:
+            c.check(c.lib.tetra_etsi_timing_om(c.handle, self.etsi, _hip.ptr(y), C, m2, _hip.ptr(om), nchunk,
+                                               om.shape[1], self.plan.c.up, _hip.ptr(sym), _hip.ptr(soft),
+                                               _hip.ptr(hard), _hip.ptr(ns), sm, None), "etsi_timing_om")
+        else:
+            c.check(c.lib.tetra_etsi_timing(c.handle, self.etsi, _hip.ptr(y), C, m2, _hip.ptr(sym), _hip.ptr(soft),
+                                            _hip.ptr(hard), _hip.ptr(ns), sm, None), "etsi_timing")
         M = self.plan.M
         return (hard.reshape(M, nchunk, sm), soft.reshape(M, nchunk, 2 * sm), sym.reshape(M, nchunk, sm),
                 ns.reshape(M, nchunk))
@@ -170,6 +204,10 @@ class BenchStep:
         torch.cuda.current_stream(device).synchronize()
         c.check(c.lib.tetra_etsi_set_cells(c.handle, _hip.ptr(self.cells), self.C), "set_cells")
         self.y = torch.empty((M, self.nchunk * self.m2, 2), dtype=torch.float32, device=device)
+        # the timing's Oerder-Meyr class sums from the resampler (grouped_om): its group partials
+        self.om_grouped = grouped_om(self.plan, self.m2)
+        self.ngrp = -(-self.nchunk * self.m2 // self.plan.c.up)
+        self.om = torch.empty((M, self.ngrp, 4), dtype=torch.float32, device=device) if self.om_grouped else None
         self.sym = torch.empty((self.C, self.sm, 2), dtype=torch.float32, device=device)
         self.soft = torch.empty((self.C, 2 * self.sm), dtype=torch.int8, device=device)
         self.hard = torch.empty((self.C, self.sm), dtype=torch.uint8, device=device)
@@ -208,6 +246,7 @@ class BenchStep:
                         "set_stream")
         self.back.check(self.back.lib.tetra_etsi_set_cells(self.back.handle, _hip.ptr(self.cells), self.C), "set_cells")
         self.ys = [self.y, torch.empty_like(self.y)]
+        self.oms = [self.om, torch.empty_like(self.om) if self.om is not None else None]
         self.ev_front = [torch.cuda.Event() for _ in range(2)]
         self.ev_back = [torch.cuda.Event() for _ in range(2)]
         for e in self.ev_back:
@@ -223,35 +262,45 @@ class BenchStep:
         c.check(c.lib.tetra_waterfall(c.handle, _hip.ptr(self.x), _hip.TETRA_CF32, 1, self.Nw, 2048, 2048, self.nfr,
                                       _hip.ptr(self.wf)), "waterfall")
 
-    def _front(self, c, y):
+    def _front(self, c, y, om):
         if not (self.pipelined and self.wf_back):
             self._waterfall(c)
-        c.check(c.lib.tetra_channelize(c.handle, self.plan.c, _hip.ptr(self.x), self.Nw, _hip.ptr(y),
-                                       self.nchunk * self.m2), "channelize")
+        if om is not None:
+            c.check(c.lib.tetra_channelize_om(c.handle, self.plan.c, _hip.ptr(self.x), self.Nw, _hip.ptr(y),
+                                              self.nchunk * self.m2, _hip.ptr(om)), "channelize_om")
+        else:
+            c.check(c.lib.tetra_channelize(c.handle, self.plan.c, _hip.ptr(self.x), self.Nw, _hip.ptr(y),
+                                           self.nchunk * self.m2), "channelize")
 
-    def _back(self, c, y):
+    def _back(self, c, y, om):
         if self.pipelined and self.wf_back:
             self._waterfall(c)
-        c.check(c.lib.tetra_etsi_timing(c.handle, self.etsi, _hip.ptr(y), self.C, self.m2, _hip.ptr(self.sym),
-                                        _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.sm, None),
-                "etsi_timing")
+        if om is not None:
+            c.check(c.lib.tetra_etsi_timing_om(c.handle, self.etsi, _hip.ptr(y), self.C, self.m2, _hip.ptr(om),
+                                               self.nchunk, self.ngrp, self.plan.c.up, _hip.ptr(self.sym),
+                                               _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.sm,
+                                               None), "etsi_timing_om")
+        else:
+            c.check(c.lib.tetra_etsi_timing(c.handle, self.etsi, _hip.ptr(y), self.C, self.m2, _hip.ptr(self.sym),
+                                            _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.sm,
+                                            None), "etsi_timing")
         c.check(c.lib.tetra_lmac_etsi(c.handle, _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.C,
                                       self.sm, _hip.ptr(self.nburst), _hip.ptr(self.bursts), _hip.ptr(self.nblock),
                                       _hip.ptr(self.blocks), _hip.ptr(self.type1)), "lmac_etsi")
 
     def __call__(self):
         if not self.pipelined:
-            self._front(self.c, self.y)
-            self._back(self.c, self.y)
+            self._front(self.c, self.y, self.om)
+            self._back(self.c, self.y, self.om)
             return
         i = self.k & 1
         self.k += 1
-        y = self.ys[i]
-        self.s_front.wait_event(self.ev_back[i])   # the timing two steps back has consumed y[i]
-        self._front(self.c, y)
+        y, om = self.ys[i], self.oms[i]
+        self.s_front.wait_event(self.ev_back[i])   # the timing two steps back has consumed y[i], om[i]
+        self._front(self.c, y, om)
         self.ev_front[i].record(self.s_front)
         self.s_back.wait_event(self.ev_front[i])
-        self._back(self.back, y)
+        self._back(self.back, y, om)
         self.ev_back[i].record(self.s_back)
 
     def stage_bytes(self):
@@ -266,7 +315,8 @@ class BenchStep:
         return {"waterfall": (12.0 * self.nfr * 2048 / self.Nw, "k_waterfall"),
                 "wb_analysis": (8.0 + 8.0 * M / D, ana),   # fused fold + FFT: x in, Y out
                 "wb_fold": (8.0 + 8.0 * M / D, "k_pfb_fold"), "wb_fft": (2 * 8.0 * M / D, None),
-                "wb_resamp": (8.0 * M / D + yb, "k_pfb_resamp_fix"),
+                "wb_resamp": (8.0 * M / D + yb + (yb * 2.0 / self.plan.c.up if self.om_grouped else 0.0),
+                              "k_pfb_resamp_fix"),
                 "etsi_timing": (yb + 11.0 * M * 18000.0 / fs, "k_timing")}
 
     def config(self, world):
