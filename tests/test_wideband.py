@@ -172,15 +172,18 @@ def test_wideband_round_trip(capture):
 
 
 @pytest.mark.gpu
-def test_bench_wideband_pipeline_matches_serial():
+def test_bench_wideband_pipeline_matches_serial(monkeypatch):
     """bench.py --chain wideband: the two-stream pipeline (channeliser of capture k+1 beside the
-    timing + lower MAC of capture k, y double-buffered) gives every step the serial chain's results."""
+    timing + lower MAC of capture k, y double-buffered) and the three-stream one (TETRA_WB_STAGES=3:
+    channeliser, timing and lower MAC of three captures, the timing's outputs double-buffered too)
+    give every step the serial chain's results."""
     import torch
     from tetraear import _hip
     from tetraear.signal.wideband import BenchStep
     dev = torch.device("cuda", 0)
     outs = []
-    for pipe in (False, True):
+    for pipe, stages in ((False, "2"), (True, "2"), (True, "3")):
+        monkeypatch.setenv("TETRA_WB_STAGES", stages)
         c = _hip.Context()
         c.check(c.lib.tetra_set_stream(c.handle, None), "set_stream")
         st = BenchStep(c, 2_000_000, seed=3, device=dev)
@@ -197,8 +200,9 @@ def test_bench_wideband_pipeline_matches_serial():
             blocks[ch, :int(nk[ch])])] + [t1[ch, j, :n1[int(blocks[ch, j, 0])]] for ch in range(st.C)
                                           for j in range(int(nk[ch]))])
         assert st.quality()["crc_ok"] > 0
-    for a, b in zip(outs[0], outs[1]):
-        assert torch.equal(a, b)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
 
 
 @pytest.fixture(scope="module")

@@ -222,11 +222,12 @@ class BenchStep:
         self.pipelined = False
 
     def pipeline(self):
-        """Two-stage software pipeline over consecutive captures: the channeliser of step k+1 on the
-        front stream while the waterfall rows and the per-carrier timing + lower MAC of step k run on a
-        back stream (its own context).  The carrier samples y are what crosses the streams: double-buffered,
-        each stage waits only on the event that protects its buffer.  Every step still does the
-        whole chain."""
+        """Software pipeline over consecutive captures: the channeliser of step k+2 on the front
+        stream while the per-carrier timing of step k+1 runs on a middle stream and the waterfall rows
+        and the lower MAC of step k on a back stream (each its own context).  The carrier samples y
+        (with their Oerder-Meyr partials) and the timing's outputs are what crosses the streams:
+        double-buffered, each stage waits only on the events that protect its buffers.  Every step
+        still does the whole chain."""
         import torch
         dev = self.x.device
         self.back = _hip.Context()
@@ -251,12 +252,28 @@ class BenchStep:
         self.ev_back = [torch.cuda.Event() for _ in range(2)]
         for e in self.ev_back:
             e.record(self.s_back)
+        # three streams (default): the timing on a middle stream of its own, the lower MAC (and the
+        # waterfall rows) on the back stream -- three captures in flight; the timing's outputs (symbols,
+        # soft bits, dibits, counts) are then double-buffered too.  Same box: 0.386-0.387 ms per step
+        # against 0.397-0.415 with two streams (profiles/r04_ab_wb_stages.txt).  TETRA_WB_STAGES=2: the
+        # two-stream form (timing + lower MAC on the back stream)
+        self.mid = None
+        if os.environ.get("TETRA_WB_STAGES", "3") == "3":
+            self.mid = _hip.Context()
+            self.s_mid = torch.cuda.Stream(device=dev)
+            self.mid.check(self.mid.lib.tetra_set_stream(self.mid.handle, ctypes.c_void_p(self.s_mid.cuda_stream)),
+                           "set_stream")
+            self.outs = [(self.sym, self.soft, self.hard, self.nsym)]
+            self.outs.append(tuple(torch.empty_like(t) for t in self.outs[0]))
+            self.ev_mid = [torch.cuda.Event() for _ in range(2)]
+            for e in self.ev_mid:
+                e.record(self.s_mid)
         self.k = 0
         self.pipelined = True
         return self
 
     def contexts(self):
-        return [self.c] + ([self.back] if self.pipelined else [])
+        return [self.c] + ([self.back] if self.pipelined else []) + ([self.mid] if self.mid is not None else [])
 
     def _waterfall(self, c):
         c.check(c.lib.tetra_waterfall(c.handle, _hip.ptr(self.x), _hip.TETRA_CF32, 1, self.Nw, 2048, 2048, self.nfr,
@@ -272,9 +289,7 @@ class BenchStep:
             c.check(c.lib.tetra_channelize(c.handle, self.plan.c, _hip.ptr(self.x), self.Nw, _hip.ptr(y),
                                            self.nchunk * self.m2), "channelize")
 
-    def _back(self, c, y, om):
-        if self.pipelined and self.wf_back:
-            self._waterfall(c)
+    def _timing(self, c, y, om):
         if om is not None:
             c.check(c.lib.tetra_etsi_timing_om(c.handle, self.etsi, _hip.ptr(y), self.C, self.m2, _hip.ptr(om),
                                                self.nchunk, self.ngrp, self.plan.c.up, _hip.ptr(self.sym),
@@ -284,9 +299,17 @@ class BenchStep:
             c.check(c.lib.tetra_etsi_timing(c.handle, self.etsi, _hip.ptr(y), self.C, self.m2, _hip.ptr(self.sym),
                                             _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.sm,
                                             None), "etsi_timing")
+
+    def _lmac(self, c):
         c.check(c.lib.tetra_lmac_etsi(c.handle, _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.C,
                                       self.sm, _hip.ptr(self.nburst), _hip.ptr(self.bursts), _hip.ptr(self.nblock),
                                       _hip.ptr(self.blocks), _hip.ptr(self.type1)), "lmac_etsi")
+
+    def _back(self, c, y, om):
+        if self.pipelined and self.wf_back:
+            self._waterfall(c)
+        self._timing(c, y, om)
+        self._lmac(c)
 
     def __call__(self):
         if not self.pipelined:
@@ -296,11 +319,25 @@ class BenchStep:
         i = self.k & 1
         self.k += 1
         y, om = self.ys[i], self.oms[i]
-        self.s_front.wait_event(self.ev_back[i])   # the timing two steps back has consumed y[i], om[i]
+        self.s_front.wait_event(self.ev_back[i] if self.mid is None else self.ev_mid[i])   # y[i], om[i] consumed
         self._front(self.c, y, om)
         self.ev_front[i].record(self.s_front)
-        self.s_back.wait_event(self.ev_front[i])
-        self._back(self.back, y, om)
+        if self.mid is None:
+            self.s_back.wait_event(self.ev_front[i])
+            self._back(self.back, y, om)
+            self.ev_back[i].record(self.s_back)
+            return
+        # three streams: timing of this capture on the middle one once its channeliser is done and the
+        # lower MAC two captures back has consumed output buffer i; the lower MAC on the back one
+        self.sym, self.soft, self.hard, self.nsym = self.outs[i]
+        self.s_mid.wait_event(self.ev_front[i])
+        self.s_mid.wait_event(self.ev_back[i])
+        self._timing(self.mid, y, om)
+        self.ev_mid[i].record(self.s_mid)
+        self.s_back.wait_event(self.ev_mid[i])
+        if self.wf_back:
+            self._waterfall(self.back)
+        self._lmac(self.back)
         self.ev_back[i].record(self.s_back)
 
     def stage_bytes(self):
