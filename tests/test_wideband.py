@@ -189,6 +189,7 @@ def test_bench_wideband_pipeline_matches_serial(monkeypatch):
         st = BenchStep(c, 2_000_000, seed=3, device=dev)
         if pipe:
             st.pipeline()
+        assert len(st.contexts()) == (1 if not pipe else int(stages))   # what bench.py profiles
         for _ in range(3):
             st()
         torch.cuda.synchronize(dev)

@@ -220,6 +220,7 @@ class BenchStep:
         self.nfr = Nw // 2048   # waterfall rows of the capture (2048-pt Hann frames, hop 2048)
         self.wf = torch.empty((self.nfr, 2048), dtype=torch.float32, device=device)
         self.pipelined = False
+        self.mid = None
 
     def pipeline(self):
         """Software pipeline over consecutive captures: the channeliser of step k+2 on the front
