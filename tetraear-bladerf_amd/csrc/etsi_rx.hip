@@ -578,7 +578,6 @@ __device__ __forceinline__ float4 om_grouped(const float2 *__restrict__ yall, co
         v.z = v.z + p.z;
         v.w = v.w + p.w;
     }
-    // a lane past the head / tail holds 0, and adding +0 to a sum of squares leaves it unchanged
     const float ph = fmaf(hv.x, hv.x, hv.y * hv.y), pt = fmaf(tv.x, tv.x, tv.y * tv.y);
     wave_sum2(v.x, v.y);
     wave_sum2(v.z, v.w);
@@ -2437,6 +2436,7 @@ int tetra_etsi_timing_om(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *y
     {
         PROF(ctx, "etsi_timing");
         hipLaunchKernelGGL(timing_kernel(M2, smax, true), dim3((unsigned)C), dim3(64), 0, ctx->stream,
+                           // no d_j scratch: the LEAN form recomputes d_j from the stored symbols
                            (const float2 *)yd, (int)M2, P->gain, P->soft_scale, (float2 *)so, nullptr, sbo, ho, no,
                            (int)smax, (float4 *)dg, timing_probe(), (const float4 *)omd, (int)nchunk, (int)ngrp, U);
     }
