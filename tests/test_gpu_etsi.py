@@ -96,6 +96,65 @@ def test_timing_forms_bit_exact(synth_small, ring, lean, monkeypatch):
             assert np.array_equal(soft[ch, :2 * (n - 1)], sbo), (m2, ch)
 
 
+@pytest.mark.parametrize("m2,nchunk,U", [(3932, 3, 36), (1000, 5, 36), (1000, 4, 4), (2048, 3, 64), (404, 7, 12),
+                                          (36, 4, 36), (20, 6, 36)])
+def test_timing_om_geometries_bit_exact(synth_small, m2, nchunk, U):
+    """tetra_etsi_timing_om, apart from the resampler: rows of nchunk chunks of real 72 kHz samples, the
+    group partials from the oracle (eo_om_group_partials), and chunk boundaries on and off the groups
+    (whole chunks of groups, heads and tails, chunks shorter than one group) -- the GPU's class sums
+    and every output equal the oracle's timing with the grouped order."""
+    from tetraear import _hip
+    from tetraear.signal.etsi import etsi_plan, lengths
+    iq = synth_small[0][:2]
+    plan = etsi_plan()
+    C0, N = iq.shape
+    _, M2, _ = lengths(plan, N)
+    c = _hip.ctx()
+    y0 = np.zeros((C0, M2), np.complex64)
+    c.check(c.lib.tetra_etsi_chanfilt(c.handle, plan, _hip.ptr(iq), C0, N, _hip.ptr(y0)))
+    # carrier rows cut from the two channels' y (wrapping), nchunk chunks each
+    rows = np.stack([np.resize(np.roll(y0[r % C0], 977 * r), nchunk * m2) for r in range(3)]).astype(np.complex64)
+    ngrp = -(-nchunk * m2 // U)
+    om = np.stack([E.Receiver.om_group_partials(r, U) for r in rows]).astype(np.float32)
+    assert om.shape == (3, ngrp, 4)
+    C, sm = 3 * nchunk, m2 // 4 + 2
+    sym = np.zeros((C, sm), np.complex64)
+    soft, hard, ns = np.zeros((C, 2 * sm), np.int8), np.zeros((C, sm), np.uint8), np.zeros(C, np.int32)
+    c.check(c.lib.tetra_etsi_timing_om(c.handle, plan, _hip.ptr(rows), C, m2, _hip.ptr(om), nchunk, ngrp, U,
+                                       _hip.ptr(sym), _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(ns), sm, None),
+            "etsi_timing_om")
+    ora = E.Receiver()
+    for r in range(3):
+        for ci in range(nchunk):
+            s0 = ci * m2
+            A = E.Receiver.om_grouped(rows[r], s0, m2, U, om[r])
+            so, sbo, ho, _ = ora.timing(rows[r, s0:s0 + m2], om=A)
+            ch = r * nchunk + ci
+            n = int(ns[ch])
+            assert n == len(so), (r, ci)
+            assert np.array_equal(sym[ch, :n], so) and np.array_equal(hard[ch, :n - 1], ho), (r, ci)
+            assert np.array_equal(soft[ch, :2 * (n - 1)], sbo), (r, ci)
+
+
+def test_timing_om_rejects_bad_geometry():
+    """The grouped-order entry point returns an error code (no launch) for geometries its class sums
+    do not cover: C not a multiple of nchunk, M2 not a multiple of 4, U not a multiple of 4 or > 64,
+    partials that do not cover the rows."""
+    from tetraear import _hip
+    from tetraear.signal.etsi import etsi_plan
+    plan = etsi_plan()
+    c = _hip.ctx()
+    y = np.zeros((4, 400), np.complex64)
+    om = np.zeros((2, 40, 4), np.float32)
+    sym, soft = np.zeros((4, 102), np.complex64), np.zeros((4, 204), np.int8)
+    hard, ns = np.zeros((4, 102), np.uint8), np.zeros(4, np.int32)
+    for C, m2, nchunk, ngrp, U in ((4, 400, 3, 40, 36), (4, 398, 2, 40, 36), (4, 400, 2, 40, 18),
+                                   (4, 400, 2, 40, 68), (4, 400, 2, 10, 36)):
+        rc = c.lib.tetra_etsi_timing_om(c.handle, plan, _hip.ptr(y), C, m2, _hip.ptr(om), nchunk, ngrp, U,
+                                        _hip.ptr(sym), _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(ns), 102, None)
+        assert rc != 0, (C, m2, nchunk, ngrp, U)
+
+
 def test_lower_mac_matches_oracle(synth_small):
     from tetraear.signal.etsi import EtsiReceiver
     from tetraear.core.etsi import EtsiLowerMac
