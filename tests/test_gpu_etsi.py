@@ -368,11 +368,12 @@ def test_full_size_round_trip():
     assert nok / nblk > 0.97, (nok, nblk)
 
 
-def test_bench_pipeline_matches_serial():
+def test_bench_pipeline_matches_serial(monkeypatch):
     """bench.py's step variants give the same per-step results as the single-stream fused chain:
     the two-stream pipeline (front: fused demod, back: lower MAC, double-buffered symbol outputs),
-    the split demod (chanfilt -> y in HBM -> timing) pipelined, and the host-fed (PCIe) mode; the
-    SC16 pipeline against the SC16 single-stream chain."""
+    the same with consecutive demods on two front streams (TETRA_ETSI_FRONT2=1), the split demod
+    (chanfilt -> y in HBM -> timing) pipelined, and the host-fed (PCIe) mode; the SC16 pipeline
+    against the SC16 single-stream chain."""
     import torch
     from tetraear import _hip
     from tetraear.signal.etsi import BenchStep
@@ -383,13 +384,15 @@ def test_bench_pipeline_matches_serial():
     c = _hip.Context()
     c.check(c.lib.tetra_set_stream(c.handle, None), "set_stream")
     outs = {"cf32": [], "sc16": []}   # SC16 steps compare among themselves (other input)
-    for pipe, demod, host, fmt in ((False, "fused", False, "cf32"), (True, "fused", False, "cf32"),
-                                   (True, "split", False, "cf32"), (True, "fused", True, "cf32"),
-                                   (False, "split", True, "cf32"), (True, "fused", False, "sc16"),
-                                   (False, "fused", False, "sc16")):
+    for pipe, demod, host, fmt, f2 in ((False, "fused", False, "cf32", "0"), (True, "fused", False, "cf32", "0"),
+                                       (True, "fused", False, "cf32", "1"), (True, "split", False, "cf32", "0"),
+                                       (True, "fused", True, "cf32", "0"), (False, "split", True, "cf32", "0"),
+                                       (True, "fused", False, "sc16", "0"), (False, "fused", False, "sc16", "0")):
+        monkeypatch.setenv("TETRA_ETSI_FRONT2", f2)
         st = BenchStep(c, 64, 131072, 2.4e6, seed=11, device=dev, demod=demod, iq_format=fmt)
         if pipe:
             st.pipeline()
+            assert len(st.contexts()) == 2 + (f2 == "1")
         if host:
             st.host_feed()
         for _ in range(3):

@@ -9,6 +9,7 @@ int8 soft bits for the channel decoder.  All sample work runs in libtetra_hip.so
 (k_chanfilt, k_timing); this module designs the filters and moves arrays.
 """
 import ctypes
+import os
 import functools
 
 import numpy as np
@@ -321,12 +322,23 @@ class BenchStep:
         self.ev_back = [torch.cuda.Event() for _ in range(2)]
         for e in self.ev_back:
             e.record(self.s_back)
+        # TETRA_ETSI_FRONT2=1 (fused demod, device-resident input): consecutive batches' demods on two
+        # front streams (contexts), so one batch's last workgroups and the next batch's first ones overlap
+        # instead of draining the chip at every launch boundary
+        self.front2 = None
+        if (os.environ.get("TETRA_ETSI_FRONT2") == "1" and self.demod_mode == "fused"
+                and not getattr(self, "hostfed", False)):
+            self.front2 = _hip.Context()
+            self.s_front2 = torch.cuda.Stream(device=dev)
+            self.front2.check(self.front2.lib.tetra_set_stream(self.front2.handle,
+                                                               ctypes.c_void_p(self.s_front2.cuda_stream)), "set_stream")
         self.k = 0
         self.pipelined = True
         return self
 
     def contexts(self):
-        return [self.c] + ([self.back] if self.pipelined else [])
+        return ([self.c] + ([self.back] if self.pipelined else [])
+                + ([self.front2] if getattr(self, "front2", None) is not None else []))
 
     def host_feed(self):
         """PCIe-inclusive mode (bench.py --host-input): every step's batch starts in pinned host
@@ -422,9 +434,10 @@ class BenchStep:
             return
         self.k += 1
         sym, soft, hard, nsym = self.bufs[i]
-        self.s_front.wait_event(self.ev_back[i])        # lower MAC of batch k-2 has consumed buffer i
-        self._demod(self.c, sym, soft, hard, nsym)
-        self.ev_front[i].record(self.s_front)
+        fc, fs = (self.front2, self.s_front2) if self.front2 is not None and i else (self.c, self.s_front)
+        fs.wait_event(self.ev_back[i])                  # lower MAC of batch k-2 has consumed buffer i
+        self._demod(fc, sym, soft, hard, nsym)
+        self.ev_front[i].record(fs)
         self.s_back.wait_event(self.ev_front[i])
         self._lmac(self.back, soft, hard, nsym)
         self.ev_back[i].record(self.s_back)
