@@ -15,7 +15,9 @@ A step = one pass of the hot path over the rank's batch:
                  timing/decision -> lower MAC, every carrier cut into 3932-sample timing chunks
 
 Launch: python bench.py --gpus 1 --steps 5 --warmup 2
+        python bench.py --gpus N ...   (starts torch.distributed.run --nproc-per-node N as a child)
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+        (--gpus must equal the launcher's WORLD_SIZE, or bench exits non-zero before any GPU work)
 """
 import argparse
 import ctypes
@@ -265,8 +267,50 @@ def time_steps(step, steps, warmup, world, sync, on_timed=None):
     return time.perf_counter() - t0
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(a):
+    """`--gpus N` means N GPUs, however bench.py is started.
+
+    Under a launcher (WORLD_SIZE set) the world must equal --gpus, or bench exits non-zero before any
+    GPU work.  Started bare with N > 1, bench starts `torch.distributed.run --nproc-per-node N` on
+    itself as a CHILD process (never exec: nothing here has touched the GPU yet, and the ranks are
+    new processes), lets rank 0's one JSON line through on the inherited stdout and returns the
+    child's exit code.  Returns None when this process is itself the (only or a) rank to run."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != a.gpus:
+            print(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={env_world} ranks; "
+                  f"launch with --nproc-per-node {a.gpus}", file=sys.stderr, flush=True)
+            return 2
+        return None
+    if a.gpus <= 1:
+        return None
+    backend = os.environ.get("TETRA_BENCH_DIST", "nccl")
+    have = torch.cuda.device_count()   # counts devices without initialising HIP in this process
+    if backend == "nccl" and have < a.gpus:
+        print(f"bench.py: --gpus {a.gpus} asks for one GPU per rank but {have} are visible "
+              f"(TETRA_BENCH_DIST=gloo rehearses more ranks than GPUs)", file=sys.stderr, flush=True)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    import subprocess
+    return subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+
+
 def main():
     a = parse()
+    rc = launch_ranks(a)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

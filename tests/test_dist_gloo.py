@@ -126,3 +126,65 @@ def test_two_rank_gloo_matches_single_process():
         x = (0.3 * (rng.standard_normal(4000) + 1j * rng.standard_normal(4000))).astype(np.complex64)
         assert merged[ch] == oracle.SignalProcessor(2.4e6).process(x, 0).tolist()
     assert abs(agg - 3 * 4000 * 2 / 2.0 / 1e6) < 1e-12
+
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(args, **env):
+    import subprocess
+    import sys
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    e.update(env)
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, cwd=REPO, env=e,
+                          capture_output=True, text=True, timeout=120)
+
+
+def test_gpus_must_equal_launcher_world():
+    """A launcher that started 1 rank for --gpus 2 is refused before any GPU work (rc 2)."""
+    r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu"], WORLD_SIZE="1", RANK="0",
+               LOCAL_RANK="0")
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert "--gpus 2" in r.stderr and "WORLD_SIZE=1" in r.stderr
+    assert '{"metric"' not in r.stdout
+
+
+def test_gpus_over_visible_devices_refused_on_rccl():
+    """Bare --gpus 2 with RCCL needs two visible GPUs (none here): refused, nothing launched."""
+    r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu"], TETRA_BENCH_DIST="nccl")
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert "visible" in r.stderr
+
+
+def test_bare_gpus_n_starts_n_ranks_as_a_child(monkeypatch):
+    """Bare --gpus 2 starts torch.distributed.run --nproc-per-node 2 on bench.py with the same
+    arguments, as a child process, and returns its exit code (the GPU run: tests/test_gpu_dist.py)."""
+    import subprocess
+    import sys
+    sys.path.insert(0, REPO)
+    import bench
+    seen = {}
+
+    def fake_call(cmd, env=None):
+        seen["cmd"], seen["env"] = cmd, env
+        return 7
+
+    monkeypatch.setattr(subprocess, "call", fake_call)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setenv("TETRA_BENCH_DIST", "gloo")
+    argv = ["bench.py", "--gpus", "2", "--channels", "256", "--steps", "3"]
+    monkeypatch.setattr(sys, "argv", argv)
+    a = bench.parse()
+    assert bench.launch_ranks(a) == 7
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert cmd[cmd.index("--nproc-per-node") + 1] == "2"
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert os.path.samefile(cmd[cmd.index("--master-port") + 2], os.path.join(REPO, "bench.py"))
+    assert cmd[-len(argv) + 1:] == argv[1:]
+    # one rank, or a launcher-started rank, runs in this process
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "1"])
+    assert bench.launch_ranks(bench.parse()) is None
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    assert bench.launch_ranks(bench.parse()) is None
