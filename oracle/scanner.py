@@ -6,9 +6,14 @@ numpy from that survey row's description of them, in the dtype numpy computes th
 float32 angles, differences and wrap; the cluster distance in float64).  Vectorised: the reference's
 per-sample loops become array expressions with the same comparisons.
 
-Parity unpinned against the reference itself: pinned by analytic known answers in
-tests/test_scanner.py -- an ideal pi/4-DQPSK walk gives modulation confidence 1.0, a phase walk
-whose strided differences spell the sync pattern gives correlation 1.0, tones at the decision edges.
+validate_frames (:149-202) and analyze_signal (:233-289) run the compat oracle's process() and
+decode() (oracle/compat.py) for the frame validation.
+
+Pinned (round 5) to the reference's own outputs: tests/golden/g5_scanner.npz records the reference
+TetraSignalDetector's six methods on 20 seeded cases x {complex64, complex128}
+(tests/golden/make_golden_scanner.py); tests/test_scanner.py checks this module against every one,
+and the analytic known answers (an ideal pi/4-DQPSK walk gives modulation confidence 1.0, a phase walk
+whose strided differences spell the sync pattern gives correlation 1.0, tones at the decision edges).
 """
 import numpy as np
 
@@ -79,3 +84,54 @@ def check_power_stability(x, num_windows=5):
     ws = len(x) // num_windows
     p = [calculate_power(x[i * ws:(i + 1) * ws]) for i in range(num_windows)]
     return bool(np.std(p) < 10.0)
+
+
+def validate_frames(x, fs):
+    """(frames_valid, crc_pass_rate): process() + decode() of the chunk (scanner.py:149-202) -- at
+    least 10000 samples and 255 symbols; valid with >= 2 frames and a CRC pass rate above 0.5."""
+    import compat
+    x = np.asarray(x)
+    if len(x) < 10000:
+        return False, 0.0
+    try:
+        hard = compat.SignalProcessor(fs).process(x)
+        if len(hard) < 255:
+            return False, 0.0
+        frames = compat.decode_with_mac(hard)
+    except Exception:
+        return False, 0.0
+    if not frames:
+        return False, 0.0
+    passed = 0.0
+    for f in frames:
+        bc = f.get('burst_crc')
+        if bc is True:
+            passed += 1
+        elif bc is not False and 'type' in f and 'number' in f:
+            passed += 0.5
+    rate = passed / max(len(frames), 1)
+    return len(frames) >= 2 and rate > 0.5, rate
+
+
+def analyze_signal(x, fs, bottom=-85.0):
+    """The detector's verdict dict (scanner.py:233-289)."""
+    power = calculate_power(x, bottom)
+    is_mod, mod_conf = detect_tetra_modulation(x)
+    has_sync, sync_corr = detect_sync_pattern(x, fs)
+    frames_valid, crc_rate = validate_frames(x, fs)
+    stable = check_power_stability(x)
+    if has_sync and is_mod:
+        confidence = mod_conf * 0.4 + sync_corr * 0.4 + crc_rate * 0.2
+    elif has_sync:
+        confidence = sync_corr * 0.6
+    elif is_mod:
+        confidence = mod_conf * 0.5
+    else:
+        confidence = 0.0
+    is_tetra = bool(is_mod and has_sync and stable)
+    if frames_valid:
+        is_tetra = True
+        confidence = max(confidence, 0.7)
+    return {'power_db': power, 'is_tetra': is_tetra, 'confidence': confidence, 'modulation_confidence': mod_conf,
+            'sync_detected': has_sync, 'sync_correlation': sync_corr, 'frames_validated': frames_valid,
+            'crc_pass_rate': crc_rate, 'power_stable': stable, 'signal_present': power > bottom}

@@ -100,3 +100,19 @@ def family(name, rng, n, fs):
     else:
         raise ValueError(name)
     return sc16_round(x)
+
+
+# ---------------------------------------------------------------- g5_scanner.npz input encodings
+# A scanner case's input is stored as one of (so the fixture stays small and decodes exactly):
+#   c_<i>  complex64 samples;
+#   q_<i>  int16 [n, 2] on the SC16 grid (x = q / 32768 in float32, as sc16_round);
+#   k_<i>  uint8 constellation indices with p_<i> complex64 [4] points and r_<i> = (repeat, offset):
+#          x = repeat(p[k], repeat)[offset:] (a phase-step walk held for `repeat` samples per symbol).
+def scanner_input(z, i):
+    if f"c_{i}" in z.files:
+        return z[f"c_{i}"]
+    if f"q_{i}" in z.files:
+        q = z[f"q_{i}"]
+        return (q[:, 0].astype(np.float32) / 32768 + 1j * (q[:, 1].astype(np.float32) / 32768)).astype(np.complex64)
+    rep, off = (int(v) for v in z[f"r_{i}"])
+    return np.repeat(z[f"p_{i}"][z[f"k_{i}"]], rep)[off:]

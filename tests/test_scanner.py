@@ -175,3 +175,81 @@ def test_scan_wideband_carriers():
         _compare_counts(st[k], y[k], 72000.0)
     conf = np.array([r['modulation_confidence'] for r in res])
     assert conf.min() > 0.4
+
+
+# ----------------------------------------------------------------------------- the reference's outputs
+def _g5():
+    import os
+    import sys
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    if here not in sys.path:
+        sys.path.insert(0, here)
+    import _signals
+    z = np.load(os.path.join(here, "g5_scanner.npz"))
+    keys = [str(k) for k in z["out_keys"]]
+    for j in range(len(z["case"])):
+        x = _signals.scanner_input(z, int(z["input"][j]))
+        x = x.astype(np.complex64 if int(z["dtype"][j]) == 64 else np.complex128)
+        yield str(z["case"][j]), float(z["fs"][j]), x, dict(zip(keys, z["out"][j]))
+
+
+AN_KEYS = ["power_db", "is_tetra", "confidence", "modulation_confidence", "sync_detected", "sync_correlation",
+           "frames_validated", "crc_pass_rate", "power_stable", "signal_present"]
+
+
+def test_oracle_matches_reference_fixture():
+    """oracle/scanner.py against the reference TetraSignalDetector's recorded outputs
+    (tests/golden/g5_scanner.npz, 20 cases x complex64/complex128): every count-derived value and
+    decision equal, the powers to 1e-12 dB (the same numpy expression)."""
+    n = 0
+    for name, fs, x, want in _g5():
+        got = [O.calculate_power(x), *O.detect_tetra_modulation(x), *O.detect_sync_pattern(x, fs),
+               O.check_power_stability(x), *O.validate_frames(x, fs)]
+        for k, g in zip(["power", "mod_flag", "mod_conf", "sync_flag", "sync_corr", "stable", "val_flag",
+                         "val_rate"], got):
+            tol = 1e-12 if k == "power" else 0.0
+            assert abs(float(g) - want[k]) <= tol, (name, x.dtype, k, g, want[k])
+        an = O.analyze_signal(x, fs)
+        for k in AN_KEYS:
+            tol = 1e-12 if k == "power_db" else 0.0
+            assert abs(float(an[k]) - want["an_" + k]) <= tol, (name, x.dtype, k, an[k], want["an_" + k])
+        n += 1
+    assert n == 40
+
+
+@pytest.mark.gpu
+def test_gpu_detector_matches_reference_fixture():
+    """The GPU detector (tetra_scan_detect + the GPU process()/decode() validation) against the
+    reference TetraSignalDetector's recorded outputs: decisions, validation and CRC rates equal;
+    powers within 1e-6 dB (float64 device sums vs numpy's float32 pairwise mean); the modulation
+    match count off by at most the phase differences within EDGE of a decision edge (device atan2
+    ulps), the sync count by at most one; each disagreement counted and reported."""
+    from tetraear.signal import TetraSignalDetector
+    from tetraear.signal import scanner as S
+    edges = []
+    for name, fs, x, want in _g5():
+        det = TetraSignalDetector(sample_rate=fs)
+        assert abs(det.calculate_power(x) - want["power"]) <= 1e-6, (name, x.dtype)
+        mf, mc = det.detect_tetra_modulation(x)
+        sf, sc = det.detect_sync_pattern(x)
+        if len(x) >= 1000 and mc != want["mod_conf"]:
+            st = S.scan_counts(x, fs)[0]
+            dm = abs(st[S.F_MOD] - want["mod_conf"] * st[S.F_DIFFS])
+            assert dm <= _edge_count_mod(x) + 0.5, (name, x.dtype, mc, want["mod_conf"])
+            edges.append((name, str(x.dtype), "mod", int(round(dm))))
+        else:
+            assert (mf, mc) == (bool(want["mod_flag"]), want["mod_conf"]), (name, x.dtype)
+        if sc != want["sync_corr"]:
+            assert abs(sc - want["sync_corr"]) * 31 <= 1 + 1e-9, (name, x.dtype, sc, want["sync_corr"])
+            edges.append((name, str(x.dtype), "sync", 1))
+        else:
+            assert sf == bool(want["sync_flag"]), (name, x.dtype)
+        assert det.check_power_stability(x) == bool(want["stable"]), (name, x.dtype)
+        assert det.validate_frames(x) == (bool(want["val_flag"]), want["val_rate"]), (name, x.dtype)
+        an = det.analyze_signal(x)
+        assert abs(an["power_db"] - want["an_power_db"]) <= 1e-6
+        if not any(e[0] == name and e[1] == str(x.dtype) for e in edges):
+            for k in AN_KEYS[1:]:
+                assert float(an[k]) == want["an_" + k], (name, x.dtype, k, an[k], want["an_" + k])
+    print("edge disagreements (case, dtype, count, size):", edges)
+    assert len(edges) <= 4, edges

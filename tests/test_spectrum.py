@@ -274,3 +274,19 @@ def test_process_batch_afc_feeds_the_demod_on_device():
     h2, s2, n2 = p.process_batch(x, fo)
     h3, s3, n3 = p.process_batch(x, np.array(offs) * BIN_HZ)
     assert np.array_equal(h2, hard) and np.array_equal(s2, soft) and np.array_equal(h3, hard) and np.array_equal(n3, ns)
+    # device-tensor samples: the format follows the dtype, a strided view is made contiguous first
+    xt = torch.from_numpy(x).to("cuda")
+    h4, s4, n4 = p.process_batch(xt, fo)
+    assert np.array_equal(h4, hard) and np.array_equal(s4, soft) and np.array_equal(n4, ns)
+    h5, _, n5 = p.process_batch(torch.view_as_real(xt), fo)                      # float32 [C, N, 2]
+    assert np.array_equal(h5, hard) and np.array_equal(n5, ns)
+    wide = torch.zeros((len(x), 2 * x.shape[1]), dtype=torch.complex64, device="cuda")
+    wide[:, ::2] = xt
+    h6, _, n6 = p.process_batch(wide[:, ::2], fo)                                # non-contiguous view
+    assert np.array_equal(h6, hard) and np.array_equal(n6, ns)
+    x128 = x.astype(np.complex128)
+    h7, s7, n7 = p.process_batch(torch.from_numpy(x128).to("cuda"), fo)          # complex128: the cf64 chain
+    h8, s8, n8 = p.process_batch(x128, np.array(offs) * BIN_HZ)
+    assert np.array_equal(h7, h8) and np.array_equal(s7, s8) and np.array_equal(n7, n8)
+    with pytest.raises(TypeError):
+        p.process_batch(torch.zeros((2, 4096), dtype=torch.int32, device="cuda"), fo[:2])

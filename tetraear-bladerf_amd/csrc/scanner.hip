@@ -9,6 +9,13 @@
 //   * the mean power |x|^2 of the chunk and of its five equal windows (power stability).
 // The host turns these counts into the detector's decisions (tetraear/signal/scanner.py).
 //
+// The cluster test runs on the chunk normalised by its peak magnitude, as scanner.py:71 does before
+// its angles: d = max|x| + 1e-10 in the dtype (|x| as numpy's abs: float32 hypot through double,
+// float64 hypot), then numpy's complex-by-real division (its Smith form with a zero imaginary
+// divisor: ((re + im*0) * (1/d), (im - re*0) * (1/d))).  The sync bits use the raw samples, as
+// scanner.py:110-117 does.  Rows of any length: the sync bits are held in LDS SC_MAXBITS at a time,
+// consecutive passes overlapping by 64 bits so every 31-bit window lies wholly inside one pass.
+//
 // Phase arithmetic follows numpy's on the input dtype: complex64 -> float32 angles, differences and
 // wrap ((d + pi) mod 2 pi - pi, Python-style remainder), the cluster distance test in float64 against
 // the float64 multiples of pi/4; complex128 -> float64 throughout.  atan2 is the device's (the host's
@@ -28,12 +35,22 @@ template <> struct Cx<float2> {
     using R = float;
     static __device__ R ang(float2 v) { return atan2f(v.y, v.x); }
     static __device__ double pw(float2 v) { return (double)v.x * v.x + (double)v.y * v.y; }
+    // numpy's |z| for complex64: hypotf, which glibc evaluates as sqrt in double rounded once to float
+    static __device__ R mag(float2 v) { return (float)sqrt((double)v.x * v.x + (double)v.y * v.y); }
 };
 template <> struct Cx<double2> {
     using R = double;
     static __device__ R ang(double2 v) { return atan2(v.y, v.x); }
     static __device__ double pw(double2 v) { return v.x * v.x + v.y * v.y; }
+    static __device__ R mag(double2 v) { return hypot(v.x, v.y); }
 };
+// angle of z / d (scanner.py:71) with numpy's complex division by (d + 0j): rat = 0 / d, scl = 1 / (d + 0 * rat)
+template <typename T, typename R> __device__ inline R ang_scaled(T v, R rat, R scl) {
+    T u;
+    u.x = (v.x + v.y * rat) * scl;
+    u.y = (v.y - v.x * rat) * scl;
+    return Cx<T>::ang(u);
+}
 
 // numpy's float remainder (Python semantics: the result takes the divisor's sign)
 template <typename R> __device__ inline R pymod(R a, R b) {
@@ -84,10 +101,21 @@ __global__ __launch_bounds__(SC_T) void k_scan_detect(const T *__restrict__ x, l
     __shared__ uint32_t bits[SC_MAXBITS / 32 + 2];
     __shared__ double red[SC_T / 64];
     __shared__ int redi[SC_T / 64];
+    __shared__ R redm[SC_T / 64];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const long ws = N / 5;   // stability windows [i ws, (i + 1) ws), i < 5
     for (int ch = blockIdx.x; ch < C; ch += gridDim.x) {
         const T *row = x + (size_t)ch * N;
+        // --- peak magnitude of the chunk (scanner.py:71's normaliser)
+        R mx = 0;
+        for (long n = tid; n < N; n += SC_T) mx = fmax(mx, Cx<T>::mag(row[n]));
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+        if (lane == 0) redm[wv] = mx;
+        __syncthreads();
+        for (int w = 0; w < SC_T / 64; ++w) mx = fmax(mx, redm[w]);
+        const R dnm = mx + (R)1e-10;
+        const R rat = (R)0 / dnm, scl = (R)1 / (dnm + (R)0 * rat);
         // --- modulation cluster test + power, tile by tile
         double p_all = 0.0, p_w[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
         int matches = 0;
@@ -97,14 +125,14 @@ __global__ __launch_bounds__(SC_T) void k_scan_detect(const T *__restrict__ x, l
                 const long n = t0 + tid + SC_T * r;
                 if (n < N) {
                     const T v = row[n];
-                    ang[1 + tid + SC_T * r] = Cx<T>::ang(v);
+                    ang[1 + tid + SC_T * r] = ang_scaled<T, R>(v, rat, scl);
                     const double p = Cx<T>::pw(v);
                     p_all += p;
                     const long w = ws > 0 ? n / ws : 5;
                     if (w < 5) p_w[w] += p;
                 }
             }
-            if (tid == 0) ang[0] = t0 > 0 ? Cx<T>::ang(row[t0 - 1]) : (R)0;
+            if (tid == 0) ang[0] = t0 > 0 ? ang_scaled<T, R>(row[t0 - 1], rat, scl) : (R)0;
             __syncthreads();
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -116,31 +144,38 @@ __global__ __launch_bounds__(SC_T) void k_scan_detect(const T *__restrict__ x, l
             }
             __syncthreads();
         }
-        // --- sync bits of the strided samples, packed by ballots (bit k = lane k & 63 of a 64-chunk)
+        // --- sync bits of the strided samples, packed by ballots (bit k = lane k & 63 of a 64-chunk),
+        //     SC_MAXBITS per pass; pass p holds bits [p0, p0 + nb) and scores the windows that start in
+        //     it and end inside it; the next pass starts 64 bits before this one's end
         const long K = (N + D - 1) / D;             // strided samples
         const long nbits = K > 0 ? K - 1 : 0;
-        const long nb = nbits < SC_MAXBITS ? nbits : SC_MAXBITS;
-        for (long k0 = 64L * wv; k0 < nb; k0 += 64L * (SC_T / 64)) {
-            const long k = k0 + lane;
-            int b = 0;
-            if (k < nb) {
-                const R a0 = Cx<T>::ang(row[k * D]), a1 = Cx<T>::ang(row[(k + 1) * D]);
-                b = sync_bit<R>(wrap<R>(a1 - a0));
-            }
-            const unsigned long long m = __ballot(b);
-            if (lane == 0) {   // k0 < nb <= SC_MAXBITS: words k0/32, k0/32 + 1 < SC_MAXBITS/32 + 2
-                bits[k0 / 32] = (uint32_t)m;
-                bits[k0 / 32 + 1] = (uint32_t)(m >> 32);
-            }
-        }
-        __syncthreads();
-        // --- best 31-bit match over window starts 0 .. nb - 32 (scanner.py's range(len(bits) - 31))
-        const long npos = nb > 31 ? nb - 31 : 0;
+        const long npos = nbits > 31 ? nbits - 31 : 0;   // scanner.py's range(len(bits) - 31)
         int best = 0;
-        for (long i = tid; i < npos; i += SC_T) {
-            const uint64_t v = ((uint64_t)bits[(i >> 5) + 1] << 32) | bits[i >> 5];
-            const uint32_t wnd = (uint32_t)(v >> (i & 31)) & 0x7FFFFFFFu;
-            best = max(best, 31 - __popc(wnd ^ pattern));
+        for (long p0 = 0; p0 == 0 || p0 + 31 < nbits; p0 += SC_MAXBITS - 64) {
+            const long nb = nbits - p0 < SC_MAXBITS ? nbits - p0 : SC_MAXBITS;
+            __syncthreads();   // the previous pass's window reads are done
+            for (long k0 = 64L * wv; k0 < nb; k0 += 64L * (SC_T / 64)) {
+                const long k = k0 + lane;
+                int b = 0;
+                if (k < nb) {
+                    const long g = p0 + k;
+                    const R a0 = Cx<T>::ang(row[g * D]), a1 = Cx<T>::ang(row[(g + 1) * D]);
+                    b = sync_bit<R>(wrap<R>(a1 - a0));
+                }
+                const unsigned long long m = __ballot(b);
+                if (lane == 0) {   // k0 < nb <= SC_MAXBITS: words k0/32, k0/32 + 1 < SC_MAXBITS/32 + 2
+                    bits[k0 / 32] = (uint32_t)m;
+                    bits[k0 / 32 + 1] = (uint32_t)(m >> 32);
+                }
+            }
+            __syncthreads();
+            const long lpos = nb > 31 ? nb - 31 : 0;   // windows [p0, p0 + lpos) lie inside this pass
+            for (long i = tid; i < lpos; i += SC_T) {
+                const uint64_t v = ((uint64_t)bits[(i >> 5) + 1] << 32) | bits[i >> 5];
+                const uint32_t wnd = (uint32_t)(v >> (i & 31)) & 0x7FFFFFFFu;
+                best = max(best, 31 - __popc(wnd ^ pattern));
+            }
+            if (nbits - p0 <= SC_MAXBITS) break;
         }
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
@@ -177,8 +212,6 @@ int tetra_scan_detect(tetra_ctx *ctx, const void *iq, int iq_fmt, size_t C, size
     if (iq_fmt != TETRA_CF32 && iq_fmt != TETRA_CF64)
         return tetra_fail(ctx, TETRA_E_INVALID, "scan detector takes cf32 or cf64 samples");
     if (!iq || !stats || C == 0 || N == 0 || downsample < 1) return tetra_fail(ctx, TETRA_E_INVALID, "bad scan request");
-    if ((N + downsample - 1) / downsample - 1 > (size_t)SC_MAXBITS)
-        return tetra_fail(ctx, TETRA_E_INVALID, "more than %d sync bits per channel", SC_MAXBITS);
     const size_t bps = iq_fmt == TETRA_CF32 ? 8 : 16;
     Staging st(ctx);
     const void *xd = st.in(iq, C * N * bps);

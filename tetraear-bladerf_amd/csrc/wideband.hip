@@ -1169,8 +1169,11 @@ int channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size_t Nw,
         const size_t lds = (size_t)std::max(rows * RS_C, RS_C * (RS_T + 1)) * 8;
         if (lds > 160 * 1024) return tetra_fail(ctx, TETRA_E_INVALID, "resampler tile does not fit LDS");
         const dim3 gr((unsigned)((M + RS_C - 1) / RS_C), (unsigned)((n_keep + RS_T - 1) / RS_T));
-        if (Q == 23)   // D = M / 2 (fused analysis: Y rotated)
+        if (Q == 23 && fused)   // D = M / 2 with the fused analysis: Y rotated there
             hipLaunchKernelGGL((k_pfb_resamp<23, false>), gr, dim3(256), lds, ctx->stream, u, M, (int)nblk, P->up, P->down,
+                               taps + L, yd, (int)n_keep);
+        else if (Q == 23)       // D = M / 2 plan on the unfused analysis: the resampler rotates
+            hipLaunchKernelGGL((k_pfb_resamp<23, true>), gr, dim3(256), lds, ctx->stream, u, M, (int)nblk, P->up, P->down,
                                taps + L, yd, (int)n_keep);
         else if (fused)
             hipLaunchKernelGGL((k_pfb_resamp<45, false>), gr, dim3(256), lds, ctx->stream, u, M, (int)nblk, P->up, P->down,

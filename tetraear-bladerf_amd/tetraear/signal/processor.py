@@ -51,6 +51,18 @@ def _fmt_of(x):
     return _hip.TETRA_CF64
 
 
+def _tensor_fmt(x):
+    """Library sample format of a torch tensor batch: complex64 [C, N] or float32 [C, N, 2] is cf32,
+    complex128 [C, N] or float64 [C, N, 2] is cf64; anything else is refused (never reinterpreted)."""
+    import torch
+    if x.dim() == 2 and x.dtype in (torch.complex64, torch.complex128):
+        return _hip.TETRA_CF32 if x.dtype == torch.complex64 else _hip.TETRA_CF64
+    if x.dim() == 3 and x.shape[2] == 2 and x.dtype in (torch.float32, torch.float64):
+        return _hip.TETRA_CF32 if x.dtype == torch.float32 else _hip.TETRA_CF64
+    raise TypeError(f"process_batch: a tensor batch must be complex64/complex128 [C, N] or float32/float64 "
+                    f"[C, N, 2], not {x.dtype} {tuple(x.shape)}")
+
+
 def _as_complex(x, fmt):
     t = np.complex64 if fmt == _hip.TETRA_CF32 else np.complex128
     return np.ascontiguousarray(x, dtype=t)
@@ -313,8 +325,12 @@ class SignalProcessor:
         afc = isinstance(freq_offsets, str)
         if afc and freq_offsets != "afc":
             raise ValueError("freq_offsets must be None, an array of Hz, a device tensor or 'afc'")
-        fmt = _fmt_of(x) if not hasattr(x, "data_ptr") else _hip.TETRA_CF32
-        xc = _as_complex(x, fmt) if not hasattr(x, "data_ptr") else x
+        if hasattr(x, "data_ptr"):
+            fmt = _tensor_fmt(x)
+            xc = x.contiguous()
+        else:
+            fmt = _fmt_of(x)
+            xc = _as_complex(x, fmt)
         plan, m, _ = compat_plan(self.sample_rate, N, fmt)
         smax = m // plan.sps + 1
         soft = np.empty((C, smax), np.complex128)

@@ -91,7 +91,8 @@ def grouped_om(plan, m2=M2_CHUNK):
     """The wideband timing takes its Oerder-Meyr class sums from the resampler's group partials
     (tetra_channelize_om + tetra_etsi_timing_om) where the plan's output groups hold whole classes
     (up a multiple of 4: the D = M / 2 design) and TETRA_WB_OM is not 0."""
-    return plan.c.up % 4 == 0 and plan.c.up <= 64 and m2 % 4 == 0 and os.environ.get("TETRA_WB_OM", "1") != "0"
+    return (plan.c.up % 4 == 0 and plan.c.up <= 64 and m2 % 4 == 0 and m2 >= 16
+            and os.environ.get("TETRA_WB_OM", "1") != "0")
 
 
 class WidebandReceiver:
@@ -128,7 +129,7 @@ class WidebandReceiver:
     def grouped_om(self):
         """Whether demod forms the timing's Oerder-Meyr sums in the resampler (the D = M / 2 plan;
         TETRA_WB_OM=0 keeps the timing's own pass over y, for A/B)."""
-        return grouped_om(self.plan)
+        return grouped_om(self.plan, self.m2)
 
     def demod(self, x):
         """x [Nw] -> (hard, soft_bits, sym, nsym) per (carrier, chunk): [M, nchunk, smax] uint8,
