@@ -8,7 +8,10 @@ reference's float decisions (threshold comparisons, the adaptive re-search rule)
 frame dicts, through decode_frame's MAC PDU stage (decoder.py:994-1053: parse_mac_pdu on the GPU,
 the drop rule, mac_pdu, the encryption fields).  Call metadata, SDS and decryption
 (decoder.py:1055-1117) are not part of this hot-path build: they stay the reference's Python and
-attach through ``upper_mac``.
+attach through ``upper_mac``, which runs them -- the reference's parser methods and _decrypt_frame --
+whenever the reference's package root is on sys.path after this build's (tetraear/_overlay.py).
+Then the other members of the reference's TetraDecoder (common_keys, _decrypt_frame,
+format_frame_info, ...) resolve too; the hot-path methods here never delegate.
 
 ``mode="etsi"`` (or ``TETRAEAR_DEMOD=etsi`` for callers that construct ``TetraDecoder()``
 unchanged) decodes ETSI channel coding (cell acquisition from the BSCH, descramble, deinterleave,
@@ -22,7 +25,7 @@ from typing import Optional
 
 import numpy as np
 
-from tetraear import _hip
+from tetraear import _hip, _overlay
 from tetraear.core.protocol import TetraProtocolParser, burst_data_bits, burst_from_bits
 
 logger = logging.getLogger(__name__)
@@ -97,6 +100,48 @@ class TetraDecoder:
         from tetraear.signal.processor import demod_mode
         self.mode = demod_mode(mode)
         self._etsi = None
+
+    # ------------------------------------------------------------------ keys and the reference's rest
+    def set_keys(self, keys):
+        """User keys for the decryption's brute force (decoder.py:101-138).  Each hex string (spaces,
+        ':' and '-' ignored) becomes ('TEA1', key) for 10 bytes, or the same 16 bytes as TEA2, TEA3
+        and TEA4; a 32-byte key contributes its first 16 bytes that way.  Other lengths and strings
+        that do not parse are logged and skipped."""
+        self.user_keys = []
+        for text in keys:
+            try:
+                raw = bytes.fromhex(text.replace(' ', '').replace(':', '').replace('-', ''))
+                if len(raw) == 10:
+                    self.user_keys.append(('TEA1', raw))
+                elif len(raw) in (16, 32):
+                    if len(raw) == 32:
+                        logger.warning("256-bit key provided; using first 128 bits for TEA2/TEA3/TEA4 attempts")
+                    self.user_keys += [(alg, raw[:16]) for alg in ('TEA2', 'TEA3', 'TEA4')]
+                else:
+                    logger.warning(f"Invalid key length: {len(raw)} bytes (expected 10 or 16)")
+            except Exception as e:
+                logger.error(f"Failed to parse key '{text}': {e}")
+        logger.info(f"Loaded {len(self.user_keys)} user-provided encryption keys")
+
+    def _reference(self):
+        return _overlay.reference_module("core/decoder").TetraDecoder
+
+    def __getattr__(self, name):
+        """Members of the reference's TetraDecoder this build does not define -- the common-key
+        table (decoder.py:36-99), _decrypt_frame (:576-834), format_frame_info and
+        _get_frame_type_name (:1121-1200) -- bound to this decoder, when the reference is on the
+        path.  Only reached when normal lookup fails: the hot-path methods are never the reference's."""
+        if name.startswith("__") or not _overlay.active():
+            raise AttributeError(f"{type(self).__name__!r} object has no attribute {name!r}")
+        ref = self._reference()
+        if name == "common_keys":   # built on first use by the reference's own setup, user keys kept
+            users = self.__dict__.get("user_keys", [])
+            _overlay.bind(self, ref, "_setup_common_keys")()
+            self.user_keys = users
+            return self.__dict__["common_keys"]
+        if not hasattr(ref, name):
+            raise AttributeError(f"{type(self).__name__!r} object has no attribute {name!r}")
+        return _overlay.bind(self, ref, name)
 
     # ------------------------------------------------------------------ bits
     def symbols_to_bits(self, symbols):
@@ -222,7 +267,7 @@ class TetraDecoder:
         bytes with a distinct-byte ratio above 0.7 count as encrypted (decoder.py:1036-1053).
         Then upper_mac (call metadata / SDS, decoder.py:1055-1091) runs on the kept frame."""
         if pdu is None:
-            return frame if burst.crc_ok else None
+            return self.upper_mac(frame, burst, None) if burst.crc_ok else None
         frame['mac_pdu'] = {'type': pdu.pdu_type.name, 'encrypted': pdu.encrypted, 'address': pdu.address,
                             'length': pdu.length, 'data': pdu.data}
         if pdu.encrypted:
@@ -262,18 +307,58 @@ class TetraDecoder:
         return frame
 
     def upper_mac(self, frame, burst, mac_pdu=None):
-        """Hook for the reference's call metadata / SDS / decryption (decoder.py:1055-1117), called
-        with every frame the MAC PDU stage keeps and its MacPDU (None when the slot has none).
+        """The reference's call metadata, SDS and decryption (decoder.py:1055-1117), called with every
+        frame the MAC PDU stage keeps and its MacPDU (None when the slot has none).
 
-        This build stops at the MAC PDU and returns the frame unchanged: its frames carry the
-        reference's lower-MAC and MAC PDU fields (number, header, burst_crc, encrypted,
-        encryption_algorithm, additional_info['encryption_mode'], mac_pdu) and NOT the upper-MAC
-        ones -- call_metadata, sds_message, decoded_text, is_reassembled, additional_info's
-        talkgroup / source_ssi / mcc / mnc / sds_text -- nor auto_decrypt's decryption (upper MAC
-        out of scope; tests/test_oracle_golden.py declares exactly these keys as the gap).  A hook
-        that runs the reference's parsers here restores them; to keep the reference's frame
-        selection it must also drop (return None) a frame whose CRC failed when one of those parsers
-        raises, as decoder.py:1097-1100 does.  INTEGRATION.md shows such a hook."""
+        With the reference on the path (tetraear/_overlay.py) this runs them: the parser's
+        parse_call_metadata / parse_sds_data and this decoder's _decrypt_frame are the reference's own
+        methods, and the frame gains the reference's upper-MAC keys -- call_metadata, sds_message,
+        decoded_text, is_reassembled, additional_info's talkgroup / source_ssi / mcc / mnc / sds_text,
+        and the decryption's fields -- with the reference's frame selection: an exception in the
+        metadata / SDS step drops a frame whose CRC failed (decoder.py:1097-1100).  Without the
+        reference it returns the frame unchanged: this build's frames then carry the lower-MAC and
+        MAC PDU fields only (upper MAC out of scope; tests/test_oracle_golden.py declares
+        exactly the keys above as the gap).  A subclass may override it."""
+        if not _overlay.active():
+            return frame
+        info = frame['additional_info']
+        if mac_pdu is not None:
+            try:
+                meta = self.protocol_parser.parse_call_metadata(mac_pdu)
+                if meta:
+                    frame['call_metadata'] = {
+                        'call_type': meta.call_type, 'talkgroup_id': meta.talkgroup_id, 'source_ssi': meta.source_ssi,
+                        'dest_ssi': meta.dest_ssi, 'channel': meta.channel_allocated,
+                        'call_identifier': meta.call_identifier, 'priority': meta.call_priority, 'mcc': meta.mcc,
+                        'mnc': meta.mnc, 'encryption': meta.encryption_enabled,
+                        'encryption_alg': meta.encryption_algorithm}
+                    for key, v in (('talkgroup', meta.talkgroup_id), ('source_ssi', meta.source_ssi),
+                                   ('mcc', meta.mcc), ('mnc', meta.mnc)):
+                        if v:
+                            info[key] = v
+                payload = mac_pdu.reassembled_data if mac_pdu.reassembled_data else mac_pdu.data
+                if not mac_pdu.encrypted and len(payload) > 0:
+                    text = self.protocol_parser.parse_sds_data(payload)
+                    if text and not text.startswith("[BIN]"):
+                        frame['sds_message'] = frame['decoded_text'] = text
+                        info['sds_text'] = text[:50]
+                        if mac_pdu.reassembled_data:
+                            frame['is_reassembled'] = True
+                            info['description'] += " (Reassembled)"
+            except Exception as e:
+                logger.debug(f"MAC PDU parsing error: {e}")
+                if not burst.crc_ok:
+                    return None
+        if frame.get('encrypted') and (self.key_manager or self.auto_decrypt):
+            frame = self._decrypt_frame(frame)
+            if frame.get('decrypted') and 'decrypted_bytes' in frame:
+                try:
+                    text = self.protocol_parser.parse_sds_data(bytes.fromhex(frame['decrypted_bytes']))
+                    if text:
+                        frame['sds_message'] = frame['decoded_text'] = text
+                        info['sds_text'] = text[:50]
+                except Exception:
+                    pass
         return frame
 
     def _etsi_frames(self, raw):

@@ -7,9 +7,12 @@ Mirrors the hot-path part of /root/reference/tetraear/core/protocol.py:
                                                              protocol.py:142-347
   parse_mac_pdu (MAC PDU headers, fragment reassembly)          protocol.py:349-596
 Burst typing, slicing, the CRC and the MAC PDU header fields run in libtetra_hip.so.  The rest of
-the reference's upper MAC (SDS, LIP, call metadata -- protocol.py:597-1300) is out of scope of
-this hot-path build and stays the reference's Python; ``upper_mac`` hooks are where it attaches
-(INTEGRATION.md).
+the reference's upper MAC (call metadata, SDS, LIP, GSM 7-bit text -- protocol.py:597-1300) is out
+of scope of this hot-path build and stays the reference's Python: with the reference's package
+root on sys.path after this build's (tetraear/_overlay.py), ``parse_call_metadata``,
+``parse_sds_message``, ``parse_sds_data``, ``parse_lip``, ``extract_voice_payload``,
+``format_call_metadata`` and their helpers run the reference's own methods on this parser's state
+(MCC / MNC / colour code, statistics), with this module's enums and dataclasses.
 """
 import logging
 from dataclasses import dataclass
@@ -18,7 +21,7 @@ from typing import Optional
 
 import numpy as np
 
-from tetraear import _hip
+from tetraear import _hip, _overlay
 
 logger = logging.getLogger(__name__)
 
@@ -310,4 +313,52 @@ class TetraProtocolParser:
         return pdu
 
     def get_statistics(self):
-        return dict(self.stats)
+        """The counters plus clear / encrypted shares and the CRC success rate, in percent
+        (protocol.py:1261-1275)."""
+        frames = self.stats['clear_mode_frames'] + self.stats['encrypted_frames']
+        clear = self.stats['clear_mode_frames'] / frames * 100 if frames > 0 else 0
+        enc = self.stats['encrypted_frames'] / frames * 100 if frames > 0 else 0
+        return {**self.stats, 'clear_mode_percentage': clear, 'encrypted_percentage': enc,
+                'crc_success_rate': self.stats['crc_pass'] / max(1, self.stats['total_bursts']) * 100}
+
+    # ------------------------------------------------------------ upper MAC: the reference's
+    def _reference(self):
+        mod = _overlay.reference_module("core/protocol", patch={
+            "BurstType": BurstType, "ChannelType": ChannelType, "PDUType": PDUType, "TetraBurst": TetraBurst,
+            "MacPDU": MacPDU, "CallMetadata": CallMetadata})
+        return mod.TetraProtocolParser
+
+    def __getattr__(self, name):
+        """Members of the reference parser this build does not define (the upper MAC's helpers,
+        protocol.py:623-1260), bound to this parser; only reached when normal lookup fails, so the
+        hot-path methods above are never the reference's."""
+        if name.startswith("__") or not _overlay.active():
+            raise AttributeError(f"{type(self).__name__!r} object has no attribute {name!r}")
+        ref = self._reference()
+        if not hasattr(ref, name):
+            raise AttributeError(f"{type(self).__name__!r} object has no attribute {name!r}")
+        return _overlay.bind(self, ref, name)
+
+    def parse_call_metadata(self, mac_pdu):
+        """Talkgroup / SSI / channel of a MAC PDU (protocol.py:597-621), the reference's."""
+        return _overlay.bind(self, self._reference(), "parse_call_metadata")(mac_pdu)
+
+    def parse_sds_message(self, mac_pdu):
+        """SDS text of a MAC PDU (protocol.py:786-800), the reference's."""
+        return _overlay.bind(self, self._reference(), "parse_sds_message")(mac_pdu)
+
+    def parse_sds_data(self, data):
+        """SDS payload bytes to text (protocol.py:802-1018), the reference's."""
+        return _overlay.bind(self, self._reference(), "parse_sds_data")(data)
+
+    def parse_lip(self, data):
+        """Location Information Protocol payload (protocol.py:1020-1112), the reference's."""
+        return _overlay.bind(self, self._reference(), "parse_lip")(data)
+
+    def extract_voice_payload(self, mac_pdu):
+        """Voice frame bytes of a traffic MAC PDU (protocol.py:1239-1259), the reference's."""
+        return _overlay.bind(self, self._reference(), "extract_voice_payload")(mac_pdu)
+
+    def format_call_metadata(self, metadata):
+        """Display string of a CallMetadata (protocol.py:1277-1300), the reference's."""
+        return _overlay.bind(self, self._reference(), "format_call_metadata")(metadata)

@@ -1,9 +1,13 @@
 """Signal processing (demodulation).  Mirrors /root/reference/tetraear/signal/__init__.py:11-28.
 
-The scanner's signal detector (TetraSignalDetector) runs on the GPU (tetraear.signal.scanner).
-BladeRF capture and the frequency sweep (FrequencyScanner) are hardware/UI components outside this
-hot-path build; asking for them raises ImportError naming the reference module that provides them.
+SignalProcessor and the scanner's signal detector (TetraSignalDetector) are this build's, on the
+GPU.  BladeRF capture (``capture``) and the frequency sweep (FrequencyScanner) are the reference's:
+they resolve when the reference's package root is on sys.path after this one (tetraear/_overlay.py)
+and raise ImportError naming the missing reference otherwise.
 """
+from tetraear import _overlay
+
+__path__ = _overlay.extend(__path__, __name__)
 
 
 def __getattr__(name):
@@ -13,10 +17,17 @@ def __getattr__(name):
     if name == "TetraSignalDetector":
         from tetraear.signal.scanner import TetraSignalDetector
         return TetraSignalDetector
-    if name in ("BladeRFCapture", "list_bladerf_devices", "FrequencyScanner"):
-        raise ImportError(f"{name} is not part of the MI355X hot-path build; use the reference's "
-                          f"tetraear.signal.{'capture' if 'BladeRF' in name or 'bladerf' in name else 'scanner'}")
+    if name == "FrequencyScanner":
+        from tetraear.signal.scanner import FrequencyScanner
+        return FrequencyScanner
+    if name in ("BladeRFCapture", "list_bladerf_devices"):
+        if not _overlay.active():
+            raise _overlay.ReferenceUnavailable(
+                f"{name} is the reference's (tetraear/signal/capture.py): put the reference's package root on "
+                f"sys.path after this build's, or set TETRAEAR_REFERENCE_ROOT")
+        from tetraear.signal import capture
+        return getattr(capture, name)
     raise AttributeError(f"module {__name__!r} has no attribute {name!r}")
 
 
-__all__ = ["SignalProcessor", "TetraSignalDetector"]
+__all__ = ["SignalProcessor", "BladeRFCapture", "list_bladerf_devices", "TetraSignalDetector", "FrequencyScanner"]

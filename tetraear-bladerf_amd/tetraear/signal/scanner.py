@@ -12,13 +12,16 @@ turns the counts into the reference's decisions.
 ``scan_wideband`` feeds the detector from the C3 channeliser: each of the 800 carriers of a 20 MSps
 capture, as 72 kHz samples, is a candidate channel of one batch.
 
-The hardware sweep (``FrequencyScanner``: tuning the BladeRF, dwell, retries) stays out of scope.
+The hardware sweep (``FrequencyScanner``: tuning the BladeRF, dwell, retries; scanner.py:292-554) is
+the reference's: with its package root on sys.path after this build's, ``FrequencyScanner`` here is
+the reference's class from its own file, its detector swapped for this module's GPU
+``TetraSignalDetector`` (tetraear/_overlay.py).
 """
 import logging
 
 import numpy as np
 
-from tetraear import _hip
+from tetraear import _hip, _overlay
 
 logger = logging.getLogger(__name__)
 
@@ -207,3 +210,11 @@ def scan_wideband(x, fs=20e6, validate=False):
     from tetraear.signal.wideband import WidebandReceiver
     y = WidebandReceiver(fs).channelize(x)
     return TetraSignalDetector(sample_rate=72000.0).analyze_batch(y, validate=validate), y
+
+
+def __getattr__(name):
+    """``FrequencyScanner`` (scanner.py:292): the reference's sweep over this module's detector."""
+    if name == "FrequencyScanner":
+        mod = _overlay.reference_module("signal/scanner", patch={"TetraSignalDetector": TetraSignalDetector})
+        return mod.FrequencyScanner
+    raise AttributeError(f"module {__name__!r} has no attribute {name!r}")
