@@ -69,6 +69,10 @@ int tetra_profile(tetra_ctx *ctx, int enable);
 int tetra_read_floor(tetra_ctx *ctx, const void *x, size_t rows, size_t row_bytes, size_t lds_bytes);
 int tetra_profile_read(tetra_ctx *ctx, char *names, size_t names_len, double *ms, int64_t *count,
                        int max_stages, int *n_stages);
+/* Diagnostic: launch the one-wave marker kernel k_region_mark(tag) on the context stream.  bench.py
+ * brackets its timed steps with tag 1 / tag 2, so rocprofv3 traces and counter passes of the bench
+ * command can select the timed launches by dispatch order (tools/pmc_summary.py). */
+int tetra_mark(tetra_ctx *ctx, int tag);
 
 /* =====================================================================================
  * Compat demod -- bit-compatible with SignalProcessor (processor.py:221-273)

@@ -281,3 +281,21 @@ extern "C" int tetra_read_floor(tetra_ctx *ctx, const void *x, size_t rows, size
     HIP_TRY(ctx, hipGetLastError());
     return TETRA_OK;
 }
+
+// ------------------------------------------------------------------ profile region marker (diagnostic)
+// One 64-lane wave that stores `tag` into the diagnostics slot (a vector store by lane 0).  bench.py
+// launches it on the context stream right before and right after its timed steps, so a rocprofv3
+// kernel trace or counter collection of the bench command can pick out the timed launches by
+// dispatch order (tools/pmc_summary.py: the launches between the two k_region_mark dispatches).
+__global__ __launch_bounds__(64) void k_region_mark(int tag, int *out) {
+    if (threadIdx.x == 0) out[0] = tag;
+}
+
+extern "C" int tetra_mark(tetra_ctx *ctx, int tag) {
+    if (!ctx) return TETRA_E_INVALID;
+    int *o = (int *)ws(ctx, S_W13, 256);
+    if (!o) return TETRA_E_NOMEM;
+    hipLaunchKernelGGL(k_region_mark, dim3(1), dim3(64), 0, ctx->stream, tag, o);
+    HIP_TRY(ctx, hipGetLastError());
+    return TETRA_OK;
+}

@@ -118,6 +118,7 @@ def _bind(L):
         "tetra_etsi_encode_blocks": (_i32, [_vp, _vp, _sz, _i32, _vp, _vp]),
         "tetra_wb_lengths": (_i32, [ctypes.POINTER(WbPlan), _sz, _vp, _vp]),
         "tetra_read_floor": (_i32, [_vp, _vp, _sz, _sz, _sz]),
+        "tetra_mark": (_i32, [_vp, _i32]),
         "tetra_resample": (_i32, [_vp, _vp, _i32, _sz, _sz, _sz, _vp]),
         "tetra_waterfall": (_i32, [_vp, _vp, _i32, _sz, _sz, _sz, _sz, _sz, _vp]),
         "tetra_afc_gate": (_i32, [_vp, _vp, _i32, _sz, _sz, ctypes.c_double, _vp, _vp, _vp, _vp]),

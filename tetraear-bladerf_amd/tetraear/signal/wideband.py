@@ -180,7 +180,7 @@ class BenchStep:
     """bench.py --chain wideband (C3): one step = the capture's waterfall rows (2048-pt Hann, hop
     2048), channelise the device-resident 20 MSps capture, timing + decision on every (carrier,
     chunk), lower MAC (sync, Viterbi, CRC) on all of them."""
-    dtype = "f32 (DSP, rocFFT), int8/int32 (Viterbi)"
+    dtype = "f32 (DSP), int8/int32 (Viterbi)"
 
     def __init__(self, c, Nw, seed, device, snr_db=30.0, fs=FS_WB, M=M_WB):
         import torch
