@@ -88,7 +88,8 @@ typedef struct tetra_compat_plan {
     int32_t ntaps;        /* butter(4) -> 5 */
     int32_t sps;          /* int(rate/18000) (processor.py:183) */
     int32_t phase_step;   /* max(1, sps//8) (processor.py:194) */
-    int32_t reserved[2];
+    int32_t flags;        /* TETRA_COMPAT_*: decimator form (0: automatic) */
+    int32_t reserved;
     double fs_dec;        /* sample rate after decimation: time base of frequency_shift */
     float sos_f32[24];    /* cheby1(8, 0.05, 0.8/q) SOS [4][6] as complex64 real parts */
     float zi_f32[8];      /* sosfilt_zi in complex64 */
@@ -98,6 +99,16 @@ typedef struct tetra_compat_plan {
     double lzi[8];        /* lfilter_zi(b, a) */
     double thr[4];        /* -5*pi/8, -3*pi/8, 3*pi/8, 5*pi/8 as Python evaluates them */
 } tetra_compat_plan;
+
+/* tetra_compat_plan.flags.  The decimator of tetra_demod_compat runs either sequentially in time
+ * (scipy's exact operation order: bit-identical to the reference) or time-blocked (tiles of 256
+ * samples recursed in parallel, their start states composed in float64: within the cheby1 filter's
+ * fp32 noise of scipy -- <= 3.4e-6 on .symbols over the reference fixtures at q <= 10, no decision
+ * changed -- and 10-20x lower latency for a single channel).  Automatic (0): time-blocked for
+ * C <= 64 channels, decimation q <= 16 and N + 54 <= 262144 samples, else sequential.  The component
+ * entry point tetra_decimate is always sequential. */
+#define TETRA_COMPAT_SEQUENTIAL 1   /* force the scipy-exact sequential decimator */
+#define TETRA_COMPAT_BLOCKED    2   /* force the time-blocked decimator (TETRA_E_INVALID outside its limits) */
 
 /* Fused process() over a batch of C equal-length chunks.
  *   iq        [C][N] complex, format iq_fmt (TETRA_CF32 for SC16-derived capture data)
@@ -113,6 +124,10 @@ int tetra_demod_compat(tetra_ctx *ctx, const tetra_compat_plan *plan, const void
                        void *soft, uint8_t *hard, int32_t *nsym, size_t smax, int32_t *soft_f32);
 /* Number of soft symbols process() yields for N input samples under `plan`. */
 int64_t tetra_compat_symbols(const tetra_compat_plan *plan, size_t N);
+/* Host-only: the time-blocked decimator's table Phi^(2^r), r = 0..9, row-major 8 x 8 float64 each
+ * (Phi = A^256, A the 4-section cascade's one-sample zero-input transition) from the plan's
+ * complex64 (f64 = 0) or complex128 (f64 = 1) SOS; table holds 640 doubles. */
+int tetra_compat_blocked_table(const tetra_compat_plan *plan, int f64, double *table);
 
 /* Component entry points, one per SignalProcessor method (each over C rows of length N). */
 /* scipy.signal.decimate(x, q) as called at processor.py:254: out [C][ceil(N/q)] in iq_fmt. */

@@ -129,6 +129,113 @@ def filtfilt(b, a, x):
     return y[edge:-edge]
 
 
+# ----------------------------------------------------------------------------- time-blocked decimate
+# The product's latency-mode decimator (tetraear-bladerf_amd/csrc/compat_demod.hip, k_sosb_*), restated
+# operation for operation, so the GPU can be checked bit for bit; its distance from the reference's
+# sequential decimate is checked against the reference's own fixtures (tests/test_compat_blocked.py).
+# Not a reference function: the reference only has the sequential scipy.signal.decimate
+# (/root/reference/tetraear/signal/processor.py:254).
+SB_B, SB_MAXT, SB_NPOW, SB_MAXC, SB_MAXQ = 256, 1024, 10, 64, 16
+
+
+def blocked_fits(C, N, q):
+    """The shapes tetra_demod_compat decimates time-blocked by default (compat_demod.hip: blocked_fits)."""
+    return 1 <= C <= SB_MAXC and 2 <= q <= SB_MAXQ and N > 27 and -(-(N + 54) // SB_B) <= SB_MAXT
+
+
+def blocked_table(coef):
+    """Phi^(2^r), r < SB_NPOW (Phi = A^SB_B, A the cascade's one-sample zero-input transition in scipy's
+    _sosfilt order), as float64 [SB_NPOW, 8, 8]; every product summed in k order, no FMA -- the
+    host loops of compat_demod.hip: blocked_table."""
+    c = [float(v) for v in np.asarray(coef, np.float64).ravel()]
+    A = [[0.0] * 8 for _ in range(8)]
+    for k in range(8):
+        z = [0.0] * 8
+        z[k] = 1.0
+        zn = [0.0] * 8
+        u = 0.0
+        for s in range(4):
+            b0, b1, b2, a1, a2 = c[6 * s], c[6 * s + 1], c[6 * s + 2], c[6 * s + 4], c[6 * s + 5]
+            xn = b0 * u + z[2 * s]
+            zn[2 * s] = (b1 * u - a1 * xn) + z[2 * s + 1]
+            zn[2 * s + 1] = b2 * u - a2 * xn
+            u = xn
+        for i in range(8):
+            A[i][k] = zn[i]
+
+    def square(P):
+        out = [[0.0] * 8 for _ in range(8)]
+        for i in range(8):
+            for j in range(8):
+                acc = 0.0
+                for k in range(8):
+                    acc = acc + P[i][k] * P[k][j]
+                out[i][j] = acc
+        return out
+
+    b = 1
+    while b < SB_B:
+        A = square(A)
+        b <<= 1
+    tab = [A]
+    for _ in range(1, SB_NPOW):
+        tab.append(square(tab[-1]))
+    return np.array(tab, np.float64)
+
+
+def _blocked_pass(coef, zi, c, real_t, tab):
+    """sosfilt of one real sequence c from state zi * c[0], time-blocked: every tile of SB_B samples
+    from zero state (end states e_k), the start states by the float64 Hillis-Steele scan
+    w_k += Phi^d w_{k-d}, every tile again from its start state."""
+    L = len(c)
+    Tn = -(-L // SB_B)
+    fn = lib().orc_sosfilt_f32 if real_t is np.float32 else lib().orc_sosfilt_f64
+    s0 = np.ascontiguousarray(zi * c[0], dtype=real_t)
+    w = np.zeros((Tn, 8), np.float64)
+    w[0] = s0.astype(np.float64)
+    for k in range(Tn - 1):
+        z = np.zeros(8, real_t)
+        fn(coef, 4, z, np.array(c[k * SB_B:(k + 1) * SB_B], real_t), SB_B)
+        w[k + 1] = z.astype(np.float64)
+    r = 0
+    while (1 << r) < Tn:
+        d = 1 << r
+        u = w[:-d].copy()
+        acc = w[d:].copy()
+        for j in range(8):
+            acc = acc + tab[r][None, :, j] * u[:, j:j + 1]
+        w[d:] = acc
+        r += 1
+    out = np.empty(L, real_t)
+    for k in range(Tn):
+        t = np.array(c[k * SB_B:(k + 1) * SB_B], real_t)
+        fn(coef, 4, w[k].astype(real_t), t, len(t))
+        out[k * SB_B:k * SB_B + len(t)] = t
+    return out
+
+
+def decimate_blocked(x, q):
+    """decimate(x, q) as the product's time-blocked decimator computes it (see above)."""
+    x = np.asarray(x)
+    dtype = x.dtype
+    real_t = np.float32 if dtype in (np.float32, np.complex64) else np.float64
+    sos = np.asarray(_ss.cheby1(8, 0.05, 0.8 / q, output="sos"), dtype=dtype)
+    zr = np.ascontiguousarray(_ss.sosfilt_zi(sos).real, dtype=real_t).ravel()
+    coef = np.ascontiguousarray(sos.real, dtype=real_t).ravel()
+    tab = blocked_table(coef)
+    edge = 27
+    if x.shape[0] <= edge:
+        raise ValueError(f"The length of the input vector x must be greater than padlen, which is {edge}.")
+    ext = _odd_ext(x, edge)
+    outs = []
+    for comp in _components(ext):
+        f = _blocked_pass(coef, zr, np.ascontiguousarray(comp, real_t), real_t, tab)
+        b = _blocked_pass(coef, zr, np.ascontiguousarray(f[::-1]), real_t, tab)
+        outs.append(b[::-1])
+    y = (outs[0] + 1j * outs[1]).astype(dtype) if np.iscomplexobj(ext) else outs[0].astype(dtype)
+    return y[edge:-edge][::q]
+
+
 # ----------------------------------------------------------------------------- demod
 
 def _pairwise_sum(v):
@@ -139,11 +246,14 @@ def _pairwise_sum(v):
 class SignalProcessor:
     """Restatement of processor.py:18-273."""
 
-    def __init__(self, sample_rate=2.4e6):
+    def __init__(self, sample_rate=2.4e6, decimator="sequential"):
         self.sample_rate = sample_rate
         self.symbol_rate = 18000
         self.samples_per_symbol = int(sample_rate / self.symbol_rate)
         self.symbols = None
+        # "sequential": the reference's decimate; "blocked": the product's latency-mode decimator;
+        # "auto": blocked where tetra_demod_compat picks it for one channel (blocked_fits)
+        self.decimator = decimator
 
     def filter_signal(self, samples, bandwidth=25000, sample_rate=None):
         if len(samples) == 0:
@@ -213,7 +323,9 @@ class SignalProcessor:
             q = int(rate / 240000)
             if q > 1:
                 try:
-                    samples = decimate(samples, q)
+                    blk = self.decimator == "blocked" or (self.decimator == "auto" and
+                                                          blocked_fits(1, len(samples), q))
+                    samples = decimate_blocked(samples, q) if blk else decimate(samples, q)
                     rate = rate / q
                 except Exception:
                     pass

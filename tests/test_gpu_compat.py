@@ -299,3 +299,58 @@ def test_lmac_packed_equals_global_rows(hip, g2):
         k = int(n1[i])
         assert np.array_equal(r1[i, :k], r2[i, :k])
         assert np.array_equal(f1[i, :k], f2[i, :k]) and np.array_equal(b1[i, :k], b2[i, :k])
+
+
+def test_blocked_decimator_equals_its_oracle(hip, g1):
+    """process() on one chunk takes the time-blocked decimator (latency mode, auto for C <= 64,
+    q <= 16).  Every G1 case it serves equals the oracle's restatement of that form
+    (oracle/compat.py: decimate_blocked): hard symbols exactly, .symbols exactly without a mixer and
+    within 1e-12 with one (device sin/cos ulps); the reference itself within 1e-5
+    (test_process_matches_golden, tests/test_compat_blocked.py).  decimator="sequential" keeps the
+    scipy-exact form on the same call."""
+    from tetraear.signal import SignalProcessor
+    z, meta = g1
+    served = 0
+    for i, m in enumerate(meta):
+        x = iq_to_c64(z[f"c{i}_iq"])
+        if not m["dec_ok"] or m["q"] < 2 or not O.blocked_fits(1, len(x), m["q"]):
+            continue
+        p = SignalProcessor(m["fs"])
+        hard = p.process(x, m["freq_offset"])
+        o = O.SignalProcessor(m["fs"], decimator="blocked")
+        want = o.process(x, m["freq_offset"])
+        assert np.array_equal(hard, want), (i, m)
+        tol = 0.0 if m["freq_offset"] == 0 else 1e-12
+        assert np.max(np.abs(p.symbols - o.symbols)) <= tol, (i, m)
+        ps = SignalProcessor(m["fs"], decimator="sequential")
+        hs = ps.process(x, m["freq_offset"])
+        want_sym = z[f"c{i}_symbols"]
+        assert np.max(np.abs(ps.symbols - want_sym)) <= (0.0 if m["freq_offset"] == 0 else SOFT_TOL), (i, m)
+        _hard_equal(hs, z[f"c{i}_hard"], want_sym)
+        served += 1
+    assert served >= 20
+
+
+@pytest.mark.parametrize("dtype", [np.complex64, np.complex128])
+def test_blocked_batch_and_limits(hip, dtype):
+    """A 64-channel batch decimates time-blocked channel by channel as the oracle does (cf32 and
+    cf64); 65 channels take the sequential form (auto) and equal the sequential oracle; forcing the
+    blocked form outside its limits (q = 83) is refused."""
+    from tetraear.signal import SignalProcessor
+    from tetraear import _hip
+    rng = np.random.default_rng(11)
+    N = 20000
+    x = (0.3 * (rng.standard_normal((65, N)) + 1j * rng.standard_normal((65, N)))).astype(dtype)
+    fo = (np.arange(65) % 5 - 2) * 1171.875
+    p = SignalProcessor(2.4e6)
+    hard, soft, ns = p.process_batch(x[:64], fo[:64])
+    h65, s65, n65 = p.process_batch(x, fo)
+    for c in (0, 17, 63):
+        o = O.SignalProcessor(2.4e6, decimator="blocked")
+        want = o.process(x[c], fo[c])
+        assert ns[c] == len(o.symbols) and np.array_equal(hard[c, :ns[c] - 1], want), c
+        assert np.max(np.abs(soft[c, :ns[c]] - o.symbols)) <= 1e-12, c
+        seq = O.SignalProcessor(2.4e6).process(x[c], fo[c])
+        assert np.array_equal(h65[c, :n65[c] - 1], seq), c
+    with pytest.raises(_hip.TetraHipError):
+        SignalProcessor(20e6, decimator="blocked").process(x[0].astype(dtype))

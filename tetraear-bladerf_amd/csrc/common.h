@@ -29,6 +29,7 @@ enum Slot {
     S_W13,                                                 // diagnostics (tetra_read_floor sink)
     S_W14,                                                 // ETSI: scrambler inits the cell table holds
     S_W15,                                                 // ETSI generic-rate tap tables (etsi_rate.hip)
+    S_W16,                                                 // compat time-blocked decimator: tile states, Phi table
     S_COUNT
 };
 
@@ -58,6 +59,9 @@ struct tetra_ctx {
     void *fft = nullptr;               // rocFFT plan cache (wideband.hip), freed by fft_free
     void (*fft_free)(void *) = nullptr;
     bool wf_tables_ready = false;      // waterfall tables uploaded to slot S_W11
+    std::vector<double> sosb_tab;      // compat time-blocked decimator: Phi^(2^r) table as last uploaded
+    int sosb_key = -1;                 // ... for this (q, precision)
+    const void *sosb_dev = nullptr;    // ... to this address (slot S_W16)
 };
 
 extern thread_local std::string g_tetra_err;

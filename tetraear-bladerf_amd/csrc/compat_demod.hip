@@ -537,6 +537,214 @@ __global__ __launch_bounds__(256) void k_sos_bwd_bank(const float *__restrict__ 
     for (; tau < L + 3; ++tau) tick(tau, tau < L ? sp[L - 1 - tau] : 0.f);
 }
 
+// ------------------------------------------------------------------ time-blocked decimator (latency mode)
+// sosfiltfilt for a few channels, parallel in time.  A stream's
+// odd extension ext[0, L) is cut into tiles of SB_B samples; one quad of lanes runs the 4-section
+// cascade over one tile (the skewed section pipeline of k_sos_fwd: section s works on sample tau - s
+// at tick tau), so every tile of every stream recurses at once.  Per pass (forward, then backward on
+// the reversed forward output):
+//   1. k_sosb_tile<.., false>: each tile from zero state -> its end state e_k (8 numbers: the two
+//      DF-II-T states of 4 sections), T arithmetic;
+//   2. k_sosb_scan: the true start states s_k of every tile in float64, s_{k+1} = Phi s_k + e_k with
+//      Phi = A^SB_B (A: the cascade's one-sample zero-input transition), s_0 = sosfilt_zi * ext[0] as
+//      the sequential pass sets it -- as an inclusive Hillis-Steele scan over the tiles with the
+//      host's table Phi^(2^r) (compat_blocked_table);
+//   3. k_sosb_tile<.., true>: each tile again from (T) s_k, its outputs to the scratch row (forward)
+//      or decimated to `out` (backward).
+// Tile 0 starts from the sequential pass's exact state, so its outputs are scipy's bit for bit;
+// later tiles start from the float64-composed state instead of the state a sequential fp32
+// recursion would have accumulated, so outputs differ from scipy's by the filter's fp32 noise
+// (measured on the 31 reference fixtures: <= 3.4e-6 on .symbols for q <= 10, no hard decision
+// changed; oracle/compat.py: decimate_blocked restates every operation and the GPU equals it bit
+// for bit).  Used by tetra_demod_compat for C <= SB_MAXC channels and q <= SB_MAXQ (at q = 83 the
+// cheby1 band is so narrow the noise reaches 5.7e-5), and never by the component entry point
+// tetra_decimate, which stays scipy-exact.
+constexpr int SB_B = 256;        // samples per tile
+constexpr int SB_MAXT = 1024;    // tiles per stream (one scan workgroup): L <= 262144
+constexpr int SB_NPOW = 10;      // Phi^(2^r), r < SB_NPOW: covers SB_MAXT tiles
+constexpr int SB_MAXC = 64;      // channels up to which tetra_demod_compat takes this path
+constexpr int SB_MAXQ = 16;      // decimation factors up to which it does
+template <typename T> struct SbCfg { static constexpr int ST = sizeof(T) == 4 ? 64 : 32; };   // stream-tiles / workgroup
+
+struct SbGeo {
+    int C, Tn, pad, q;
+    long N, L, Lp;
+};
+
+// stream-tile g = (ch * Tn + tile) * 2 + comp
+template <typename T, bool FWD, bool FINAL>
+__global__ __launch_bounds__(4 * SbCfg<T>::ST) void k_sosb_tile(const T *__restrict__ x, T *__restrict__ scr, SbGeo G,
+                                                                const T *__restrict__ sos,
+                                                                const double *__restrict__ states,
+                                                                double *__restrict__ ends, T *__restrict__ out, Lay lo) {
+    constexpr int ST = SbCfg<T>::ST;
+    __shared__ T buf[ST][SB_B + 1];
+    const int tid = threadIdx.x, sec = tid & 3, stl = tid >> 2;
+    const long ntiles = (long)2 * G.C * G.Tn;
+    // cooperative load of the workgroup's tiles: ext (forward) or the reversed scratch row (backward)
+    for (int i = tid; i < ST * SB_B; i += 4 * ST) {
+        const int r = i / SB_B, j = i % SB_B;
+        const long g = (long)blockIdx.x * ST + r;
+        T v = 0;
+        if (g < ntiles) {
+            const int comp = (int)(g & 1), tile = (int)((g >> 1) % G.Tn), ch = (int)((g >> 1) / G.Tn);
+            const long e = (long)tile * SB_B + j;
+            if (e < G.L) {
+                if (FWD) {   // scipy _arraytools.odd_ext, in T
+                    const T *xr = x + (size_t)ch * G.N * 2 + comp;
+                    if (e < G.pad) v = (T)2 * xr[0] - xr[2 * (G.pad - e)];
+                    else if (e < G.pad + G.N) v = xr[2 * (e - G.pad)];
+                    else v = (T)2 * xr[2 * (G.N - 1)] - xr[2 * (G.N - 2 - (e - G.pad - G.N))];
+                } else {
+                    v = scr[(size_t)(2 * ch + comp) * G.Lp + (G.L - 1 - e)];
+                }
+            }
+            buf[r][j] = v;
+        }
+    }
+    __syncthreads();
+    const long g = (long)blockIdx.x * ST + stl;
+    const bool own = g < ntiles;
+    const int tile = own ? (int)((g >> 1) % G.Tn) : 0;
+    const long len = own ? min((long)SB_B, G.L - (long)tile * SB_B) : 0;
+    Biquad<T> bq{sos[6 * sec], sos[6 * sec + 1], sos[6 * sec + 2], sos[6 * sec + 4], sos[6 * sec + 5], (T)0, (T)0};
+    if (FINAL && own) {
+        bq.z0 = (T)states[g * 8 + 2 * sec];
+        bq.z1 = (T)states[g * 8 + 2 * sec + 1];
+    }
+    T y = 0;
+    for (int tau0 = 0; tau0 < SB_B + 3; tau0 += 16) {
+        T in[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) in[u] = buf[stl][min(tau0 + u, SB_B - 1)];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const T left = from_left(y);
+            const int j = tau0 + u - sec;
+            if (j >= 0 && j < len) {
+                y = bq.step(sec == 0 ? in[u] : left);
+                // input j was read at the top of this batch or an earlier one: the slot is free
+                if (FINAL && sec == 3) buf[stl][j] = y;
+            }
+        }
+    }
+    if (!FINAL) {
+        if (own) {
+            ends[g * 8 + 2 * sec] = (double)bq.z0;
+            ends[g * 8 + 2 * sec + 1] = (double)bq.z1;
+        }
+        return;
+    }
+    __syncthreads();
+    for (int i = tid; i < ST * SB_B; i += 4 * ST) {
+        const int r = i / SB_B, j = i % SB_B;
+        const long gg = (long)blockIdx.x * ST + r;
+        if (gg >= ntiles) continue;
+        const int comp = (int)(gg & 1), tl = (int)((gg >> 1) % G.Tn), ch = (int)((gg >> 1) / G.Tn);
+        const long e = (long)tl * SB_B + j;
+        if (e >= G.L) continue;
+        if (FWD) {
+            scr[(size_t)(2 * ch + comp) * G.Lp + e] = buf[r][j];
+        } else {   // ext index L-1-e, sample t = ext - pad; decimate keeps t % q == 0
+            const long t = G.L - 1 - e - G.pad;
+            if (t >= 0 && t < G.N && t % G.q == 0) out[lo.off(ch, t / G.q) + comp] = buf[r][j];
+        }
+    }
+}
+
+// Start states of every tile of one stream (workgroup = stream 2 ch + comp, thread = tile):
+// w_0 = sosfilt_zi * ext[0] (T, as the sequential pass computes it), w_k = e_{k-1}; then for
+// d = 1, 2, 4, ..: w_k += Phi^d w_{k-d} (k >= d), each product summed in j order without FMA
+// (oracle/compat.py: _blocked_scan restates it).
+template <typename T, bool FWD>
+__global__ __launch_bounds__(1024) void k_sosb_scan(const T *__restrict__ x, const T *__restrict__ scr, SbGeo G,
+                                                    const T *__restrict__ zi, const double *__restrict__ phi,
+                                                    const double *__restrict__ ends, double *__restrict__ states) {
+    __shared__ double w[SB_MAXT][8];
+    const int k = threadIdx.x, s = blockIdx.x, ch = s >> 1, comp = s & 1;
+    const bool on = k < G.Tn;
+    double v[8];
+    if (on) {
+        if (k == 0) {
+            T x0;
+            if (FWD) {
+                const T *xr = x + (size_t)ch * G.N * 2 + comp;
+                x0 = (T)2 * xr[0] - xr[2 * G.pad];
+            } else {
+                x0 = scr[(size_t)s * G.Lp + G.L - 1];
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = (double)(zi[i] * x0);
+        } else {
+            const double *e = ends + ((size_t)(ch * G.Tn + k - 1) * 2 + comp) * 8;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = e[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[k][i] = v[i];
+    }
+    for (int r = 0; (1 << r) < G.Tn; ++r) {
+        const int d = 1 << r;
+        __syncthreads();
+        double u[8];
+        const bool upd = on && k >= d;
+        if (upd) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) u[i] = w[k - d][i];
+        }
+        __syncthreads();
+        if (upd) {
+            const double *P = phi + (size_t)r * 64;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                double acc = v[i];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc = acc + P[i * 8 + j] * u[j];
+                v[i] = acc;
+                w[k][i] = acc;
+            }
+        }
+    }
+    if (on) {
+        double *o = states + ((size_t)(ch * G.Tn + k) * 2 + comp) * 8;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = v[i];
+    }
+}
+
+// A (the cascade's one-sample zero-input transition, from the coefficients the kernels use, in
+// double) and the table Phi^(2^r) = A^(SB_B 2^r), r < SB_NPOW, row-major 8 x 8 each; every product
+// summed in k order without FMA (the oracle computes the same table the same way).
+void blocked_table(const double *coef /*[24] sos rows*/, double *tab /*[SB_NPOW * 64]*/) {
+    double A[64];
+    for (int k = 0; k < 8; ++k) {
+        double z[8] = {0}, zn[8];
+        z[k] = 1.0;
+        double u = 0.0;
+        for (int s = 0; s < NSEC; ++s) {
+            const double *c = coef + 6 * s;
+            const double xn = c[0] * u + z[2 * s];
+            zn[2 * s] = (c[1] * u - c[4] * xn) + z[2 * s + 1];
+            zn[2 * s + 1] = c[2] * u - c[5] * xn;
+            u = xn;
+        }
+        for (int i = 0; i < 8; ++i) A[i * 8 + k] = zn[i];
+    }
+    auto square = [](const double *P, double *out) {
+        double t[64];
+        for (int i = 0; i < 8; ++i)
+            for (int j = 0; j < 8; ++j) {
+                double acc = 0.0;
+                for (int k = 0; k < 8; ++k) acc = acc + P[i * 8 + k] * P[k * 8 + j];
+                t[i * 8 + j] = acc;
+            }
+        for (int i = 0; i < 64; ++i) out[i] = t[i];
+    };
+    for (int b = 1; b < SB_B; b <<= 1) square(A, A);   // A^SB_B (SB_B a power of two)
+    for (int i = 0; i < 64; ++i) tab[i] = A[i];
+    for (int r = 1; r < SB_NPOW; ++r) square(tab + (r - 1) * 64, tab + r * 64);
+}
+
 // ------------------------------------------------------------------ mixer + filtfilt (lfilter)
 // Value of component `comp` of (possibly frequency-shifted) sample n, in double.
 __device__ __forceinline__ double mix_pair(double xr, double xi, long n, int comp, bool mix, double c, double fs) {
@@ -1026,6 +1234,65 @@ int run_decimate(tetra_ctx *ctx, const tetra_compat_plan *P, const T *x, Lay lx,
     return TETRA_OK;
 }
 
+// The time-blocked decimator (k_sosb_*): same contract as run_decimate (complex rows [C][N] in,
+// decimate's output to `out` in layout lo), with the tile geometry checked by blocked_fits.
+bool blocked_fits(int C, long N, int q) {
+    return C >= 1 && C <= SB_MAXC && q >= 2 && q <= SB_MAXQ && N > 27 && (N + 54 + SB_B - 1) / SB_B <= SB_MAXT;
+}
+
+template <typename T>
+int run_decimate_blocked(tetra_ctx *ctx, const tetra_compat_plan *P, const T *x, int C, long N, T *out, Lay lo) {
+    const int pad = 27;
+    const long L = N + 2 * pad;
+    const long Lp = (L + 3) & ~3L;
+    const int Tn = (int)ceil_div(L, SB_B);
+    const size_t ntile = (size_t)2 * C * Tn;
+    T *scr = (T *)ws(ctx, S_W0, (size_t)2 * C * Lp * sizeof(T));
+    T *coef = (T *)ws(ctx, S_W7, 32 * sizeof(T));
+    double *sb = (double *)ws(ctx, S_W16, (2 * ntile * 8 + SB_NPOW * 64) * sizeof(double));
+    if (!scr || !coef || !sb) return TETRA_E_NOMEM;
+    double *ends = sb, *states = sb + ntile * 8, *phi = sb + 2 * ntile * 8;
+    T hc[32];
+    double dc[24];
+    for (int i = 0; i < 24; ++i) {
+        hc[i] = std::is_same<T, float>::value ? (T)P->sos_f32[i] : (T)P->sos_f64[i];
+        dc[i] = (double)hc[i];
+    }
+    for (int i = 0; i < 8; ++i) hc[24 + i] = std::is_same<T, float>::value ? (T)P->zi_f32[i] : (T)P->zi_f64[i];
+    const int key = P->q * 2 + (std::is_same<T, float>::value ? 0 : 1);
+    if (ctx->sosb_key != key || ctx->sosb_dev != (const void *)phi) {
+        ctx->sosb_tab.resize(SB_NPOW * 64);
+        blocked_table(dc, ctx->sosb_tab.data());
+        HIP_TRY(ctx, hipMemcpyAsync(phi, ctx->sosb_tab.data(), SB_NPOW * 64 * sizeof(double), hipMemcpyHostToDevice,
+                                    ctx->stream));
+        ctx->sosb_key = key;
+        ctx->sosb_dev = phi;
+    }
+    HIP_TRY(ctx, hipMemcpyAsync(coef, hc, sizeof hc, hipMemcpyHostToDevice, ctx->stream));
+    const SbGeo G{C, Tn, pad, P->q, N, L, Lp};
+    constexpr int ST = SbCfg<T>::ST;
+    const dim3 gt((unsigned)ceil_div((long)ntile, ST)), bt(4 * ST);
+    const dim3 gs((unsigned)(2 * C)), bs((unsigned)std::min(SB_MAXT, (int)ceil_div(Tn, 64) * 64));
+    {
+        PROF(ctx, "compat_sosb_fwd");
+        hipLaunchKernelGGL((k_sosb_tile<T, true, false>), gt, bt, 0, ctx->stream, x, scr, G, coef, nullptr, ends,
+                           (T *)nullptr, lo);
+        hipLaunchKernelGGL((k_sosb_scan<T, true>), gs, bs, 0, ctx->stream, x, scr, G, coef + 24, phi, ends, states);
+        hipLaunchKernelGGL((k_sosb_tile<T, true, true>), gt, bt, 0, ctx->stream, x, scr, G, coef, states, nullptr,
+                           (T *)nullptr, lo);
+    }
+    {
+        PROF(ctx, "compat_sosb_bwd");
+        hipLaunchKernelGGL((k_sosb_tile<T, false, false>), gt, bt, 0, ctx->stream, x, scr, G, coef, nullptr, ends,
+                           (T *)nullptr, lo);
+        hipLaunchKernelGGL((k_sosb_scan<T, false>), gs, bs, 0, ctx->stream, x, scr, G, coef + 24, phi, ends, states);
+        hipLaunchKernelGGL((k_sosb_tile<T, false, true>), gt, bt, 0, ctx->stream, x, scr, G, coef, states, nullptr, out,
+                           lo);
+    }
+    HIP_TRY(ctx, hipGetLastError());
+    return TETRA_OK;
+}
+
 template <typename TIn>
 int run_filtfilt(tetra_ctx *ctx, const tetra_compat_plan *P, const TIn *x, Lay lx, int C, long M,
                  const double *mixc, const uint8_t *mixon, double *out, Lay lo) {
@@ -1078,6 +1345,14 @@ int check_plan(tetra_ctx *ctx, const tetra_compat_plan *P) {
 }  // namespace
 
 extern "C" {
+
+int tetra_compat_blocked_table(const tetra_compat_plan *P, int f64, double *table) {
+    if (!P || !table) return TETRA_E_INVALID;
+    double dc[24];
+    for (int i = 0; i < 24; ++i) dc[i] = f64 ? P->sos_f64[i] : (double)P->sos_f32[i];
+    blocked_table(dc, table);
+    return TETRA_OK;
+}
 
 int64_t tetra_compat_symbols(const tetra_compat_plan *P, size_t N) {
     if (!P || N == 0) return 0;
@@ -1224,10 +1499,23 @@ int tetra_demod_compat(tetra_ctx *ctx, const tetra_compat_plan *P, const void *i
     if (dec) {
         void *db = ws(ctx, S_W1, grouped_elems((int)C, M) * es);
         if (!db) return TETRA_E_NOMEM;
-        rc = fmt == TETRA_CF64 ? run_decimate<double>(ctx, P, (const double *)x, row_major(N), (int)C, (long)N,
-                                                      (double *)db, grouped(M))
-                               : run_decimate<float>(ctx, P, (const float *)x, row_major(N), (int)C, (long)N,
-                                                     (float *)db, grouped(M));
+        // latency mode: a few channels decimate time-blocked (parallel in time, within the filter's
+        // fp32 noise of scipy); TETRA_COMPAT_SEQUENTIAL keeps the scipy-exact sequential passes
+        const bool blocked = (P->flags & TETRA_COMPAT_BLOCKED) ||
+                             (!(P->flags & TETRA_COMPAT_SEQUENTIAL) && blocked_fits((int)C, (long)N, P->q));
+        if (blocked && !blocked_fits((int)C, (long)N, P->q))
+            return tetra_fail(ctx, TETRA_E_INVALID, "time-blocked decimator: C <= %d, q <= %d, N + 54 <= %d samples",
+                              SB_MAXC, SB_MAXQ, SB_MAXT * SB_B);
+        if (blocked)
+            rc = fmt == TETRA_CF64 ? run_decimate_blocked<double>(ctx, P, (const double *)x, (int)C, (long)N,
+                                                                  (double *)db, grouped(M))
+                                   : run_decimate_blocked<float>(ctx, P, (const float *)x, (int)C, (long)N,
+                                                                 (float *)db, grouped(M));
+        else
+            rc = fmt == TETRA_CF64 ? run_decimate<double>(ctx, P, (const double *)x, row_major(N), (int)C, (long)N,
+                                                          (double *)db, grouped(M))
+                                   : run_decimate<float>(ctx, P, (const float *)x, row_major(N), (int)C, (long)N,
+                                                         (float *)db, grouped(M));
         if (rc) return rc;
         d = db;
         ld = grouped(M);

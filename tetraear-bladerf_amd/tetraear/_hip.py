@@ -30,7 +30,7 @@ class CompatPlan(ctypes.Structure):
     _fields_ = [
         ("q", ctypes.c_int32), ("dec_f64", ctypes.c_int32), ("filt", ctypes.c_int32),
         ("ntaps", ctypes.c_int32), ("sps", ctypes.c_int32), ("phase_step", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 2), ("fs_dec", ctypes.c_double),
+        ("flags", ctypes.c_int32), ("reserved", ctypes.c_int32), ("fs_dec", ctypes.c_double),
         ("sos_f32", ctypes.c_float * 24), ("zi_f32", ctypes.c_float * 8),
         ("sos_f64", ctypes.c_double * 24), ("zi_f64", ctypes.c_double * 8),
         ("b", ctypes.c_double * 8), ("a", ctypes.c_double * 8), ("lzi", ctypes.c_double * 8),
@@ -38,6 +38,7 @@ class CompatPlan(ctypes.Structure):
     ]
 
 
+COMPAT_SEQUENTIAL, COMPAT_BLOCKED = 1, 2   # tetra_compat_plan.flags: decimator form (0: automatic)
 ETSI_FORCE_GENERIC = 1   # tetra_etsi_plan.flags: run a canonical plan on the generic-rate kernel
 
 
@@ -85,6 +86,7 @@ def _bind(L):
         "tetra_profile": (_i32, [_vp, _i32]),
         "tetra_profile_read": (_i32, [_vp, ctypes.c_char_p, _sz, _vp, _vp, _i32, _i32p]),
         "tetra_compat_symbols": (ctypes.c_int64, [ctypes.POINTER(CompatPlan), _sz]),
+        "tetra_compat_blocked_table": (_i32, [ctypes.POINTER(CompatPlan), _i32, _vp]),
         "tetra_demod_compat": (_i32, [_vp, ctypes.POINTER(CompatPlan), _vp, _i32, _sz, _sz, _vp, _vp, _vp, _vp, _vp,
                                       _sz, _i32p]),
         "tetra_decimate": (_i32, [_vp, ctypes.POINTER(CompatPlan), _vp, _i32, _sz, _sz, _vp]),

@@ -93,9 +93,18 @@ def _fill(arr, vals):
         arr[i] = v
 
 
-def compat_plan(sample_rate, n, fmt, bandwidth=25000):
-    """Build the device plan for process() on n samples (processor.py:239-273 decisions)."""
+DECIMATORS = {"auto": 0, "sequential": _hip.COMPAT_SEQUENTIAL, "blocked": _hip.COMPAT_BLOCKED}
+
+
+def compat_plan(sample_rate, n, fmt, bandwidth=25000, decimator="auto"):
+    """Build the device plan for process() on n samples (processor.py:239-273 decisions).
+
+    ``decimator`` picks the form of decimate's sosfiltfilt (include/tetra_hip.h, TETRA_COMPAT_*):
+    "sequential" is scipy's operation order, bit-identical to the reference; "blocked" recurses
+    256-sample tiles in parallel (latency mode, within the filter's fp32 noise of scipy); "auto"
+    lets tetra_demod_compat take the blocked form for batches of <= 64 channels at q <= 16."""
     p = _hip.CompatPlan()
+    p.flags = DECIMATORS[decimator]
     rate = sample_rate
     p.q = 0
     if rate > TARGET_RATE * 2:
@@ -141,12 +150,17 @@ def mixer_coefficient(freq_offset):
 class SignalProcessor:
     """Processes raw IQ samples for TETRA demodulation (processor.py:18)."""
 
-    def __init__(self, sample_rate=2.4e6, mode=None):
+    def __init__(self, sample_rate=2.4e6, mode=None, decimator="auto"):
         self.sample_rate = sample_rate
         self.symbol_rate = SYMBOL_RATE
         self.samples_per_symbol = int(sample_rate / self.symbol_rate)
         self.symbols = None
         self.mode = demod_mode(mode)
+        if decimator not in DECIMATORS:
+            raise ValueError(f"decimator must be one of {sorted(DECIMATORS)}, not {decimator!r}")
+        # compat process(): the decimator form (compat_plan); "auto" serves a single chunk with the
+        # time-blocked (latency) form, a large batch with the scipy-exact sequential one
+        self.decimator = decimator
         self._etsi = None
 
     # --------------------------------------------------------------- component methods
@@ -286,7 +300,7 @@ class SignalProcessor:
         real_in = not np.iscomplexobj(x)
         fmt = _fmt_of(x)
         xc = _as_complex(x, fmt)
-        plan, m, _ = compat_plan(self.sample_rate, len(x), fmt)
+        plan, m, _ = compat_plan(self.sample_rate, len(x), fmt, decimator=self.decimator)
         smax = m // plan.sps + 1
         soft = np.empty(smax, np.complex128)
         hard = np.empty(smax, np.uint8)
@@ -331,7 +345,7 @@ class SignalProcessor:
         else:
             fmt = _fmt_of(x)
             xc = _as_complex(x, fmt)
-        plan, m, _ = compat_plan(self.sample_rate, N, fmt)
+        plan, m, _ = compat_plan(self.sample_rate, N, fmt, decimator=self.decimator)
         smax = m // plan.sps + 1
         soft = np.empty((C, smax), np.complex128)
         hard = np.empty((C, smax), np.uint8)
