@@ -124,10 +124,12 @@ int tetra_demod_compat(tetra_ctx *ctx, const tetra_compat_plan *plan, const void
                        void *soft, uint8_t *hard, int32_t *nsym, size_t smax, int32_t *soft_f32);
 /* Number of soft symbols process() yields for N input samples under `plan`. */
 int64_t tetra_compat_symbols(const tetra_compat_plan *plan, size_t N);
-/* Host-only: the time-blocked decimator's table Phi^(2^r), r = 0..9, row-major 8 x 8 float64 each
- * (Phi = A^256, A the 4-section cascade's one-sample zero-input transition) from the plan's
- * complex64 (f64 = 0) or complex128 (f64 = 1) SOS; table holds 640 doubles. */
-int tetra_compat_blocked_table(const tetra_compat_plan *plan, int f64, double *table);
+/* Host-only: the latency mode's state-transition tables.  which = 0 / 1: the time-blocked
+ * decimator's Phi^(2^r), r = 0..9, row-major 8 x 8 float64 each (Phi = A^256, A the 4-section
+ * cascade's one-sample zero-input transition) from the plan's complex64 / complex128 SOS, 640
+ * doubles; which = 2: the time-blocked filtfilt's Psi^(2^r) (Psi = B^128, B lfilter's one-sample
+ * transition of its 4 states), 160 doubles. */
+int tetra_compat_blocked_table(const tetra_compat_plan *plan, int which, double *table);
 
 /* Component entry points, one per SignalProcessor method (each over C rows of length N). */
 /* scipy.signal.decimate(x, q) as called at processor.py:254: out [C][ceil(N/q)] in iq_fmt. */

@@ -236,6 +236,101 @@ def decimate_blocked(x, q):
     return y[edge:-edge][::q]
 
 
+LB_B, LB_NS = 128, 4
+
+
+def lf_blocked_fits(C, M, ntaps=5):
+    """The shapes whose filtfilt tetra_demod_compat runs time-blocked in latency mode."""
+    return 1 <= C <= SB_MAXC and ntaps == LB_NS + 1 and -(-(M + 6 * ntaps) // LB_B) <= SB_MAXT
+
+
+def lfilter_table(b, a):
+    """Psi^(2^r) (Psi = B^LB_B, B scipy lfilter's one-sample zero-input transition of its 4 DF-II-T
+    states), float64 [SB_NPOW, 4, 4], in compat_demod.hip: lfilter_table's operation order."""
+    b = [float(v) for v in b]
+    a = [float(v) for v in a]
+    K = LB_NS
+    Bm = [[0.0] * K for _ in range(K)]
+    for c in range(K):
+        z = [0.0] * K
+        z[c] = 1.0
+        xn = 0.0
+        yn = z[0] + b[0] * xn
+        zn = [0.0] * K
+        for k in range(K - 1):
+            zn[k] = (z[k + 1] + xn * b[k + 1]) - yn * a[k + 1]
+        zn[K - 1] = xn * b[K] - yn * a[K]
+        for i in range(K):
+            Bm[i][c] = zn[i]
+
+    def square(P):
+        out = [[0.0] * K for _ in range(K)]
+        for i in range(K):
+            for j in range(K):
+                acc = 0.0
+                for k in range(K):
+                    acc = acc + P[i][k] * P[k][j]
+                out[i][j] = acc
+        return out
+
+    n = 1
+    while n < LB_B:
+        Bm = square(Bm)
+        n <<= 1
+    tab = [Bm]
+    for _ in range(1, SB_NPOW):
+        tab.append(square(tab[-1]))
+    return np.array(tab, np.float64)
+
+
+def _lf_blocked_pass(bb, aa, zi, c, tab):
+    """lfilter of one real float64 sequence c from state zi * c[0], time-blocked (tiles of LB_B)."""
+    L = len(c)
+    Tn = -(-L // LB_B)
+    w = np.zeros((Tn, LB_NS), np.float64)
+    w[0] = zi * c[0]
+    for k in range(Tn - 1):
+        z = np.zeros(LB_NS, np.float64)
+        lib().orc_lfilter_f64(bb, aa, len(bb), z, np.array(c[k * LB_B:(k + 1) * LB_B], np.float64), LB_B)
+        w[k + 1] = z
+    r = 0
+    while (1 << r) < Tn:
+        d = 1 << r
+        u = w[:-d].copy()
+        acc = w[d:].copy()
+        for j in range(LB_NS):
+            acc = acc + tab[r][None, :, j] * u[:, j:j + 1]
+        w[d:] = acc
+        r += 1
+    out = np.empty(L, np.float64)
+    for k in range(Tn):
+        t = np.array(c[k * LB_B:(k + 1) * LB_B], np.float64)
+        lib().orc_lfilter_f64(bb, aa, len(bb), w[k].copy(), t, len(t))
+        out[k * LB_B:k * LB_B + len(t)] = t
+    return out
+
+
+def filtfilt_blocked(b, a, x):
+    """filtfilt(b, a, x) as the product's latency mode computes it (compat_demod.hip: k_lfb_*)."""
+    assert a[0] == 1.0
+    edge = 3 * max(len(a), len(b))
+    if x.shape[0] <= edge:
+        raise ValueError(f"The length of the input vector x must be greater than padlen, which is {edge}.")
+    zi = np.ascontiguousarray(_ss.lfilter_zi(b, a), dtype=np.float64)
+    ext = _odd_ext(x, edge)
+    dtype = np.result_type(b, a, ext, zi[:1] * ext[:1])
+    bb = np.ascontiguousarray(b, np.float64)
+    aa = np.ascontiguousarray(a, np.float64)
+    tab = lfilter_table(bb, aa)
+    outs = []
+    for comp in _components(ext.astype(dtype)):
+        f = _lf_blocked_pass(bb, aa, zi, np.ascontiguousarray(comp, np.float64), tab)
+        r = _lf_blocked_pass(bb, aa, zi, np.ascontiguousarray(f[::-1]), tab)
+        outs.append(r[::-1])
+    y = (outs[0] + 1j * outs[1]).astype(dtype) if np.iscomplexobj(ext.astype(dtype)) else outs[0].astype(dtype)
+    return y[edge:-edge]
+
+
 # ----------------------------------------------------------------------------- demod
 
 def _pairwise_sum(v):
@@ -263,6 +358,17 @@ class SignalProcessor:
         try:
             b, a = _ss.butter(4, cutoff, btype="low")
             return filtfilt(b, a, np.asarray(samples))
+        except Exception:
+            return samples
+
+    def _filter_blocked(self, samples, fs):
+        """filter_signal(samples, 25000, fs) with the latency mode's time-blocked filtfilt."""
+        if len(samples) == 0:
+            return samples
+        cutoff = min(0.99, max(0.01, (25000 / 2) / (fs / 2)))
+        try:
+            b, a = _ss.butter(4, cutoff, btype="low")
+            return filtfilt_blocked(b, a, np.asarray(samples))
         except Exception:
             return samples
 
@@ -331,7 +437,10 @@ class SignalProcessor:
                     pass
         if freq_offset != 0:
             samples = self.frequency_shift(samples, freq_offset, sample_rate=rate)
-        filtered = self.filter_signal(samples, bandwidth=25000, sample_rate=rate)
+        if self.decimator != "sequential" and lf_blocked_fits(1, len(samples)):   # one chunk: latency mode
+            filtered = self._filter_blocked(samples, rate)
+        else:
+            filtered = self.filter_signal(samples, bandwidth=25000, sample_rate=rate)
         sym = self.extract_symbols(filtered, sample_rate=rate)
         self.symbols = sym
         return self.demodulate_dqpsk(sym)

@@ -89,3 +89,39 @@ def test_blocked_edges_against_sequential(n):
         assert np.array_equal(a, b)
     else:
         assert np.max(np.abs(a - b)) <= 1e-5 * np.max(np.abs(a))
+
+
+def test_blocked_chain_within_float64_rounding_of_filtfilt(g1):
+    """The latency mode's whole chain (oracle, decimator="auto" as one process() call runs it):
+    time-blocked decimate where it fits and time-blocked filtfilt, against the reference fixtures --
+    the filtfilt part is float64, so with a sequential decimator (the 20 MSps case) it stays within
+    1e-12 of the reference; every served case within 1e-5 and no decision off outside the band."""
+    z, meta = g1
+    n = 0
+    for i, m in enumerate(meta):
+        x = iq_to_c64(z[f"c{i}_iq"])
+        p = O.SignalProcessor(m["fs"], decimator="auto")
+        hard = p.process(x, m["freq_offset"])
+        want, wh = z[f"c{i}_symbols"], z[f"c{i}_hard"]
+        assert p.symbols.dtype == want.dtype and p.symbols.shape == want.shape, (i, m)
+        if not len(want):
+            continue
+        err = np.max(np.abs(p.symbols - want))
+        dec_blocked = m["dec_ok"] and m["q"] >= 2 and O.blocked_fits(1, len(x), m["q"])
+        assert err <= (1e-5 if dec_blocked else 1e-12 * max(1.0, np.max(np.abs(want)))), (i, m, err)
+        bad = (hard != wh) & ~band(want)[:len(hard)]
+        assert not bad.any(), (i, m)
+        n += 1
+    assert n >= 25
+
+
+def test_library_lfilter_table_equals_the_oracle_table():
+    from tetraear import _hip
+    from tetraear.signal.processor import compat_plan
+    for fs in (1.8e6, 2.4e6, 240000.0, 1.0e6):
+        plan, _, _ = compat_plan(fs, 131072, _hip.TETRA_CF32)
+        want = O.lfilter_table(np.array(plan.b[:5]), np.array(plan.a[:5]))
+        got = np.zeros(O.SB_NPOW * 16)
+        assert _hip.lib().tetra_compat_blocked_table(plan, 2, _hip.ptr(got)) == 0
+        assert np.array_equal(got, want.ravel()), fs
+        assert np.all(np.isfinite(want)) and np.max(np.abs(want[-1])) < 1.0

@@ -30,6 +30,8 @@ enum Slot {
     S_W14,                                                 // ETSI: scrambler inits the cell table holds
     S_W15,                                                 // ETSI generic-rate tap tables (etsi_rate.hip)
     S_W16,                                                 // compat time-blocked decimator: tile states, Phi table
+    S_W17,                                                 // compat time-blocked filtfilt: tile states
+    S_W18,                                                 // compat latency mode: extract_symbols' |y|^2 rows
     S_COUNT
 };
 

@@ -920,6 +920,188 @@ __global__ __launch_bounds__(64) void k_lf_bwd(const double *__restrict__ scr, L
     }
 }
 
+// ------------------------------------------------------------------ time-blocked filtfilt (latency mode)
+// filter_signal's lfilter passes for a few channels, parallel in time like the decimator above: one
+// lane per (channel, component, tile of LB_B samples), the tile's input -- the odd extension of the
+// (mixed) decimated samples, each mixed in parallel as it is loaded -- staged in LDS; pass 1 from zero
+// state gives each tile's end state (the 4 DF-II-T states), k_lfb_scan the true start states in
+// float64 (Psi = B^LB_B, B the one-sample zero-input transition of scipy's lfilter loop), pass 2
+// the outputs.  Everything is float64, so the outputs differ from scipy's sequential pass by float64
+// rounding only (oracle/compat.py: filtfilt_blocked restates it; the GPU equals it bit for bit).
+constexpr int LB_B = 128;        // samples per tile
+constexpr int LB_ST = 64;        // stream-tiles per workgroup (one lane each)
+constexpr int LB_NS = 4;         // states (butter(4): 5 taps)
+
+struct LbGeo {
+    int C, Tn, pad;
+    long M, L;
+};
+
+// stream-tile g = (ch * Tn + tile) * 2 + comp
+template <typename TIn, bool FWD, bool FINAL>
+__global__ __launch_bounds__(LB_ST) void k_lfb_tile(const TIn *__restrict__ x, Lay lx, const double *__restrict__ mixc,
+                                                    const uint8_t *__restrict__ mixon, double fs,
+                                                    double *__restrict__ scr, Lay ls, LbGeo G,
+                                                    const double *__restrict__ b, const double *__restrict__ a,
+                                                    const double *__restrict__ states, double *__restrict__ ends,
+                                                    double *__restrict__ out, Lay lo) {
+    __shared__ double buf[LB_ST][LB_B + 1];
+    const int tid = threadIdx.x;
+    const long ntiles = (long)2 * G.C * G.Tn;
+    for (int i = tid; i < LB_ST * LB_B; i += LB_ST) {
+        const int r = i / LB_B, j = i % LB_B;
+        const long g = (long)blockIdx.x * LB_ST + r;
+        double v = 0.0;
+        if (g < ntiles) {
+            const int comp = (int)(g & 1), tile = (int)((g >> 1) % G.Tn), ch = (int)((g >> 1) / G.Tn);
+            const long e = (long)tile * LB_B + j;
+            if (e < G.L) {
+                if (FWD) {
+                    const bool mix = mixon && mixon[ch];
+                    v = lf_ext(x + lx.off(ch, 0), lx.s_n, G.M, G.pad, e, comp, mix, mix ? mixc[ch] : 0.0, fs);
+                } else {
+                    v = scr[ls.off(ch, G.L - 1 - e) + comp];
+                }
+            }
+        }
+        buf[r][j] = v;
+    }
+    __syncthreads();
+    const long g = (long)blockIdx.x * LB_ST + tid;
+    const bool own = g < ntiles;
+    const int tile = own ? (int)((g >> 1) % G.Tn) : 0;
+    const int len = own ? (int)min((long)LB_B, G.L - (long)tile * LB_B) : 0;
+    Lfilt<LB_NS + 1> f;
+#pragma unroll
+    for (int k = 0; k <= LB_NS; ++k) { f.bb[k] = b[k]; f.aa[k] = a[k]; }
+#pragma unroll
+    for (int k = 0; k < LB_NS; ++k) f.z[k] = (FINAL && own) ? states[g * LB_NS + k] : 0.0;
+    for (int j0 = 0; j0 < len; j0 += 16) {
+        double in[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) in[u] = buf[tid][min(j0 + u, LB_B - 1)];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            if (j0 + u < len) {
+                const double y = f.step(in[u]);
+                if (FINAL) buf[tid][j0 + u] = y;
+            }
+        }
+    }
+    if (!FINAL) {
+        if (own) {
+#pragma unroll
+            for (int k = 0; k < LB_NS; ++k) ends[g * LB_NS + k] = f.z[k];
+        }
+        return;
+    }
+    __syncthreads();
+    for (int i = tid; i < LB_ST * LB_B; i += LB_ST) {
+        const int r = i / LB_B, j = i % LB_B;
+        const long gg = (long)blockIdx.x * LB_ST + r;
+        if (gg >= ntiles) continue;
+        const int comp = (int)(gg & 1), tl = (int)((gg >> 1) % G.Tn), ch = (int)((gg >> 1) / G.Tn);
+        const long e = (long)tl * LB_B + j;
+        if (e >= G.L) continue;
+        if (FWD) {
+            scr[ls.off(ch, e) + comp] = buf[r][j];
+        } else {   // ext index L-1-e -> output t = ext - pad
+            const long t = G.L - 1 - e - G.pad;
+            if (t >= 0 && t < G.M) out[lo.off(ch, t) + comp] = buf[r][j];
+        }
+    }
+}
+
+// Start states of every tile of one stream (workgroup = stream 2 ch + comp, thread = tile), as
+// k_sosb_scan: w_0 = zi * ext[0] (forward) or zi * scr[L-1] (backward), w_k = e_{k-1};
+// w_k += Psi^d w_{k-d} for d = 1, 2, 4, .., products summed in j order without FMA.
+template <typename TIn, bool FWD>
+__global__ __launch_bounds__(1024) void k_lfb_scan(const TIn *__restrict__ x, Lay lx, const double *__restrict__ mixc,
+                                                   const uint8_t *__restrict__ mixon, double fs,
+                                                   const double *__restrict__ scr, Lay ls, LbGeo G,
+                                                   const double *__restrict__ zi, const double *__restrict__ psi,
+                                                   const double *__restrict__ ends, double *__restrict__ states) {
+    __shared__ double w[SB_MAXT][LB_NS];
+    const int k = threadIdx.x, s = blockIdx.x, ch = s >> 1, comp = s & 1;
+    const bool on = k < G.Tn;
+    double v[LB_NS];
+    if (on) {
+        if (k == 0) {
+            double x0;
+            if (FWD) {
+                const bool mix = mixon && mixon[ch];
+                x0 = lf_ext(x + lx.off(ch, 0), lx.s_n, G.M, G.pad, 0, comp, mix, mix ? mixc[ch] : 0.0, fs);
+            } else {
+                x0 = scr[ls.off(ch, G.L - 1) + comp];
+            }
+#pragma unroll
+            for (int i = 0; i < LB_NS; ++i) v[i] = zi[i] * x0;
+        } else {
+            const double *e = ends + ((size_t)(ch * G.Tn + k - 1) * 2 + comp) * LB_NS;
+#pragma unroll
+            for (int i = 0; i < LB_NS; ++i) v[i] = e[i];
+        }
+#pragma unroll
+        for (int i = 0; i < LB_NS; ++i) w[k][i] = v[i];
+    }
+    for (int r = 0; (1 << r) < G.Tn; ++r) {
+        const int d = 1 << r;
+        __syncthreads();
+        double u[LB_NS];
+        const bool upd = on && k >= d;
+        if (upd) {
+#pragma unroll
+            for (int i = 0; i < LB_NS; ++i) u[i] = w[k - d][i];
+        }
+        __syncthreads();
+        if (upd) {
+            const double *P = psi + (size_t)r * LB_NS * LB_NS;
+#pragma unroll
+            for (int i = 0; i < LB_NS; ++i) {
+                double acc = v[i];
+#pragma unroll
+                for (int j = 0; j < LB_NS; ++j) acc = acc + P[i * LB_NS + j] * u[j];
+                v[i] = acc;
+                w[k][i] = acc;
+            }
+        }
+    }
+    if (on) {
+        double *o = states + ((size_t)(ch * G.Tn + k) * 2 + comp) * LB_NS;
+#pragma unroll
+        for (int i = 0; i < LB_NS; ++i) o[i] = v[i];
+    }
+}
+
+// B (scipy lfilter's one-sample zero-input transition of the 4 DF-II-T states) and the table
+// Psi^(2^r) = B^(LB_B 2^r), r < SB_NPOW, row-major 4 x 4 each; products summed in k order, no FMA.
+void lfilter_table(const double *bcoef, const double *acoef, double *tab /*[SB_NPOW * 16]*/) {
+    constexpr int K = LB_NS;
+    double Bm[K * K];
+    for (int c = 0; c < K; ++c) {
+        double z[K] = {0}, zn[K];
+        z[c] = 1.0;
+        const double xn = 0.0;
+        const double yn = z[0] + bcoef[0] * xn;
+        for (int k = 0; k < K - 1; ++k) zn[k] = (z[k + 1] + xn * bcoef[k + 1]) - yn * acoef[k + 1];
+        zn[K - 1] = xn * bcoef[K] - yn * acoef[K];
+        for (int i = 0; i < K; ++i) Bm[i * K + c] = zn[i];
+    }
+    auto square = [](const double *P, double *outp) {
+        double t[K * K];
+        for (int i = 0; i < K; ++i)
+            for (int j = 0; j < K; ++j) {
+                double acc = 0.0;
+                for (int k = 0; k < K; ++k) acc = acc + P[i * K + k] * P[k * K + j];
+                t[i * K + j] = acc;
+            }
+        for (int i = 0; i < K * K; ++i) outp[i] = t[i];
+    };
+    for (int n = 1; n < LB_B; n <<= 1) square(Bm, Bm);
+    for (int i = 0; i < K * K; ++i) tab[i] = Bm[i];
+    for (int r = 1; r < SB_NPOW; ++r) square(tab + (r - 1) * K * K, tab + r * K * K);
+}
+
 // frequency_shift alone (component API, and the unfiltered-but-shifted process() path).
 template <typename TIn>
 __global__ __launch_bounds__(256) void k_mix(const TIn *__restrict__ x, Lay lx, int C, long N,
@@ -952,6 +1134,20 @@ __device__ __forceinline__ T np_cabs(T xr, T xi) {
     const bool div_ok = !(larger == (T)0 || smaller == inf);
     const T r = div_ok ? smaller / larger : (T)0;
     return sqrt(fma(r, r, (T)1)) * larger;
+}
+
+// extract_symbols' element values |y[n]|^2 (numpy's |z|, squared) for every sample of every channel,
+// in parallel: the latency mode's prepass, so k_extract's per-phase pairwise sums read them instead of
+// each lane computing its phase's ~1000 |z| one after another.  pw rows [C][M].
+template <typename T>
+__global__ __launch_bounds__(256) void k_cabs2(const T *__restrict__ y, Lay ly, int C, long M, T *__restrict__ pw) {
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int ch = (int)(gid / M);
+    const long n = gid - (long)ch * M;
+    if (ch >= C) return;
+    const size_t o = ly.off(ch, n);
+    const T a = np_cabs(y[o], y[o + 1]);
+    pw[(size_t)ch * M + n] = a * a;
 }
 
 // np.mean of v(0..n-1): numpy's pairwise summation (leaf blocks <= 128 with 8 accumulators,
@@ -1016,7 +1212,9 @@ struct PhasePower {
     size_t sy;
     long ph;
     int sps;
+    const T *pw;   // the channel's k_cabs2 row, or null: compute |z|^2 here
     __device__ __forceinline__ T operator()(long i) const {
+        if (pw) return pw[ph + i * sps];
         const size_t o = (size_t)(ph + i * sps) * sy;
         const T a = np_cabs(yp[o], yp[o + 1]);
         return a * a;
@@ -1073,7 +1271,7 @@ __device__ __forceinline__ T pw_sum(const PhasePower<T> &v, long s, long n) {
 template <typename T>
 __global__ __launch_bounds__(256) void k_extract(const T *__restrict__ y, Lay ly, int C, long M, int sps, int step,
                                                  T *__restrict__ sym, long smax, int32_t *__restrict__ nsym,
-                                                 int32_t *__restrict__ bestph) {
+                                                 int32_t *__restrict__ bestph, const T *__restrict__ pw = nullptr) {
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
     const int ch = gid >> 4, k = gid & 15;
     const int lane = threadIdx.x & 63;
@@ -1085,7 +1283,7 @@ __global__ __launch_bounds__(256) void k_extract(const T *__restrict__ y, Lay ly
     T power = (T)-2;
     long ns = (ok && k < nph) ? (M - ph) / sps : 0;
     if (ns > 0) {
-        const PhasePower<T> v{yp, sy, (long)ph, sps};
+        const PhasePower<T> v{yp, sy, (long)ph, sps, pw ? pw + (size_t)ch * M : nullptr};
         power = ns <= 3584 ? pw_sum<5, T>(v, 0, ns) / (T)ns : pairwise_mean<T>(v, ns);
     }
     T best = (T)-1;
@@ -1320,12 +1518,62 @@ int run_filtfilt(tetra_ctx *ctx, const tetra_compat_plan *P, const TIn *x, Lay l
     return TETRA_OK;
 }
 
+bool lf_blocked_fits(int C, long M, int ntaps) {
+    return C >= 1 && C <= SB_MAXC && ntaps == LB_NS + 1 && (M + 6 * ntaps + LB_B - 1) / LB_B <= SB_MAXT;
+}
+
+template <typename TIn>
+int run_filtfilt_blocked(tetra_ctx *ctx, const tetra_compat_plan *P, const TIn *x, Lay lx, int C, long M,
+                         const double *mixc, const uint8_t *mixon, double *out, Lay lo) {
+    const int nt = P->ntaps, pad = 3 * nt;
+    const long L = M + 2 * pad;
+    const int Tn = (int)ceil_div(L, LB_B);
+    const size_t ntile = (size_t)2 * C * Tn;
+    double *scr = (double *)ws(ctx, S_W2, grouped_elems(C, L) * sizeof(double));
+    double *coef = (double *)ws(ctx, S_W6, (3 * MAXTAP + SB_NPOW * LB_NS * LB_NS) * sizeof(double));
+    double *lb = (double *)ws(ctx, S_W17, 2 * ntile * LB_NS * sizeof(double));
+    if (!scr || !coef || !lb) return TETRA_E_NOMEM;
+    double hc[3 * MAXTAP + SB_NPOW * LB_NS * LB_NS] = {0};
+    for (int k = 0; k < nt; ++k) { hc[k] = P->b[k]; hc[MAXTAP + k] = P->a[k]; }
+    for (int k = 0; k < nt - 1; ++k) hc[2 * MAXTAP + k] = P->lzi[k];
+    lfilter_table(P->b, P->a, hc + 3 * MAXTAP);
+    HIP_TRY(ctx, hipMemcpyAsync(coef, hc, sizeof hc, hipMemcpyHostToDevice, ctx->stream));
+    double *ends = lb, *states = lb + ntile * LB_NS;
+    const double *psi = coef + 3 * MAXTAP;
+    const LbGeo G{C, Tn, pad, M, L};
+    const dim3 gt((unsigned)ceil_div((long)ntile, LB_ST)), bt(LB_ST);
+    const dim3 gs((unsigned)(2 * C)), bs((unsigned)std::min(SB_MAXT, (int)ceil_div(Tn, 64) * 64));
+    const Lay ls = grouped(L);
+    {
+        PROF(ctx, "compat_lfb_fwd");
+        hipLaunchKernelGGL((k_lfb_tile<TIn, true, false>), gt, bt, 0, ctx->stream, x, lx, mixc, mixon, P->fs_dec, scr,
+                           ls, G, coef, coef + MAXTAP, nullptr, ends, nullptr, lo);
+        hipLaunchKernelGGL((k_lfb_scan<TIn, true>), gs, bs, 0, ctx->stream, x, lx, mixc, mixon, P->fs_dec, scr, ls, G,
+                           coef + 2 * MAXTAP, psi, ends, states);
+        hipLaunchKernelGGL((k_lfb_tile<TIn, true, true>), gt, bt, 0, ctx->stream, x, lx, mixc, mixon, P->fs_dec, scr,
+                           ls, G, coef, coef + MAXTAP, states, nullptr, nullptr, lo);
+    }
+    {
+        PROF(ctx, "compat_lfb_bwd");
+        hipLaunchKernelGGL((k_lfb_tile<TIn, false, false>), gt, bt, 0, ctx->stream, x, lx, mixc, mixon, P->fs_dec, scr,
+                           ls, G, coef, coef + MAXTAP, nullptr, ends, nullptr, lo);
+        hipLaunchKernelGGL((k_lfb_scan<TIn, false>), gs, bs, 0, ctx->stream, x, lx, mixc, mixon, P->fs_dec, scr, ls, G,
+                           coef + 2 * MAXTAP, psi, ends, states);
+        hipLaunchKernelGGL((k_lfb_tile<TIn, false, true>), gt, bt, 0, ctx->stream, x, lx, mixc, mixon, P->fs_dec, scr,
+                           ls, G, coef, coef + MAXTAP, states, nullptr, out, lo);
+    }
+    HIP_TRY(ctx, hipGetLastError());
+    return TETRA_OK;
+}
+
 template <typename T>
 void launch_extract(tetra_ctx *ctx, const T *y, Lay ly, int C, long M, int sps, int step, T *sym, long smax,
-                    int32_t *nsym, int32_t *bph) {
+                    int32_t *nsym, int32_t *bph, T *pw = nullptr) {
     PROF(ctx, "compat_extract");
+    if (pw)   // latency mode: every |y|^2 first, in parallel
+        hipLaunchKernelGGL(k_cabs2<T>, dim3(grid_for((size_t)C * M, 256)), dim3(256), 0, ctx->stream, y, ly, C, M, pw);
     hipLaunchKernelGGL(k_extract<T>, dim3(grid_for((size_t)16 * C, 256)), dim3(256), 0, ctx->stream, y, ly, C, M, sps,
-                       step, sym, smax, nsym, bph);
+                       step, sym, smax, nsym, bph, (const T *)pw);
 }
 
 template <typename T>
@@ -1346,10 +1594,15 @@ int check_plan(tetra_ctx *ctx, const tetra_compat_plan *P) {
 
 extern "C" {
 
-int tetra_compat_blocked_table(const tetra_compat_plan *P, int f64, double *table) {
-    if (!P || !table) return TETRA_E_INVALID;
+int tetra_compat_blocked_table(const tetra_compat_plan *P, int which, double *table) {
+    if (!P || !table || which < 0 || which > 2) return TETRA_E_INVALID;
+    if (which == 2) {   // filtfilt's lfilter
+        if (P->ntaps != LB_NS + 1) return TETRA_E_INVALID;
+        lfilter_table(P->b, P->a, table);
+        return TETRA_OK;
+    }
     double dc[24];
-    for (int i = 0; i < 24; ++i) dc[i] = f64 ? P->sos_f64[i] : (double)P->sos_f32[i];
+    for (int i = 0; i < 24; ++i) dc[i] = which ? P->sos_f64[i] : (double)P->sos_f32[i];
     blocked_table(dc, table);
     return TETRA_OK;
 }
@@ -1524,12 +1777,27 @@ int tetra_demod_compat(tetra_ctx *ctx, const tetra_compat_plan *P, const void *i
     const void *y = d;
     Lay ly = ld;
     bool y_f64 = fmt == TETRA_CF64;
+    // latency mode (a few channels): the filtfilt passes time-blocked too, and extract_symbols'
+    // |y|^2 computed in parallel before its per-phase sums
+    const bool latency = (P->flags & TETRA_COMPAT_BLOCKED) || (!(P->flags & TETRA_COMPAT_SEQUENTIAL) && C <= SB_MAXC);
     if (P->filt || any_mix) {
         double *fb = (double *)ws(ctx, S_W3, grouped_elems((int)C, M) * 8);
         if (!fb) return TETRA_E_NOMEM;
         if (P->filt) {
-            rc = fmt == TETRA_CF64 ? run_filtfilt<double>(ctx, P, (const double *)d, ld, (int)C, M, mc, mo, fb, grouped(M))
-                                   : run_filtfilt<float>(ctx, P, (const float *)d, ld, (int)C, M, mc, mo, fb, grouped(M));
+            const bool lfb = latency && lf_blocked_fits((int)C, M, P->ntaps);
+            if ((P->flags & TETRA_COMPAT_BLOCKED) && !lfb)
+                return tetra_fail(ctx, TETRA_E_INVALID, "time-blocked filtfilt: C <= %d, M + 30 <= %d samples",
+                                  SB_MAXC, SB_MAXT * LB_B);
+            if (lfb)
+                rc = fmt == TETRA_CF64 ? run_filtfilt_blocked<double>(ctx, P, (const double *)d, ld, (int)C, M, mc, mo, fb,
+                                                                      grouped(M))
+                                       : run_filtfilt_blocked<float>(ctx, P, (const float *)d, ld, (int)C, M, mc, mo, fb,
+                                                                     grouped(M));
+            else
+                rc = fmt == TETRA_CF64 ? run_filtfilt<double>(ctx, P, (const double *)d, ld, (int)C, M, mc, mo, fb,
+                                                              grouped(M))
+                                       : run_filtfilt<float>(ctx, P, (const float *)d, ld, (int)C, M, mc, mo, fb,
+                                                             grouped(M));
             if (rc) return rc;
         } else if (fmt == TETRA_CF64) {
             hipLaunchKernelGGL(k_mix<double>, dim3(grid_for(C * M, 256)), dim3(256), 0, ctx->stream, (const double *)d,
@@ -1543,13 +1811,18 @@ int tetra_demod_compat(tetra_ctx *ctx, const tetra_compat_plan *P, const void *i
         y_f64 = true;
     }
     // stage 3+4: extract_symbols + demodulate_dqpsk (processor.py:267-271)
+    void *pw = nullptr;
+    if (latency) {
+        pw = ws(ctx, S_W18, (size_t)C * M * (y_f64 ? 8 : 4));
+        if (!pw) return TETRA_E_NOMEM;
+    }
     if (y_f64) {
         launch_extract<double>(ctx, (const double *)y, ly, (int)C, M, P->sps, P->phase_step, (double *)so, (long)smax, no,
-                               nullptr);
+                               nullptr, (double *)pw);
         launch_demod<double>(ctx, (const double *)so, (long)smax, (int)C, no, 0, P->thr, ho, (long)smax);
     } else {
         launch_extract<float>(ctx, (const float *)y, ly, (int)C, M, P->sps, P->phase_step, (float *)so, (long)smax, no,
-                              nullptr);
+                              nullptr, (float *)pw);
         launch_demod<float>(ctx, (const float *)so, (long)smax, (int)C, no, 0, P->thr, ho, (long)smax);
     }
     if (soft_f32) *soft_f32 = f32_soft ? 1 : 0;

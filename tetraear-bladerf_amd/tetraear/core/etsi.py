@@ -96,6 +96,8 @@ class EtsiLowerMac:
             if self.cell_state is None or len(self.cell_state) != C:
                 self.cell_state = np.full(C, UNKNOWN_CELL, np.uint32)
                 self.acquired = np.zeros(C, bool)
+            if self.acquired is None or len(self.acquired) != C:   # cell_state handed in from outside
+                self.acquired = np.zeros(C, bool)
             c.check(c.lib.tetra_lmac_etsi_acquire(c.handle, _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(nsym), C, smax,
                                                   _hip.ptr(self.cell_state), _hip.ptr(nb), _hip.ptr(bursts),
                                                   _hip.ptr(nk), _hip.ptr(blocks), _hip.ptr(t1)),
