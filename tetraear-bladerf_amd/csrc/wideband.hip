@@ -853,11 +853,20 @@ __global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict
     constexpr int ROWS = U::ROWS;                       // rows of one output group
     constexpr int OT = 4 * UP;                          // outputs per workgroup (4 waves x one group)
     constexpr int RB = 17;                              // rows in flight per batch
-    __shared__ float2 tile[RS_C * (OT + 1)];
-    __shared__ float tapL[use.n];   // taps in use order: each read is a same-address LDS broadcast
+    typedef float pf2 __attribute__((ext_vector_type(2)));   // (re, im): one v_pk_fma_f32 per tap
+    // One LDS block, taps first (in use order; each read a same-address broadcast), then the transpose
+    // tile.  With the taps at the bottom every tap read is one base register + a constant offset;
+    // behind the 74 KB tile the offsets overflowed ds_read's 16-bit immediate and every read cost a
+    // v_mov of its address (471 of ~2200 instructions per wave and group; round 5: 2207 -> 2016
+    // instructions, serial resampler 0.111 -> 0.109 ms, profiles/r05_ab_resamp_*.txt).  Taps stored
+    // pre-paired (w, w) for the packed FMA cut the pairing moves too but doubled the LDS reads: 0.116.
+    constexpr int TAPB = ((use.n * 4 + 15) / 16) * 16;
+    __shared__ __attribute__((aligned(16))) unsigned char lds_raw[TAPB + RS_C * (OT + 1) * 8];
+    float *tapP = reinterpret_cast<float *>(lds_raw);
+    float2 *tile = reinterpret_cast<float2 *>(lds_raw + TAPB);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    for (int e = tid; e < use.n; e += 256) tapL[e] = gU[e];
+    for (int e = tid; e < use.n; e += 256) tapP[e] = gU[e];
     const int k = min(blockIdx.x * RS_C + lane, M - 1);
     const int m = blockIdx.y * 4 + wv;                  // output group: outputs UP m .. UP m + UP - 1
     const int r0 = DOWN * m;                            // wave-uniform: row offsets are scalar
@@ -865,7 +874,6 @@ __global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict
     // clamped rows only feed outputs n >= n_keep, which are not stored
     const float2 *base = Y + k;
     __syncthreads();
-    typedef float pf2 __attribute__((ext_vector_type(2)));   // (re, im): one v_pk_fma_f32 per tap
     pf2 acc[UP];
 #pragma unroll
     for (int o = 0; o < UP; ++o) acc[o] = pf2{0.f, 0.f};
@@ -892,10 +900,8 @@ __global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict
                 }
 #pragma unroll
                 for (int o = 0; o < UP; ++o) {
-                    if (use.idx[i][o] >= 0) {
-                        const float w = tapL[use.idx[i][o]];
-                        acc[o] = __builtin_elementwise_fma(pf2{w, w}, vv, acc[o]);   // = fmaf per component
-                    }
+                    if (use.idx[i][o] >= 0)
+                        acc[o] = __builtin_elementwise_fma(pf2{tapP[use.idx[i][o]], tapP[use.idx[i][o]]}, vv, acc[o]);   // = fmaf per component
                 }
             }
         }
