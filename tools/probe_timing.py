@@ -23,7 +23,7 @@ def main():
     c = _hip.ctx()
     c.check(c.lib.tetra_set_stream(c.handle, None), "set_stream")
     st = BenchStep(c, nw, seed=1, device=dev)
-    st._front(c, st.y)   # waterfall + channeliser: y for every carrier chunk
+    st._front(c, st.y, None)   # waterfall + channeliser: y for every carrier chunk (plain k_timing forms: no om)
     torch.cuda.synchronize(dev)
     C, m2, sm = st.C, st.m2, st.sm
     diag = torch.zeros((C, 4), dtype=torch.float32, device=dev)
