@@ -36,9 +36,17 @@ class ReferenceUnavailable(ImportError):
     """A member outside the hot path was asked for and no reference package is on the path."""
 
 
+_scan = (None, ())
+
+
 def reference_packages():
     """The reference's ``tetraear/`` directories: ``$TETRAEAR_REFERENCE_ROOT/tetraear`` first, then
-    every other ``tetraear`` package on ``sys.path``, in path order (never this build's own)."""
+    every other ``tetraear`` package on ``sys.path``, in path order (never this build's own).  Cached
+    until sys.path or the variable changes (upper_mac asks once per frame)."""
+    global _scan
+    key = (os.environ.get("TETRAEAR_REFERENCE_ROOT"), tuple(p for p in sys.path if isinstance(p, str)))
+    if _scan[0] == key:
+        return list(_scan[1])
     roots = []
     env = os.environ.get("TETRAEAR_REFERENCE_ROOT")
     if env:
@@ -49,6 +57,7 @@ def reference_packages():
         d = os.path.realpath(os.path.join(r, "tetraear"))
         if d != _HERE and d not in out and os.path.isfile(os.path.join(d, "__init__.py")):
             out.append(d)
+    _scan = (key, tuple(out))
     return out
 
 
