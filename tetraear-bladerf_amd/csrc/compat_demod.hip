@@ -581,25 +581,50 @@ __global__ __launch_bounds__(4 * SbCfg<T>::ST) void k_sosb_tile(const T *__restr
     __shared__ T buf[ST][SB_B + 1];
     const int tid = threadIdx.x, sec = tid & 3, stl = tid >> 2;
     const long ntiles = (long)2 * G.C * G.Tn;
-    // cooperative load of the workgroup's tiles: ext (forward) or the reversed scratch row (backward)
-    for (int i = tid; i < ST * SB_B; i += 4 * ST) {
-        const int r = i / SB_B, j = i % SB_B;
+    // cooperative load of the workgroup's tiles: ext (forward) or the reversed scratch row (backward).
+    // A single channel is a few workgroups, so each thread's 64 loads are what the pass waits for:
+    // they go out 16 at a time (unconditional, from clamped indices), and ext's odd-extension
+    // arithmetic at the row ends is applied afterwards to the raw samples it reflects.
+    constexpr int PER = SB_B / 4, U = 16;
+    auto src = [&](int i, int &r, int &j, long &e, int &ch, int &comp, bool &in) -> const T * {
+        r = i / SB_B;
+        j = i % SB_B;
         const long g = (long)blockIdx.x * ST + r;
-        T v = 0;
-        if (g < ntiles) {
-            const int comp = (int)(g & 1), tile = (int)((g >> 1) % G.Tn), ch = (int)((g >> 1) / G.Tn);
-            const long e = (long)tile * SB_B + j;
-            if (e < G.L) {
-                if (FWD) {   // scipy _arraytools.odd_ext, in T
-                    const T *xr = x + (size_t)ch * G.N * 2 + comp;
-                    if (e < G.pad) v = (T)2 * xr[0] - xr[2 * (G.pad - e)];
-                    else if (e < G.pad + G.N) v = xr[2 * (e - G.pad)];
-                    else v = (T)2 * xr[2 * (G.N - 1)] - xr[2 * (G.N - 2 - (e - G.pad - G.N))];
-                } else {
-                    v = scr[(size_t)(2 * ch + comp) * G.Lp + (G.L - 1 - e)];
-                }
+        in = g < ntiles;
+        const long gg = in ? g : 0;
+        comp = (int)(gg & 1);
+        const int tile = (int)((gg >> 1) % G.Tn);
+        ch = (int)((gg >> 1) / G.Tn);
+        e = (long)tile * SB_B + j;
+        in = in && e < G.L;
+        const long ec = in ? e : 0;
+        if (FWD) {   // the sample scipy's odd_ext reflects (or copies) at ext index e
+            const long n = ec < G.pad ? G.pad - ec : (ec < G.pad + G.N ? ec - G.pad : G.N - 2 - (ec - G.pad - G.N));
+            return x + (size_t)ch * G.N * 2 + comp + 2 * n;
+        }
+        return scr + (size_t)(2 * ch + comp) * G.Lp + (G.L - 1 - ec);
+    };
+    for (int c0 = 0; c0 < PER; c0 += U) {
+        T v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int r, j, ch, comp;
+            long e;
+            bool in;
+            v[u] = *src(tid + 4 * ST * (c0 + u), r, j, e, ch, comp, in);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int r, j, ch, comp;
+            long e;
+            bool in;
+            src(tid + 4 * ST * (c0 + u), r, j, e, ch, comp, in);
+            T w = in ? v[u] : (T)0;
+            if (FWD && in && (e < G.pad || e >= G.pad + G.N)) {   // scipy _arraytools.odd_ext, in T
+                const T *xr = x + (size_t)ch * G.N * 2 + comp;
+                w = (T)2 * (e < G.pad ? xr[0] : xr[2 * (G.N - 1)]) - w;
             }
-            buf[r][j] = v;
+            buf[r][j] = w;
         }
     }
     __syncthreads();
@@ -929,7 +954,8 @@ __global__ __launch_bounds__(64) void k_lf_bwd(const double *__restrict__ scr, L
 // the outputs.  Everything is float64, so the outputs differ from scipy's sequential pass by float64
 // rounding only (oracle/compat.py: filtfilt_blocked restates it; the GPU equals it bit for bit).
 constexpr int LB_B = 128;        // samples per tile
-constexpr int LB_ST = 64;        // stream-tiles per workgroup (one lane each)
+constexpr int LB_ST = 64;        // stream-tiles per workgroup (one lane of wave 0 each)
+constexpr int LB_T = 256;        // threads per workgroup: all four waves stage the tiles
 constexpr int LB_NS = 4;         // states (butter(4): 5 taps)
 
 struct LbGeo {
@@ -939,7 +965,7 @@ struct LbGeo {
 
 // stream-tile g = (ch * Tn + tile) * 2 + comp
 template <typename TIn, bool FWD, bool FINAL>
-__global__ __launch_bounds__(LB_ST) void k_lfb_tile(const TIn *__restrict__ x, Lay lx, const double *__restrict__ mixc,
+__global__ __launch_bounds__(LB_T) void k_lfb_tile(const TIn *__restrict__ x, Lay lx, const double *__restrict__ mixc,
                                                     const uint8_t *__restrict__ mixon, double fs,
                                                     double *__restrict__ scr, Lay ls, LbGeo G,
                                                     const double *__restrict__ b, const double *__restrict__ a,
@@ -948,27 +974,81 @@ __global__ __launch_bounds__(LB_ST) void k_lfb_tile(const TIn *__restrict__ x, L
     __shared__ double buf[LB_ST][LB_B + 1];
     const int tid = threadIdx.x;
     const long ntiles = (long)2 * G.C * G.Tn;
-    for (int i = tid; i < LB_ST * LB_B; i += LB_ST) {
-        const int r = i / LB_B, j = i % LB_B;
+    // cooperative load by all LB_T threads, 8 loads in flight per thread (unconditional, clamped),
+    // then each element's value: lf_ext's arithmetic (mixer, odd extension) on the loaded samples
+    constexpr int PER = LB_ST * LB_B / LB_T, U = 8;
+    using P2 = typename std::conditional<sizeof(TIn) == 4, float2, double2>::type;
+    auto where = [&](int i, int &r, int &j, long &e, int &ch, int &comp, bool &in) {
+        r = i / LB_B;
+        j = i % LB_B;
         const long g = (long)blockIdx.x * LB_ST + r;
-        double v = 0.0;
-        if (g < ntiles) {
-            const int comp = (int)(g & 1), tile = (int)((g >> 1) % G.Tn), ch = (int)((g >> 1) / G.Tn);
-            const long e = (long)tile * LB_B + j;
-            if (e < G.L) {
-                if (FWD) {
-                    const bool mix = mixon && mixon[ch];
-                    v = lf_ext(x + lx.off(ch, 0), lx.s_n, G.M, G.pad, e, comp, mix, mix ? mixc[ch] : 0.0, fs);
-                } else {
-                    v = scr[ls.off(ch, G.L - 1 - e) + comp];
-                }
+        in = g < ntiles;
+        const long gg = in ? g : 0;
+        comp = (int)(gg & 1);
+        const int tile = (int)((gg >> 1) % G.Tn);
+        ch = (int)((gg >> 1) / G.Tn);
+        e = (long)tile * LB_B + j;
+        in = in && e < G.L;
+        if (!in) e = 0;
+    };
+    for (int c0 = 0; c0 < PER; c0 += U) {
+        P2 raw[U];      // forward: the input pair
+        double rb[U];   // backward: the scratch value
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int r, j, ch, comp;
+            long e;
+            bool in;
+            where(tid + LB_T * (c0 + u), r, j, e, ch, comp, in);
+            if (FWD) {   // the (re, im) pair of the sample lf_ext reflects (or copies) at ext index e
+                const long n = e < G.pad ? G.pad - e : (e < G.pad + G.M ? e - G.pad : G.M - 2 - (e - G.pad - G.M));
+                raw[u] = *reinterpret_cast<const P2 *>(x + lx.off(ch, 0) + (size_t)n * lx.s_n);
+            } else {
+                rb[u] = scr[ls.off(ch, G.L - 1 - e) + comp];
             }
         }
-        buf[r][j] = v;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int r, j, ch, comp;
+            long e;
+            bool in;
+            where(tid + LB_T * (c0 + u), r, j, e, ch, comp, in);
+            double v = 0.0;
+            if (in) {
+                if (FWD) {
+                    const bool mix = mixon && mixon[ch];
+                    const int side = e < G.pad ? -1 : (e < G.pad + G.M ? 0 : 1);
+                    const long n = side < 0 ? G.pad - e : (side == 0 ? e - G.pad : G.M - 2 - (e - G.pad - G.M));
+                    if (mix) {   // mixed_val on the loaded pair, then the extension in double
+                        const double c = mixc[ch];
+                        const double th = c * ((double)n / fs);
+                        double sn, co;
+                        sincos(th, &sn, &co);
+                        const double xr = (double)raw[u].x, xi = (double)raw[u].y;
+                        v = comp ? fma(xr, sn, xi * co) : fma(xr, co, -(xi * sn));
+                        if (side != 0)
+                            v = 2.0 * mixed_val(x + lx.off(ch, 0), lx.s_n, side < 0 ? 0 : G.M - 1, comp, true, c, fs) - v;
+                    } else {     // the extension in the input precision, then promoted
+                        const TIn vv = comp ? raw[u].y : raw[u].x;
+                        if (side == 0) {
+                            v = (double)vv;
+                        } else {
+                            const TIn ev = x[lx.off(ch, side < 0 ? 0 : G.M - 1) + comp];
+                            v = (double)((TIn)2 * ev - vv);
+                        }
+                    }
+                } else {
+                    v = rb[u];
+                }
+            }
+            buf[r][j] = v;
+        }
     }
     __syncthreads();
-    const long g = (long)blockIdx.x * LB_ST + tid;
-    const bool own = g < ntiles;
+    // the recursion: one lane of wave 0 per stream-tile
+    const int row = tid < LB_ST ? tid : 0;
+    const long g = (long)blockIdx.x * LB_ST + row;
+    const bool own = tid < LB_ST && g < ntiles;
     const int tile = own ? (int)((g >> 1) % G.Tn) : 0;
     const int len = own ? (int)min((long)LB_B, G.L - (long)tile * LB_B) : 0;
     Lfilt<LB_NS + 1> f;
@@ -979,12 +1059,12 @@ __global__ __launch_bounds__(LB_ST) void k_lfb_tile(const TIn *__restrict__ x, L
     for (int j0 = 0; j0 < len; j0 += 16) {
         double in[16];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) in[u] = buf[tid][min(j0 + u, LB_B - 1)];
+        for (int u = 0; u < 16; ++u) in[u] = buf[row][min(j0 + u, LB_B - 1)];
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
             if (j0 + u < len) {
                 const double y = f.step(in[u]);
-                if (FINAL) buf[tid][j0 + u] = y;
+                if (FINAL) buf[row][j0 + u] = y;
             }
         }
     }
@@ -996,7 +1076,7 @@ __global__ __launch_bounds__(LB_ST) void k_lfb_tile(const TIn *__restrict__ x, L
         return;
     }
     __syncthreads();
-    for (int i = tid; i < LB_ST * LB_B; i += LB_ST) {
+    for (int i = tid; i < LB_ST * LB_B; i += LB_T) {
         const int r = i / LB_B, j = i % LB_B;
         const long gg = (long)blockIdx.x * LB_ST + r;
         if (gg >= ntiles) continue;
@@ -1541,7 +1621,7 @@ int run_filtfilt_blocked(tetra_ctx *ctx, const tetra_compat_plan *P, const TIn *
     double *ends = lb, *states = lb + ntile * LB_NS;
     const double *psi = coef + 3 * MAXTAP;
     const LbGeo G{C, Tn, pad, M, L};
-    const dim3 gt((unsigned)ceil_div((long)ntile, LB_ST)), bt(LB_ST);
+    const dim3 gt((unsigned)ceil_div((long)ntile, LB_ST)), bt(LB_T);
     const dim3 gs((unsigned)(2 * C)), bs((unsigned)std::min(SB_MAXT, (int)ceil_div(Tn, 64) * 64));
     const Lay ls = grouped(L);
     {
