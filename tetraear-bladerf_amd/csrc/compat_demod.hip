@@ -1387,6 +1387,110 @@ __global__ __launch_bounds__(256) void k_extract(const T *__restrict__ y, Lay ly
     }
 }
 
+// Latency mode (a few channels): one 512-thread workgroup per channel, thread = (phase q < 16, leaf
+// l < 32).  numpy's pairwise sum of a phase's |y|^2 (pw_sum<5>: splits at n/2 rounded down to a
+// multiple of 8 until a part is <= 128, leaves of 8 accumulators) is the same tree here, with its
+// <= 32 leaves summed by 32 threads at once and combined in the tree's order by one thread: the same
+// adds, so the same power, the same phase and the same symbols as k_extract.  ns <= 3584 per phase
+// (five splits); longer chunks take k_extract.
+constexpr int XL_LEAVES = 32;
+__device__ __forceinline__ int leaf_at(long n, int want, long &s, long &m) {   // DFS leaf `want` of the tree on [0, n)
+    long st_s[6], st_n[6];
+    int sp = 0, idx = 0;
+    st_s[0] = 0;
+    st_n[0] = n;
+    sp = 1;
+    while (sp > 0) {
+        --sp;
+        const long ss = st_s[sp], nn = st_n[sp];
+        if (nn <= 128) {
+            if (idx == want) {
+                s = ss;
+                m = nn;
+                return 1;
+            }
+            ++idx;
+            continue;
+        }
+        long n2 = nn / 2;
+        n2 -= n2 % 8;
+        st_s[sp] = ss + n2;   // right pushed first: the left child is visited first
+        st_n[sp] = nn - n2;
+        ++sp;
+        st_s[sp] = ss;
+        st_n[sp] = n2;
+        ++sp;
+    }
+    return 0;
+}
+template <int D, typename T>
+__device__ T leaf_combine(const T *leaf, int &idx, long n) {   // pw_sum<D>'s adds over the leaf sums
+    if constexpr (D == 0) {
+        return leaf[idx++];
+    } else {
+        if (n <= 128) return leaf[idx++];
+        long n2 = n / 2;
+        n2 -= n2 % 8;
+        const T l = leaf_combine<D - 1, T>(leaf, idx, n2);
+        const T r = leaf_combine<D - 1, T>(leaf, idx, n - n2);
+        return l + r;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(512) void k_extract_lat(const T *__restrict__ y, Lay ly, int C, long M, int sps, int step,
+                                                     T *__restrict__ sym, long smax, int32_t *__restrict__ nsym,
+                                                     int32_t *__restrict__ bestph, const T *__restrict__ pw) {
+    __shared__ T leafs[16][XL_LEAVES];
+    __shared__ T power[16];
+    __shared__ int bsel;
+    const int ch = blockIdx.x, t = threadIdx.x, q = t >> 5, l = t & 31;
+    const int nph = (sps + step - 1) / step;
+    const int ph = q * step;
+    const long ns = q < nph ? (M - ph) / sps : 0;
+    const T *yp = y + ly.off(ch, 0);
+    if (ns > 0) {
+        long s0, m0;
+        if (leaf_at(ns, l, s0, m0)) {
+            const PhasePower<T> v{yp, ly.s_n, (long)ph, sps, pw + (size_t)ch * M};
+            leafs[q][l] = pw_leaf<T>(v, s0, m0);
+        }
+    }
+    __syncthreads();
+    if (l == 0) {
+        T p = (T)-2;
+        if (ns > 0) {
+            int idx = 0;
+            p = leaf_combine<5, T>(leafs[q], idx, ns) / (T)ns;
+        }
+        if (q < 16) power[q] = p;
+    }
+    __syncthreads();
+    if (t == 0) {   // k_extract's choice: the first phase of the largest power
+        T best = (T)-1;
+        int bph = 0;
+        for (int qq = 0; qq < nph && qq < 16; ++qq) {
+            const long nq = (M - qq * step) / sps;
+            if (nq > 0 && power[qq] > best) {
+                best = power[qq];
+                bph = qq * step;
+            }
+        }
+        bsel = bph;
+        nsym[ch] = (int32_t)((M - bph) / sps);
+        if (bestph) bestph[ch] = bph;
+    }
+    __syncthreads();
+    const int bph = bsel;
+    const long nout = (M - bph) / sps;
+    T *op = sym + (size_t)ch * smax * 2;
+    for (long i = t; i < nout; i += 512) {
+        const size_t o = (size_t)(bph + i * sps) * ly.s_n;
+        op[2 * i] = yp[o];
+        op[2 * i + 1] = yp[o + 1];
+    }
+}
+
 // ------------------------------------------------------------------ demodulate_dqpsk
 // One wave per channel.  sym rows [C][stride] complex T, S = nsym[ch] (or S_all).
 template <typename T>
@@ -1652,8 +1756,12 @@ void launch_extract(tetra_ctx *ctx, const T *y, Lay ly, int C, long M, int sps, 
     PROF(ctx, "compat_extract");
     if (pw)   // latency mode: every |y|^2 first, in parallel
         hipLaunchKernelGGL(k_cabs2<T>, dim3(grid_for((size_t)C * M, 256)), dim3(256), 0, ctx->stream, y, ly, C, M, pw);
-    hipLaunchKernelGGL(k_extract<T>, dim3(grid_for((size_t)16 * C, 256)), dim3(256), 0, ctx->stream, y, ly, C, M, sps,
-                       step, sym, smax, nsym, bph, (const T *)pw);
+    if (pw && M / sps <= 3584)   // ... and each phase's pairwise sum leaf-parallel
+        hipLaunchKernelGGL(k_extract_lat<T>, dim3(C), dim3(512), 0, ctx->stream, y, ly, C, M, sps, step, sym, smax, nsym,
+                           bph, (const T *)pw);
+    else
+        hipLaunchKernelGGL(k_extract<T>, dim3(grid_for((size_t)16 * C, 256)), dim3(256), 0, ctx->stream, y, ly, C, M, sps,
+                           step, sym, smax, nsym, bph, (const T *)pw);
 }
 
 template <typename T>
