@@ -85,8 +85,8 @@ def parse():
 def traffic_from_profiles(kernel, workload_key):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of this
     workload (profiles/*_summary.json, written by tools/pmc_summary.py from separate FETCH_SIZE /
-    WRITE_SIZE passes over the timed launches, with the gfx950 x2 FETCH correction for 16-B/lane
-    loads), or None."""
+    WRITE_SIZE passes over the timed launches, with the gfx950 x2 FETCH correction, calibrated at
+    4-, 8- and 16-B loads: profiles/r05_fetch_calibration.json), or None."""
     import glob
     import re
 

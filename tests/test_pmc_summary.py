@@ -1,6 +1,6 @@
 """tools/pmc_summary.py on synthetic rocprofv3 CSVs (CPU): kernels keyed by full name, timed launches
-selected between bench.py's k_region_mark launches, the FETCH correction chosen per kernel from its
-load width, and the fallback to the last K launches when a trace has no markers."""
+selected between bench.py's k_region_mark launches, the FETCH x2 correction at every load width
+(calibrated: profiles/r05_fetch_calibration.json), and the fallback to the last K launches when a trace has no markers."""
 import csv
 import json
 import os
@@ -80,8 +80,9 @@ def test_marker_window_full_names_and_corrections(tmp_path):
     assert k[K16]["timed_launches"] == 2 and k[K16]["timed_avg_ns"] == 1100
     assert "timed_launches" not in k[K16B]                       # setup only: nothing timed, not merged
     assert k[K16]["fetch_correction"] == 2 and k[K16]["read_bytes"] == 2 * 1024 * 1000
-    assert k[K8]["fetch_correction"] == 1 and k[K8]["hbm_bytes_per_launch"] == 1024 * (300 + 200)
-    assert k[KJ]["fetch_correction"] == 1
+    assert k[K8]["fetch_correction"] == 2 and k[K8]["hbm_bytes_per_launch"] == 1024 * (2 * 300 + 200)
+    assert k[KJ]["fetch_correction"] == 2
+    assert k[K8]["load_bytes_per_lane"] == 8   # information only
 
 
 def test_no_markers_falls_back_to_last_k(tmp_path):

@@ -13,12 +13,13 @@ the SAME bench command.
   fields.  A trace without marks (older bench) falls back to ``--timed K``: each kernel's last K
   launches.
 * HBM bytes (MI355X_MICROARCH.md, HBM / rocprofv3): FETCH_SIZE / WRITE_SIZE are KiB.  On gfx950
-  FETCH_SIZE reports exactly half the bytes of a wide coalesced streaming read (16 B per lane), so
-  the read bytes of a kernel whose streamed input is 16 B per lane are 2 x FETCH_SIZE; for narrower
-  loads the raw figure already matches the bytes (the wideband resampler's 8-B loads
-  read 328 MB raw for 320 MB of Y), and WRITE_SIZE is taken as is.  A kernel's load width is its
-  first pointer argument's element size, read from the demangled signature (``HIP_vector_type<float,
-  4u> const*`` -> 16 B); ``void const*`` inputs take the width from WIDTH_OVERRIDE.
+  FETCH_SIZE reports exactly half the bytes of a coalesced streaming read, so read bytes are
+  2 x FETCH_SIZE for every kernel; WRITE_SIZE is taken as is.  The guide states the half for 16-B
+  loads; tools/probes/probe_fetch.hip measured it for 4-, 8- and 16-B loads alike (1 GiB read:
+  FETCH_SIZE 0.500 of the bytes at each width; 512 MiB written: WRITE_SIZE 1.000;
+  profiles/r05_fetch_calibration.json).  ``load_bytes_per_lane`` (the first pointer argument's
+  element size, read from the demangled signature; ``void const*`` inputs from WIDTH_OVERRIDE) is
+  kept as information only.
 usage: pmc_summary.py TRACE_DIR FETCH_DIR WRITE_DIR OUT_JSON [workload] [--timed K]
 """
 import collections
@@ -29,6 +30,7 @@ import re
 import sys
 
 MARK = "k_region_mark"
+FETCH_CORRECTION = 2   # calibrated at 4, 8 and 16 B per lane (docstring)
 # kernels that take their streamed input as `const void *`: element bytes per lane load
 WIDTH_OVERRIDE = {"k_waterfall": 8, "k_chanfilt_g": 8}
 _SCALAR = {"float": 4, "int": 4, "unsigned int": 4, "double": 8, "long": 8, "unsigned long": 8, "short": 2,
@@ -141,7 +143,7 @@ def main():
             f = [v for _, v in in_window(pmc[k].get((fetch, "FETCH_SIZE"), []), pmc_win[fetch])]
             w = [v for _, v in in_window(pmc[k].get((write, "WRITE_SIZE"), []), pmc_win[write])]
             if f:
-                corr = 2 if wdt == 16 else 1
+                corr = FETCH_CORRECTION
                 e["fetch_size_kib_raw"] = sum(f) / len(f)
                 e["fetch_correction"] = corr
                 e["read_bytes"] = corr * 1024 * e["fetch_size_kib_raw"]
