@@ -166,6 +166,26 @@ def test_full_size_batch_vs_oracle(hip, decimator):
         _hard_equal(hard[c, :ns[c] - 1], h, o.symbols)
 
 
+def test_latency_mode_long_chunk_vs_oracle(hip):
+    """One channel of 520000 samples through the automatic (latency) mode: past the time-blocked
+    decimator's 262144-sample limit (the sequential form serves it) and past k_extract_lat's 3584
+    symbols per phase (k_extract over the |y|^2 prepass serves it) -- each fallback equal to the
+    oracle's same choice."""
+    import sys, os
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import _signals
+    from tetraear.signal import SignalProcessor
+    rng = np.random.default_rng(520)
+    x, _ = _signals.family("tetra", rng, 520000, 2.4e6)
+    p = SignalProcessor(2.4e6)
+    h = p.process(x, 1171.875)
+    o = O.SignalProcessor(2.4e6, decimator="auto")
+    ho = o.process(x, 1171.875)
+    assert len(p.symbols) == len(o.symbols) > 3584
+    assert np.max(np.abs(p.symbols - o.symbols)) <= SOFT_TOL
+    _hard_equal(h, ho, o.symbols)
+
+
 def test_decoder_matches_golden(hip, g2):
     from tetraear.core import TetraDecoder
     z, recs = g2
