@@ -564,7 +564,10 @@ constexpr int SB_MAXT = 1024;    // tiles per stream (one scan workgroup): L <= 
 constexpr int SB_NPOW = 10;      // Phi^(2^r), r < SB_NPOW: covers SB_MAXT tiles
 constexpr int SB_MAXC = 64;      // channels up to which tetra_demod_compat takes this path
 constexpr int SB_MAXQ = 16;      // decimation factors up to which it does
-template <typename T> struct SbCfg { static constexpr int ST = sizeof(T) == 4 ? 64 : 32; };   // stream-tiles / workgroup
+// stream-tiles per workgroup: few, so one channel's tiles spread over many CUs; SB_LT threads stage
+// them (SB_B ST / SB_LT loads each), wave 0's 4 ST lanes run the recursion
+template <typename T> struct SbCfg { static constexpr int ST = 16; };
+constexpr int SB_LT = 256;
 
 struct SbGeo {
     int C, Tn, pad, q;
@@ -573,28 +576,36 @@ struct SbGeo {
 
 // stream-tile g = (ch * Tn + tile) * 2 + comp
 template <typename T, bool FWD, bool FINAL>
-__global__ __launch_bounds__(4 * SbCfg<T>::ST) void k_sosb_tile(const T *__restrict__ x, T *__restrict__ scr, SbGeo G,
+__global__ __launch_bounds__(SB_LT) void k_sosb_tile(const T *__restrict__ x, T *__restrict__ scr, SbGeo G,
                                                                 const T *__restrict__ sos,
                                                                 const double *__restrict__ states,
                                                                 double *__restrict__ ends, T *__restrict__ out, Lay lo) {
     constexpr int ST = SbCfg<T>::ST;
     __shared__ T buf[ST][SB_B + 1];
+    __shared__ int rch[ST], rtile[ST];   // the rows' channel and tile: one division per row, not per element
     const int tid = threadIdx.x, sec = tid & 3, stl = tid >> 2;
     const long ntiles = (long)2 * G.C * G.Tn;
+    const int nrow = (int)min((long)ST, ntiles - (long)blockIdx.x * ST);   // rows this workgroup owns
+    if (tid < ST) {
+        const int pr = (int)((((long)blockIdx.x * ST + (tid < nrow ? tid : 0))) >> 1);
+        rtile[tid] = pr % G.Tn;
+        rch[tid] = pr / G.Tn;
+    }
+    __syncthreads();
     // cooperative load of the workgroup's tiles: ext (forward) or the reversed scratch row (backward).
     // A single channel is a few workgroups, so each thread's 64 loads are what the pass waits for:
     // they go out 16 at a time (unconditional, from clamped indices), and ext's odd-extension
     // arithmetic at the row ends is applied afterwards to the raw samples it reflects.
-    constexpr int PER = SB_B / 4, U = 16;
+    constexpr int PER = ST * SB_B / SB_LT, U = PER < 16 ? PER : 16;
+    static_assert(PER % U == 0 && 4 * ST <= 64, "loads per thread; the recursion fits wave 0");
     auto src = [&](int i, int &r, int &j, long &e, int &ch, int &comp, bool &in) -> const T * {
         r = i / SB_B;
         j = i % SB_B;
-        const long g = (long)blockIdx.x * ST + r;
-        in = g < ntiles;
-        const long gg = in ? g : 0;
-        comp = (int)(gg & 1);
-        const int tile = (int)((gg >> 1) % G.Tn);
-        ch = (int)((gg >> 1) / G.Tn);
+        in = r < nrow;
+        const int rr = in ? r : 0;
+        comp = rr & 1;   // ST is even: row parity = stream-tile parity
+        const int tile = rtile[rr];
+        ch = rch[rr];
         e = (long)tile * SB_B + j;
         in = in && e < G.L;
         const long ec = in ? e : 0;
@@ -611,14 +622,14 @@ __global__ __launch_bounds__(4 * SbCfg<T>::ST) void k_sosb_tile(const T *__restr
             int r, j, ch, comp;
             long e;
             bool in;
-            v[u] = *src(tid + 4 * ST * (c0 + u), r, j, e, ch, comp, in);
+            v[u] = *src(tid + SB_LT * (c0 + u), r, j, e, ch, comp, in);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             int r, j, ch, comp;
             long e;
             bool in;
-            src(tid + 4 * ST * (c0 + u), r, j, e, ch, comp, in);
+            src(tid + SB_LT * (c0 + u), r, j, e, ch, comp, in);
             T w = in ? v[u] : (T)0;
             if (FWD && in && (e < G.pad || e >= G.pad + G.N)) {   // scipy _arraytools.odd_ext, in T
                 const T *xr = x + (size_t)ch * G.N * 2 + comp;
@@ -628,6 +639,7 @@ __global__ __launch_bounds__(4 * SbCfg<T>::ST) void k_sosb_tile(const T *__restr
         }
     }
     __syncthreads();
+    if (tid < 4 * ST) {   // wave 0: the recursion (wave-uniform branch)
     const long g = (long)blockIdx.x * ST + stl;
     const bool own = g < ntiles;
     const int tile = own ? (int)((g >> 1) % G.Tn) : 0;
@@ -637,35 +649,55 @@ __global__ __launch_bounds__(4 * SbCfg<T>::ST) void k_sosb_tile(const T *__restr
         bq.z0 = (T)states[g * 8 + 2 * sec];
         bq.z1 = (T)states[g * 8 + 2 * sec + 1];
     }
+    // Ticks 0-2 and SB_B..SB_B+2 are guarded (a section starts at tick sec and ends at SB_B - 1 + sec);
+    // the rest are branch-free: every lane steps and (FINAL) writes its output to slot j = tick - sec
+    // -- section 3 writes slot j last, and inputs of slot j were read at the top of this batch or an
+    // earlier one.  The last tile of a stream (len < SB_B) steps on the zeros past its end: its end
+    // state is not used (the scan reads e_k for k < Tn - 1) and its outputs past len are not stored.
+    (void)len;
     T y = 0;
-    for (int tau0 = 0; tau0 < SB_B + 3; tau0 += 16) {
+    for (int tau0 = 0; tau0 < SB_B; tau0 += 16) {
         T in[16];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) in[u] = buf[stl][min(tau0 + u, SB_B - 1)];
+        for (int u = 0; u < 16; ++u) in[u] = buf[stl][tau0 + u];
+        if (tau0 == 0) {
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const T left = from_left(y);
-            const int j = tau0 + u - sec;
-            if (j >= 0 && j < len) {
+            for (int u = 0; u < 16; ++u) {
+                const T left = from_left(y);
+                const T xin = sec == 0 ? in[u] : left;
+                if (u >= 3 || u >= sec) {
+                    y = bq.step(xin);
+                    if (FINAL) buf[stl][u - sec] = y;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const T left = from_left(y);
                 y = bq.step(sec == 0 ? in[u] : left);
-                // input j was read at the top of this batch or an earlier one: the slot is free
-                if (FINAL && sec == 3) buf[stl][j] = y;
+                if (FINAL) buf[stl][tau0 + u - sec] = y;
             }
         }
     }
-    if (!FINAL) {
-        if (own) {
-            ends[g * 8 + 2 * sec] = (double)bq.z0;
-            ends[g * 8 + 2 * sec + 1] = (double)bq.z1;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {   // ticks SB_B .. SB_B + 2: sections u+1 .. 3 finish
+        const T left = from_left(y);
+        if (sec > u) {
+            y = bq.step(left);
+            if (FINAL) buf[stl][SB_B + u - sec] = y;
         }
-        return;
     }
+    if (!FINAL && own) {
+        ends[g * 8 + 2 * sec] = (double)bq.z0;
+        ends[g * 8 + 2 * sec + 1] = (double)bq.z1;
+    }
+    }
+    if (!FINAL) return;
     __syncthreads();
-    for (int i = tid; i < ST * SB_B; i += 4 * ST) {
+    for (int i = tid; i < ST * SB_B; i += SB_LT) {
         const int r = i / SB_B, j = i % SB_B;
-        const long gg = (long)blockIdx.x * ST + r;
-        if (gg >= ntiles) continue;
-        const int comp = (int)(gg & 1), tl = (int)((gg >> 1) % G.Tn), ch = (int)((gg >> 1) / G.Tn);
+        if (r >= nrow) continue;
+        const int comp = r & 1, tl = rtile[r], ch = rch[r];
         const long e = (long)tl * SB_B + j;
         if (e >= G.L) continue;
         if (FWD) {
@@ -686,8 +718,10 @@ __global__ __launch_bounds__(1024) void k_sosb_scan(const T *__restrict__ x, con
                                                     const T *__restrict__ zi, const double *__restrict__ phi,
                                                     const double *__restrict__ ends, double *__restrict__ states) {
     __shared__ double w[SB_MAXT][8];
+    __shared__ double ph[SB_NPOW * 64];   // the Phi^(2^r) table, read by every thread at every level
     const int k = threadIdx.x, s = blockIdx.x, ch = s >> 1, comp = s & 1;
     const bool on = k < G.Tn;
+    for (int i = k; i < SB_NPOW * 64; i += blockDim.x) ph[i] = phi[i];   // visible after the first level's barrier
     double v[8];
     if (on) {
         if (k == 0) {
@@ -719,7 +753,7 @@ __global__ __launch_bounds__(1024) void k_sosb_scan(const T *__restrict__ x, con
         }
         __syncthreads();
         if (upd) {
-            const double *P = phi + (size_t)r * 64;
+            const double *P = ph + r * 64;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 double acc = v[i];
@@ -954,7 +988,8 @@ __global__ __launch_bounds__(64) void k_lf_bwd(const double *__restrict__ scr, L
 // the outputs.  Everything is float64, so the outputs differ from scipy's sequential pass by float64
 // rounding only (oracle/compat.py: filtfilt_blocked restates it; the GPU equals it bit for bit).
 constexpr int LB_B = 128;        // samples per tile
-constexpr int LB_ST = 64;        // stream-tiles per workgroup (one lane of wave 0 each)
+constexpr int LB_ST = 16;        // stream-tiles per workgroup (one lane of wave 0 each): one channel's
+                                 // tiles spread over many CUs, 8 staged samples (and mixers) per thread
 constexpr int LB_T = 256;        // threads per workgroup: all four waves stage the tiles
 constexpr int LB_NS = 4;         // states (butter(4): 5 taps)
 
@@ -972,8 +1007,16 @@ __global__ __launch_bounds__(LB_T) void k_lfb_tile(const TIn *__restrict__ x, La
                                                     const double *__restrict__ states, double *__restrict__ ends,
                                                     double *__restrict__ out, Lay lo) {
     __shared__ double buf[LB_ST][LB_B + 1];
+    __shared__ int rch[LB_ST], rtile[LB_ST];   // the rows' channel and tile (one division per row)
     const int tid = threadIdx.x;
     const long ntiles = (long)2 * G.C * G.Tn;
+    const int nrow = (int)min((long)LB_ST, ntiles - (long)blockIdx.x * LB_ST);
+    if (tid < LB_ST) {
+        const int pr = (int)((((long)blockIdx.x * LB_ST + (tid < nrow ? tid : 0))) >> 1);
+        rtile[tid] = pr % G.Tn;
+        rch[tid] = pr / G.Tn;
+    }
+    __syncthreads();
     // cooperative load by all LB_T threads, 8 loads in flight per thread (unconditional, clamped),
     // then each element's value: lf_ext's arithmetic (mixer, odd extension) on the loaded samples
     constexpr int PER = LB_ST * LB_B / LB_T, U = 8;
@@ -981,12 +1024,11 @@ __global__ __launch_bounds__(LB_T) void k_lfb_tile(const TIn *__restrict__ x, La
     auto where = [&](int i, int &r, int &j, long &e, int &ch, int &comp, bool &in) {
         r = i / LB_B;
         j = i % LB_B;
-        const long g = (long)blockIdx.x * LB_ST + r;
-        in = g < ntiles;
-        const long gg = in ? g : 0;
-        comp = (int)(gg & 1);
-        const int tile = (int)((gg >> 1) % G.Tn);
-        ch = (int)((gg >> 1) / G.Tn);
+        in = r < nrow;
+        const int rr = in ? r : 0;
+        comp = rr & 1;   // LB_ST is even
+        const int tile = rtile[rr];
+        ch = rch[rr];
         e = (long)tile * LB_B + j;
         in = in && e < G.L;
         if (!in) e = 0;
@@ -1056,16 +1098,17 @@ __global__ __launch_bounds__(LB_T) void k_lfb_tile(const TIn *__restrict__ x, La
     for (int k = 0; k <= LB_NS; ++k) { f.bb[k] = b[k]; f.aa[k] = a[k]; }
 #pragma unroll
     for (int k = 0; k < LB_NS; ++k) f.z[k] = (FINAL && own) ? states[g * LB_NS + k] : 0.0;
-    for (int j0 = 0; j0 < len; j0 += 16) {
+    // every tile runs all LB_B steps: the last tile of a stream (len < LB_B) steps on the zeros past
+    // its end -- its end state is not used by the scan and its outputs past len are not stored
+    (void)len;
+    for (int j0 = 0; j0 < (tid < LB_ST ? LB_B : 0); j0 += 16) {   // wave 0 only (wave-uniform)
         double in[16];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) in[u] = buf[row][min(j0 + u, LB_B - 1)];
+        for (int u = 0; u < 16; ++u) in[u] = buf[row][j0 + u];
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
-            if (j0 + u < len) {
-                const double y = f.step(in[u]);
-                if (FINAL) buf[row][j0 + u] = y;
-            }
+            const double y = f.step(in[u]);
+            if (FINAL) buf[row][j0 + u] = y;
         }
     }
     if (!FINAL) {
@@ -1078,9 +1121,8 @@ __global__ __launch_bounds__(LB_T) void k_lfb_tile(const TIn *__restrict__ x, La
     __syncthreads();
     for (int i = tid; i < LB_ST * LB_B; i += LB_T) {
         const int r = i / LB_B, j = i % LB_B;
-        const long gg = (long)blockIdx.x * LB_ST + r;
-        if (gg >= ntiles) continue;
-        const int comp = (int)(gg & 1), tl = (int)((gg >> 1) % G.Tn), ch = (int)((gg >> 1) / G.Tn);
+        if (r >= nrow) continue;
+        const int comp = r & 1, tl = rtile[r], ch = rch[r];
         const long e = (long)tl * LB_B + j;
         if (e >= G.L) continue;
         if (FWD) {
@@ -1492,9 +1534,11 @@ __global__ __launch_bounds__(512) void k_extract_lat(const T *__restrict__ y, La
 }
 
 // ------------------------------------------------------------------ demodulate_dqpsk
-// One wave per channel.  sym rows [C][stride] complex T, S = nsym[ch] (or S_all).
-template <typename T>
-__global__ __launch_bounds__(64) void k_demod(const T *__restrict__ sym, long stride, int C, const int32_t *__restrict__ nsym,
+// sym rows [C][stride] complex T, S = nsym[ch] (or S_all).
+// BS threads per channel: 64 for batches (one wave per channel), 1024 in the latency mode (a few
+// channels: ~1 symbol per thread).  The max is order-independent, so the result is the same.
+template <typename T, int BS>
+__global__ __launch_bounds__(BS) void k_demod(const T *__restrict__ sym, long stride, int C, const int32_t *__restrict__ nsym,
                                               long S_all, double t0, double t1, double t2, double t3,
                                               uint8_t *__restrict__ hard, long hstride) {
     const int ch = blockIdx.x;
@@ -1505,13 +1549,28 @@ __global__ __launch_bounds__(64) void k_demod(const T *__restrict__ sym, long st
     const T *sp = sym + (size_t)ch * stride * 2;
     T m = (T)-INFINITY;
     bool any_nan = false;
-    for (long k = lane; k < S; k += 64) {
+    for (long k = lane; k < S; k += BS) {
         const T a = np_cabs(sp[2 * k], sp[2 * k + 1]);
         any_nan |= isnan(a);
         m = fmax(m, a);
     }
     for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
     any_nan = __any(any_nan);
+    if constexpr (BS > 64) {   // across the waves
+        __shared__ T wm[BS / 64];
+        __shared__ int wn[BS / 64];
+        if ((lane & 63) == 0) {
+            wm[lane >> 6] = m;
+            wn[lane >> 6] = any_nan;
+        }
+        __syncthreads();
+        m = wm[0];
+        any_nan = wn[0];
+        for (int w = 1; w < BS / 64; ++w) {
+            m = fmax(m, wm[w]);
+            any_nan |= wn[w] != 0;
+        }
+    }
     const T mx = any_nan ? (T)NAN : m;   // np.max propagates NaN
     // samples / max_power: numpy complex division (Smith) by (m + 0j): rat = 0/m, scl = 1/m,
     // out = ((xr + xi*rat)*scl, (xi - xr*rat)*scl)
@@ -1520,7 +1579,7 @@ __global__ __launch_bounds__(64) void k_demod(const T *__restrict__ sym, long st
     const T scl = norm ? (T)1 / (mx + (T)0 * rat) : (T)1;
     const T th0 = (T)t0, th1 = (T)t1, th2 = (T)t2, th3 = (T)t3;
     uint8_t *hp = hard + (size_t)ch * hstride;
-    for (long k = 1 + lane; k < S; k += 64) {
+    for (long k = 1 + lane; k < S; k += BS) {
         T sr = sp[2 * k], si = sp[2 * k + 1], pr = sp[2 * k - 2], pi = sp[2 * k - 1];
         if (norm) {
             const T a = (sr + si * rat) * scl, b = (si - sr * rat) * scl;
@@ -1653,7 +1712,7 @@ int run_decimate_blocked(tetra_ctx *ctx, const tetra_compat_plan *P, const T *x,
     HIP_TRY(ctx, hipMemcpyAsync(coef, hc, sizeof hc, hipMemcpyHostToDevice, ctx->stream));
     const SbGeo G{C, Tn, pad, P->q, N, L, Lp};
     constexpr int ST = SbCfg<T>::ST;
-    const dim3 gt((unsigned)ceil_div((long)ntile, ST)), bt(4 * ST);
+    const dim3 gt((unsigned)ceil_div((long)ntile, ST)), bt(SB_LT);
     const dim3 gs((unsigned)(2 * C)), bs((unsigned)std::min(SB_MAXT, (int)ceil_div(Tn, 64) * 64));
     {
         PROF(ctx, "compat_sosb_fwd");
@@ -1768,8 +1827,12 @@ template <typename T>
 void launch_demod(tetra_ctx *ctx, const T *sym, long stride, int C, const int32_t *nsym, long S_all,
                   const double *thr, uint8_t *hard, long hstride) {
     PROF(ctx, "compat_demod");
-    hipLaunchKernelGGL(k_demod<T>, dim3(C), dim3(64), 0, ctx->stream, sym, stride, C, nsym, S_all, thr[0], thr[1],
-                       thr[2], thr[3], hard, hstride);
+    if (C <= SB_MAXC)   // a few channels: a workgroup of 1024 per channel
+        hipLaunchKernelGGL((k_demod<T, 1024>), dim3(C), dim3(1024), 0, ctx->stream, sym, stride, C, nsym, S_all, thr[0],
+                           thr[1], thr[2], thr[3], hard, hstride);
+    else
+        hipLaunchKernelGGL((k_demod<T, 64>), dim3(C), dim3(64), 0, ctx->stream, sym, stride, C, nsym, S_all, thr[0], thr[1],
+                           thr[2], thr[3], hard, hstride);
 }
 
 int check_plan(tetra_ctx *ctx, const tetra_compat_plan *P) {
