@@ -64,6 +64,9 @@ struct tetra_ctx {
     std::vector<double> sosb_tab;      // compat time-blocked decimator: Phi^(2^r) table as last uploaded
     int sosb_key = -1;                 // ... for this (q, precision)
     const void *sosb_dev = nullptr;    // ... to this address (slot S_W16)
+    void *pin = nullptr;               // pinned host arena: small staged copies go through it (Staging)
+    size_t pin_cap = 0;
+    bool pin_busy = false;             // a copy through the arena may still be in flight
 };
 
 extern thread_local std::string g_tetra_err;
@@ -84,14 +87,24 @@ bool is_device_ptr(const void *p);
 
 // Host/device argument staging.  `in` returns a device pointer holding the bytes of p;
 // `out` returns a device pointer whose contents are copied back to p by finish().
+// Host arguments of up to PIN_SMALL bytes are staged through the context's pinned arena (an async
+// copy, and one memcpy on the host), larger ones copied from/to the caller's pageable memory.
+constexpr size_t PIN_SMALL = 128 << 10, PIN_ARENA = 1 << 20;
 struct Staging {
     tetra_ctx *ctx;
     int next_in = S_IN0, next_out = S_OUT0;
-    struct Back { void *host; const void *dev; size_t bytes; };
+    struct Back { void *host; const void *dev; size_t bytes; void *pin; };
     std::vector<Back> back;
+    size_t pin_off = 0;
     bool host_touched = false;
     bool failed = false;
-    explicit Staging(tetra_ctx *c) : ctx(c) {}
+    explicit Staging(tetra_ctx *c) : ctx(c) {
+        if (ctx && ctx->pin_busy) {   // an earlier call left the arena (an error path skipped finish)
+            (void)hipStreamSynchronize(ctx->stream);
+            ctx->pin_busy = false;
+        }
+    }
+    void *pin_take(size_t bytes);   // 256-B aligned arena space, nullptr if none
     const void *in(const void *p, size_t bytes);
     void *out(void *p, size_t bytes);
     void *inout(void *p, size_t bytes);   // `in` + `out` on one buffer (host contents uploaded first)

@@ -47,13 +47,32 @@ bool is_device_ptr(const void *p) {
     return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
 }
 
+void *Staging::pin_take(size_t bytes) {
+    if (bytes > PIN_SMALL) return nullptr;
+    if (!ctx->pin) {
+        if (hipHostMalloc(&ctx->pin, PIN_ARENA) != hipSuccess) {
+            (void)hipGetLastError();
+            ctx->pin = nullptr;
+            return nullptr;
+        }
+        ctx->pin_cap = PIN_ARENA;
+    }
+    const size_t at = (pin_off + 255) & ~(size_t)255;
+    if (at + bytes > ctx->pin_cap) return nullptr;
+    pin_off = at + bytes;
+    ctx->pin_busy = true;
+    return (char *)ctx->pin + at;
+}
+
 const void *Staging::in(const void *p, size_t bytes) {
     if (failed) return nullptr;
     if (bytes == 0) return p ? p : ws(ctx, next_in++, 16);
     if (is_device_ptr(p)) return p;
     host_touched = true;
     void *d = ws(ctx, next_in++, bytes);
-    if (!d || hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) {
+    void *h = d ? pin_take(bytes) : nullptr;
+    if (h) memcpy(h, p, bytes);
+    if (!d || hipMemcpyAsync(d, h ? h : p, bytes, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) {
         failed = true;
         if (d) tetra_fail(ctx, TETRA_E_HIP, "H2D staging copy failed");
         return nullptr;
@@ -71,7 +90,7 @@ void *Staging::out(void *p, size_t bytes) {
         failed = true;
         return nullptr;
     }
-    back.push_back({p, d, bytes});
+    back.push_back({p, d, bytes, pin_take(bytes)});
     return d;
 }
 
@@ -92,8 +111,11 @@ int Staging::finish() {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return tetra_fail(ctx, TETRA_E_HIP, "kernel launch failed: %s", hipGetErrorString(e));
     for (auto &b : back)
-        HIP_TRY(ctx, hipMemcpyAsync(b.host, b.dev, b.bytes, hipMemcpyDeviceToHost, ctx->stream));
-    if (host_touched) HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(b.pin ? b.pin : b.host, b.dev, b.bytes, hipMemcpyDeviceToHost, ctx->stream));
+    if (host_touched || ctx->pin_busy) HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (auto &b : back)
+        if (b.pin) memcpy(b.host, b.pin, b.bytes);
+    ctx->pin_busy = false;
     return TETRA_OK;
 }
 
@@ -209,6 +231,7 @@ void tetra_destroy(tetra_ctx *ctx) {
     if (ctx->fft && ctx->fft_free) ctx->fft_free(ctx->fft);
     for (auto &b : ctx->slot)
         if (b.p) (void)hipFree(b.p);
+    if (ctx->pin) (void)hipHostFree(ctx->pin);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

@@ -96,13 +96,23 @@ def _fill(arr, vals):
 DECIMATORS = {"auto": 0, "sequential": _hip.COMPAT_SEQUENTIAL, "blocked": _hip.COMPAT_BLOCKED}
 
 
+_PLANS = {}   # compat_plan results of the warning-free cases (the GUI's repeated chunk shape)
+
+
 def compat_plan(sample_rate, n, fmt, bandwidth=25000, decimator="auto"):
     """Build the device plan for process() on n samples (processor.py:239-273 decisions).
+    Plans of calls that log nothing are cached by their arguments (~40 us of filter design per
+    chunk otherwise); the plan is read-only to the library.
 
     ``decimator`` picks the form of decimate's sosfiltfilt (include/tetra_hip.h, TETRA_COMPAT_*):
     "sequential" is scipy's operation order, bit-identical to the reference; "blocked" recurses
     256-sample tiles in parallel (latency mode, within the filter's fp32 noise of scipy); "auto"
     lets tetra_demod_compat take the blocked form for batches of <= 64 channels at q <= 16."""
+    key = (float(sample_rate), int(n), int(fmt), bandwidth, decimator)
+    hit = _PLANS.get(key)
+    if hit is not None:
+        return hit
+    warned = False
     p = _hip.CompatPlan()
     p.flags = DECIMATORS[decimator]
     rate = sample_rate
@@ -114,6 +124,7 @@ def compat_plan(sample_rate, n, fmt, bandwidth=25000, decimator="auto"):
                 p.q = q
                 rate = rate / q
             else:
+                warned = True
                 logger.warning("Decimation failed: The length of the input vector x must be greater "
                                "than padlen, which is 27.")
     m = -(-n // p.q) if p.q > 1 else n
@@ -128,6 +139,7 @@ def compat_plan(sample_rate, n, fmt, bandwidth=25000, decimator="auto"):
     p.ntaps = len(b)
     p.filt = int(m > 3 * max(len(a), len(b)))
     if not p.filt:
+        warned = True
         logger.warning("Filter design failed, using unfiltered samples: The length of the input vector x "
                        "must be greater than padlen, which is %d.", 3 * max(len(a), len(b)))
     _fill(p.b, b)
@@ -138,6 +150,10 @@ def compat_plan(sample_rate, n, fmt, bandwidth=25000, decimator="auto"):
     p.phase_step = max(1, sps // 8) if sps > 1 else 1
     p.fs_dec = rate
     _fill(p.thr, THRESHOLDS)
+    if not warned:
+        if len(_PLANS) >= 64:
+            _PLANS.clear()
+        _PLANS[key] = (p, m, rate)
     return p, m, rate
 
 
