@@ -754,14 +754,14 @@ __global__ __launch_bounds__(1024) void k_sosb_scan(const T *__restrict__ x, con
         __syncthreads();
         if (upd) {
             const double *P = ph + r * 64;
+            // the eight rows' sums side by side (each still j-ascending, no FMA: the same bits), then
+            // the new state to LDS
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                double acc = v[i];
+            for (int j = 0; j < 8; ++j)
 #pragma unroll
-                for (int j = 0; j < 8; ++j) acc = acc + P[i * 8 + j] * u[j];
-                v[i] = acc;
-                w[k][i] = acc;
-            }
+                for (int i = 0; i < 8; ++i) v[i] = v[i] + P[i * 8 + j] * u[j];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) w[k][i] = v[i];
         }
     }
     if (on) {
