@@ -14,9 +14,10 @@
  *   - Every entry point returns 0 on success or a negative TETRA_E* code; nothing aborts.
  *     tetra_last_error() returns the message of the last failure on that context.
  *   - Array arguments may be HOST or DEVICE pointers (the library asks HIP which); host arrays
- *     are staged through context-owned device buffers.  Calls with device arguments enqueue on
- *     the context's stream and return without waiting; calls that touch host memory return
- *     after their results are in host memory.
+ *     are staged through context-owned device buffers (those of up to 128 KB through a pinned
+ *     host arena of the context, as async copies).  Calls with device arguments enqueue on the
+ *     context's stream and return without waiting; calls that touch host memory return after
+ *     their results are in host memory.
  *   - Complex arrays are interleaved (re, im).  "cf32" = complex64, "cf64" = complex128.
  *   - One context per host thread; a context is not thread-safe.  No allocation happens on a
  *     repeat call with sizes no larger than a previous call (workspaces are cached).
