@@ -94,6 +94,27 @@ def test_compat_plan_decisions(g1):
             assert bool(p.filt) == (z[f"c{i}_filtered"].dtype == np.complex128), (i, m)
 
 
+def test_compat_plan_real_input_state_and_private_plans():
+    """decimate casts its sos to the input's dtype, so a real chunk's initial state comes from the
+    real dtype (at q = 7 float32 and complex64 differ in a last bit; the plan carries the one scipy
+    would use, as the oracle's decimate does).  filter_signal rewrites its plan's taps, so it gets a
+    private plan: the cached one process() reuses for the same chunk shape keeps its own taps."""
+    import scipy.signal as ss
+    from tetraear.signal.processor import compat_plan
+    from tetraear import _hip
+    sos = ss.cheby1(8, 0.05, 0.8 / 7, output="sos")
+    for real, t in ((False, np.complex64), (True, np.float32)):
+        p, _, _ = compat_plan(1.8e6, 22849, _hip.TETRA_CF32, real=real)
+        want = ss.sosfilt_zi(np.asarray(sos, t)).real.astype(np.float32).ravel()
+        assert np.array_equal(np.ctypeslib.as_array(p.zi_f32)[:8], want), real
+    a, _, _ = compat_plan(2.4e6, 5000, _hip.TETRA_CF32)
+    b, _, _ = compat_plan(2.4e6, 5000, _hip.TETRA_CF32, cache=False)
+    assert a is compat_plan(2.4e6, 5000, _hip.TETRA_CF32)[0] and b is not a
+    taps = np.ctypeslib.as_array(a.b)[:5].copy()
+    b.b[0] = 123.0
+    assert np.array_equal(np.ctypeslib.as_array(compat_plan(2.4e6, 5000, _hip.TETRA_CF32)[0].b)[:5], taps)
+
+
 def test_mode_selection_from_environment(monkeypatch):
     """TETRAEAR_DEMOD picks the chain for callers that construct SignalProcessor / TetraDecoder as
     the reference's GUI and scanner do (modern.py:1886-1887, scanner.py:164-172); an explicit mode=

@@ -105,6 +105,24 @@ def test_direct_method_calls(hip, g1):
     assert len(p.filter_signal(np.array([]))) == 0
 
 
+@pytest.mark.parametrize("decimator", ["sequential", "auto"])
+def test_real_input_and_direct_calls_before_process(hip, decimator):
+    """Real float32 chunks at 1.8 MSps (q = 7, where decimate's float32 and complex64 initial
+    states differ in a last bit) equal the oracle's -- after filter_signal ran on a chunk of the same
+    length and rate (it must not leave its taps in the plan process() reuses)."""
+    from tetraear.signal import SignalProcessor
+    rng = np.random.default_rng(77)
+    x = (0.4 * rng.standard_normal(22849)).astype(np.float32)
+    p = SignalProcessor(1.8e6, decimator=decimator)
+    p.filter_signal(x)   # 1.8 MSps taps, same chunk length as the process() call below
+    h = p.process(x)
+    o = O.SignalProcessor(1.8e6, decimator=decimator)
+    ho = o.process(x)
+    assert p.symbols.dtype == o.symbols.dtype and len(p.symbols) == len(o.symbols)
+    assert np.max(np.abs(p.symbols - o.symbols)) <= SOFT_TOL
+    _hard_equal(h, ho, o.symbols)
+
+
 def test_process_batch_equals_per_channel(hip):
     from tetraear.signal import SignalProcessor
     rng = np.random.default_rng(3)

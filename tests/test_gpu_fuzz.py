@@ -1,0 +1,175 @@
+"""Seeded random-geometry parity sweep (GPU through the C ABI vs the CPU oracle).
+
+The other GPU tests pin chosen geometries; this sweep draws the ones nobody chose -- channel counts,
+chunk lengths, sample rates, offsets, SNRs, input formats -- from fixed seeds, so a failure names a
+reproducible case.  Bars are the same as the focused tests: compat soft symbols within 1e-5 and
+hard decisions bit-exact outside the 1e-9 rad tie band (test_gpu_compat.py); the ETSI chain bit-exact
+(symbols, soft bits, hard dibits, burst positions, decoded bits and CRC flags).
+"""
+import numpy as np
+import pytest
+
+import compat as O
+import etsi as E
+from test_gpu_compat import SOFT_TOL, _hard_equal
+
+pytestmark = pytest.mark.gpu
+
+# reference rates: process() decimates by int(fs / 240e3) above 480 kHz (processor.py:245-256),
+# so these reach q = 1 (no decimation), 4, 7, 8, 10, 13 and 41
+COMPAT_RATES = [240e3, 1.0e6, 1.8e6, 2.0e6, 2.4e6, 3.2e6, 10e6]
+ETSI_RATES = [1.8e6, 1.9e6, 2.0e6, 2.1e6, 2.2e6, 2.3e6, 2.4e6]
+
+
+def _compat_case(seed):
+    rng = np.random.default_rng(1000 + seed)
+    fs = COMPAT_RATES[seed % len(COMPAT_RATES)]
+    C = int(rng.integers(1, 6))
+    tiny = rng.uniform() < 0.3   # around decimate's and filtfilt's padlen (27 and 15 samples)
+    N = int(rng.integers(1, 500 if tiny else (60000 if fs < 5e6 else 200000)))
+    decimator = ("sequential", "auto")[int(rng.integers(0, 2))]
+    dtype = (np.complex64, np.complex128, np.float32)[int(rng.integers(0, 3))]
+    fo = [float(rng.choice([0.0, rng.uniform(-4000, 4000)])) for _ in range(C)]
+    if rng.uniform() < 0.3:
+        fo = [0.0] * C
+    return rng, fs, C, N, decimator, dtype, fo
+
+
+@pytest.mark.parametrize("seed", range(42))
+def test_compat_random_geometry_vs_oracle(seed):
+    from tetraear.signal import SignalProcessor
+    rng, fs, C, N, decimator, dtype, fo = _compat_case(seed)
+    x = rng.uniform(0.05, 1.0) * (rng.standard_normal((C, N)) + 1j * rng.standard_normal((C, N)))
+    x = (x.real if dtype == np.float32 else x).astype(dtype)   # real input: the reference accepts it too
+    hard, soft, ns = SignalProcessor(fs, decimator=decimator).process_batch(x, fo)
+    for c in range(C):
+        o = O.SignalProcessor(fs, decimator=decimator)
+        h = o.process(x[c], fo[c])
+        case = (seed, fs, C, N, decimator, dtype.__name__, c)
+        assert ns[c] == len(o.symbols), case
+        if ns[c]:
+            assert np.max(np.abs(soft[c, :ns[c]] - o.symbols)) <= SOFT_TOL, case
+        _hard_equal(hard[c, :max(int(ns[c]) - 1, 0)], h, o.symbols)
+    # one channel again through process(): the single-channel (latency) entry agrees with the batch
+    p = SignalProcessor(fs, decimator=decimator)
+    h1 = p.process(x[0], fo[0])
+    assert len(p.symbols) == ns[0]
+    if ns[0]:
+        assert np.max(np.abs(p.symbols - soft[0, :ns[0]])) <= SOFT_TOL
+    o = O.SignalProcessor(fs, decimator=decimator)
+    _hard_equal(h1, o.process(x[0], fo[0]), o.symbols)
+
+
+@pytest.mark.parametrize("seed", range(42))
+def test_etsi_random_geometry_vs_oracle(seed):
+    from tetraear.signal.etsi import EtsiReceiver, synth
+    from tetraear.core.etsi import EtsiLowerMac
+    rng = np.random.default_rng(2000 + seed)
+    fs = ETSI_RATES[seed % len(ETSI_RATES)]
+    C = int(rng.integers(1, 9))
+    N = int(rng.integers(2, 6000 if rng.uniform() < 0.25 else 150000))
+    snr = float(rng.uniform(4.0, 24.0))
+    cfo = float(rng.uniform(0.0, 700.0))
+    sc16 = bool(rng.integers(0, 2))
+    iq, cells = synth(C, 150000, fs=fs, seed=3000 + seed, snr_db=snr, cfo_max=cfo)[:2]
+    iq = iq[:, :N]
+    inp = iq
+    if sc16:
+        inp = np.stack([np.rint(iq.real * 32768), np.rint(iq.imag * 32768)], -1).clip(-32768, 32767).astype(np.int16)
+        iq = (inp[..., 0].astype(np.float32) / 32768 + 1j * (inp[..., 1].astype(np.float32) / 32768)).astype(np.complex64)
+    hard, soft, sym, ns = EtsiReceiver(fs).demod_batch(inp)
+    rx = E.Receiver(fs)
+    Ne = N - N % 2
+    case = (seed, fs, C, N, round(snr, 1), round(cfo), "sc16" if sc16 else "cf32")
+    for ch in range(C):
+        so, sbo, ho, _ = rx.demod(iq[ch, :Ne])
+        n = int(ns[ch])
+        assert n == len(so), case + (ch,)
+        assert np.array_equal(sym[ch, :n], so) and np.array_equal(hard[ch, :max(n - 1, 0)], ho), case + (ch,)
+        assert np.array_equal(soft[ch, :2 * max(n - 1, 0)], sbo), case + (ch,)
+    res = EtsiLowerMac().decode_batch(soft, hard, ns, cells)
+    for ch in range(C):
+        n = int(ns[ch])
+        if n < 2:
+            assert res[ch] == [], case + (ch,)
+            continue
+        want = rx.lower_mac(soft[ch, :2 * (n - 1)], hard[ch, :n - 1], int(cells[ch]))
+        got = res[ch]
+        assert [(f["position"], f["burst_kind"]) for f in got] == [(s, k) for s, k, _ in want], case + (ch,)
+        for f, (_, _, dec) in zip(got, want):
+            assert len(f["blocks"]) == len(dec), case + (ch,)
+            for b, (kind, bits, ok) in zip(f["blocks"], dec):
+                assert b["crc_ok"] == ok and np.array_equal(b["bits"], bits), case + (ch,)
+
+
+def _crc_burst_data(rng, fixed_tail):
+    """216 type-2 burst data bits whose CRC-16 (the last 16) checks, with data[202:216] = fixed_tail
+    (the sync bits the CRC field overlaps in a normal burst): data[0:16] solved over GF(2), the CRC
+    being affine in its input."""
+    d = rng.integers(0, 2, 216).astype(np.int64)
+    d[202:216] = fixed_tail
+    target = d[200:216].copy()
+    d[:16] = 0
+    c0 = O.calculate_crc16(np.zeros(200, np.int64))
+    base = O.calculate_crc16(d[:200]) ^ target
+    L = np.zeros((16, 16), np.int64)
+    for i in range(16):
+        e = np.zeros(200, np.int64)
+        e[i] = 1
+        L[:, i] = O.calculate_crc16(e) ^ c0
+    # solve L x = base over GF(2) (Gauss-Jordan); L is invertible for 16 consecutive input bits
+    A = np.concatenate([L, base[:, None]], 1) % 2
+    for col in range(16):
+        piv = col + int(np.argmax(A[col:, col]))
+        assert A[piv, col] == 1
+        A[[col, piv]] = A[[piv, col]]
+        for r in range(16):
+            if r != col and A[r, col]:
+                A[r] ^= A[col]
+    d[:16] = A[:, 16]
+    assert O.check_crc(d)
+    return d
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_decoder_random_streams_vs_oracle(seed):
+    """Random symbol streams with bursts placed at random bit offsets: syncs with 0-4 bit errors,
+    burst CRCs valid or 1-4 bits off (the reference accepts <= 2), both symbol alphabets -- the
+    frames decode() keeps and their MAC PDU fields equal the oracle's decode_with_mac."""
+    import mac as M
+    from conftest import decoded_view
+    from tetraear.core import TetraDecoder
+    rng = np.random.default_rng(4000 + seed)
+    nb = int(rng.integers(0, 12))
+    nbits = int(rng.integers(600, 700 * max(nb, 1) + 600))
+    bits = rng.integers(0, 2, nbits).astype(np.int64)
+    at = 0
+    for _ in range(nb):
+        start = at + int(rng.integers(0, 120))
+        if start + 510 > nbits:
+            break
+        if rng.uniform() < 0.8:
+            start -= start % 2   # symbol-aligned (the slot parse reads whole symbols)
+        sync = (O.SYNC_CONT if rng.uniform() < 0.5 else O.SYNC_DISC).astype(np.int64).copy()
+        burst = rng.integers(0, 2, 510).astype(np.int64)
+        data = _crc_burst_data(rng, sync[:14])
+        burst[0:108], burst[122:230] = data[:108], data[108:]
+        for i in rng.choice(216, size=int(rng.choice([0, 0, 0, 1, 2, 3, 4])), replace=False):
+            j = i if i < 108 else i + 14
+            burst[j] ^= 1   # CRC errors: <= 2 still pass (compat_oracle.c orc_check_crc)
+        burst[216:238] = sync
+        for i in rng.choice(22, size=int(rng.choice([0, 0, 1, 2, 3, 4])), replace=False):
+            burst[216 + i] ^= 1   # sync bit errors: the decoder's 0.90 / 0.85 / 0.80 / adaptive cascade
+        bits[start:start + 510] = burst
+        at = start + 510
+    bits = bits[:nbits - nbits % 2]
+    sym = (2 * bits[0::2] + bits[1::2]).astype(np.uint8)
+    if rng.uniform() < 0.15:   # the 8-PSK alphabet branch of symbols_to_bits (decoder.py:150-160)
+        sym = rng.integers(0, 8, len(sym)).astype(np.uint8)
+    d = TetraDecoder(auto_decrypt=False)
+    got = [decoded_view(f) for f in d.decode(sym)]
+    mp = M.MacParser()
+    want = O.decode_with_mac(sym, mp)
+    assert got == want, (seed, nb, nbits)
+    st = d.protocol_parser.stats
+    assert (st["clear_mode_frames"], st["encrypted_frames"]) == (mp.n_clear, mp.n_enc), seed

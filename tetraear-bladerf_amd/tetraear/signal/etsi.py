@@ -124,12 +124,16 @@ class EtsiReceiver:
         if N % 2:
             x = np.ascontiguousarray(x[:, :N - 1])
             N -= 1
-        _, _, smax = lengths(self.plan, N)
+        _, M2, smax = lengths(self.plan, N)
+        smax = max(smax, 1)
         sym = np.zeros((C, smax), np.complex64)
         soft = np.zeros((C, 2 * smax), np.int8)
         hard = np.zeros((C, smax), np.uint8)
         ns = np.zeros(C, np.int32)
         diag = np.zeros((C, 4), np.float32)
+        if C == 0 or M2 <= 0:   # shorter than the channel filter: no symbols in any channel (as process())
+            self.diag = diag
+            return hard, soft, sym, ns
         c = _hip.ctx()
         c.check(c.lib.tetra_demod_etsi_fmt(c.handle, self.plan, _hip.ptr(x), fmt, C, N, _hip.ptr(sym),
                                            _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(ns), smax, _hip.ptr(diag)),

@@ -69,11 +69,14 @@ def _as_complex(x, fmt):
 
 
 @functools.lru_cache(maxsize=64)
-def _decimator_design(q):
-    """scipy.signal.decimate's filter (ftype='iir', n=8) in both working precisions."""
+def _decimator_design(q, real=False):
+    """scipy.signal.decimate's filter (ftype='iir', n=8) in both working precisions.  decimate casts
+    the sos to the input's dtype (scipy _signaltools.decimate) and sosfiltfilt derives its initial
+    state from that array, so a real input's state comes from the real dtype: at q = 7 the float32
+    and complex64 sosfilt_zi differ in one element's last bit."""
     sos = _design.cheby1(8, 0.05, 0.8 / q, output="sos")
     out = {}
-    for name, t in (("f32", np.complex64), ("f64", np.complex128)):
+    for name, t in (("f32", np.float32 if real else np.complex64), ("f64", np.float64 if real else np.complex128)):
         s = np.asarray(sos, dtype=t)
         out[name] = (s.real.copy(), _design.sosfilt_zi(s).real.copy())
     return out
@@ -99,7 +102,7 @@ DECIMATORS = {"auto": 0, "sequential": _hip.COMPAT_SEQUENTIAL, "blocked": _hip.C
 _PLANS = {}   # compat_plan results of the warning-free cases (the GUI's repeated chunk shape)
 
 
-def compat_plan(sample_rate, n, fmt, bandwidth=25000, decimator="auto"):
+def compat_plan(sample_rate, n, fmt, bandwidth=25000, decimator="auto", real=False, cache=True):
     """Build the device plan for process() on n samples (processor.py:239-273 decisions).
     Plans of calls that log nothing are cached by their arguments (~40 us of filter design per
     chunk otherwise); the plan is read-only to the library.
@@ -107,9 +110,11 @@ def compat_plan(sample_rate, n, fmt, bandwidth=25000, decimator="auto"):
     ``decimator`` picks the form of decimate's sosfiltfilt (include/tetra_hip.h, TETRA_COMPAT_*):
     "sequential" is scipy's operation order, bit-identical to the reference; "blocked" recurses
     256-sample tiles in parallel (latency mode, within the filter's fp32 noise of scipy); "auto"
-    lets tetra_demod_compat take the blocked form for batches of <= 64 channels at q <= 16."""
-    key = (float(sample_rate), int(n), int(fmt), bandwidth, decimator)
-    hit = _PLANS.get(key)
+    lets tetra_demod_compat take the blocked form for batches of <= 64 channels at q <= 16.
+    ``real``: the samples are real (decimate's initial state in the real dtype).  ``cache=False``
+    returns a private plan the caller may modify."""
+    key = (float(sample_rate), int(n), int(fmt), bandwidth, decimator, bool(real))
+    hit = _PLANS.get(key) if cache else None
     if hit is not None:
         return hit
     warned = False
@@ -130,7 +135,7 @@ def compat_plan(sample_rate, n, fmt, bandwidth=25000, decimator="auto"):
     m = -(-n // p.q) if p.q > 1 else n
     p.dec_f64 = int(fmt == _hip.TETRA_CF64)
     if p.q > 1:
-        d = _decimator_design(p.q)
+        d = _decimator_design(p.q, bool(real))
         _fill(p.sos_f32, d["f32"][0])
         _fill(p.zi_f32, d["f32"][1])
         _fill(p.sos_f64, d["f64"][0])
@@ -150,7 +155,7 @@ def compat_plan(sample_rate, n, fmt, bandwidth=25000, decimator="auto"):
     p.phase_step = max(1, sps // 8) if sps > 1 else 1
     p.fs_dec = rate
     _fill(p.thr, THRESHOLDS)
-    if not warned:
+    if not warned and cache:
         if len(_PLANS) >= 64:
             _PLANS.clear()
         _PLANS[key] = (p, m, rate)
@@ -223,7 +228,7 @@ class SignalProcessor:
         except Exception as e:
             logger.warning(f"Filter design failed, using unfiltered samples: {e}")
             return samples
-        p, _, _ = compat_plan(fs, len(x), _fmt_of(x), bandwidth)
+        p, _, _ = compat_plan(fs, len(x), _fmt_of(x), bandwidth, cache=False)   # its taps are replaced below
         _fill(p.b, b)
         _fill(p.a, a)
         _fill(p.lzi, zi)
@@ -316,7 +321,7 @@ class SignalProcessor:
         real_in = not np.iscomplexobj(x)
         fmt = _fmt_of(x)
         xc = _as_complex(x, fmt)
-        plan, m, _ = compat_plan(self.sample_rate, len(x), fmt, decimator=self.decimator)
+        plan, m, _ = compat_plan(self.sample_rate, len(x), fmt, decimator=self.decimator, real=real_in)
         smax = m // plan.sps + 1
         soft = np.empty(smax, np.complex128)
         hard = np.empty(smax, np.uint8)
@@ -355,13 +360,15 @@ class SignalProcessor:
         afc = isinstance(freq_offsets, str)
         if afc and freq_offsets != "afc":
             raise ValueError("freq_offsets must be None, an array of Hz, a device tensor or 'afc'")
+        real_in = False
         if hasattr(x, "data_ptr"):
             fmt = _tensor_fmt(x)
             xc = x.contiguous()
         else:
             fmt = _fmt_of(x)
+            real_in = not np.iscomplexobj(x)
             xc = _as_complex(x, fmt)
-        plan, m, _ = compat_plan(self.sample_rate, N, fmt, decimator=self.decimator)
+        plan, m, _ = compat_plan(self.sample_rate, N, fmt, decimator=self.decimator, real=real_in)
         smax = m // plan.sps + 1
         soft = np.empty((C, smax), np.complex128)
         hard = np.empty((C, smax), np.uint8)
@@ -388,11 +395,47 @@ class SignalProcessor:
             fo = np.zeros(C) if freq_offsets is None else np.asarray(freq_offsets, np.float64)
             mc = np.array([mixer_coefficient(f) if f != 0 else 0.0 for f in fo], np.float64)
             mo = (fo != 0).astype(np.uint8)
+        if not plan.filt:
+            # a chunk too short for filtfilt (processor.py:81-83 returns it unfiltered): the library
+            # takes such a batch only with the mixer on for all channels or for none, so a mixed
+            # batch runs as those two batches
+            on = (mo.cpu().numpy() if hasattr(mo, "data_ptr") else mo).astype(bool)
+            if on.any() and not on.all():
+                mc_h = mc.cpu().numpy() if hasattr(mc, "data_ptr") else mc
+                for rows in (np.flatnonzero(on), np.flatnonzero(~on)):
+                    h, s, n = self._compat_rows(plan, xc, fmt, rows, mc_h[rows], on[rows], smax)
+                    hard[rows], soft[rows], ns[rows] = h, s, n
+                if gate is not None:
+                    self.gate = {k: v.cpu().numpy() for k, v in gate.items()}
+                return hard, soft, ns
         c.check(c.lib.tetra_demod_compat(c.handle, plan, _hip.ptr(xc), fmt, C, N, _hip.ptr(mc), _hip.ptr(mo),
                                          _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(ns), smax, f32),
                 "tetra_demod_compat")
+        if f32.value:   # unfiltered cf32 without the mixer: complex64 symbols, rows smax apart
+            soft = soft.reshape(-1).view(np.complex64)[:C * smax].reshape(C, smax).astype(np.complex128)
         if gate is not None:
             self.gate = {k: v.cpu().numpy() for k, v in gate.items()}
+        return hard, soft, ns
+
+    def _compat_rows(self, plan, xc, fmt, rows, mc, on, smax):
+        """tetra_demod_compat over the channels ``rows`` of ``xc`` (host or device), mixer
+        coefficients ``mc`` and flags ``on`` (all set or all clear); symbols returned as complex128."""
+        xs = xc[rows.tolist()] if hasattr(xc, "data_ptr") else np.ascontiguousarray(xc[rows])
+        if hasattr(xs, "data_ptr"):
+            xs = xs.contiguous()
+        R, N = len(rows), xs.shape[1]
+        mc = np.ascontiguousarray(mc, np.float64)
+        mo = np.ascontiguousarray(on, np.uint8)
+        soft = np.empty((R, smax), np.complex128)
+        hard = np.empty((R, smax), np.uint8)
+        ns = np.zeros(R, np.int32)
+        f32 = ctypes_int()
+        c = _hip.ctx()
+        c.check(c.lib.tetra_demod_compat(c.handle, plan, _hip.ptr(xs), fmt, R, N, _hip.ptr(mc), _hip.ptr(mo),
+                                         _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(ns), smax, f32),
+                "tetra_demod_compat")
+        if f32.value:
+            soft = soft.reshape(-1).view(np.complex64)[:R * smax].reshape(R, smax).astype(np.complex128)
         return hard, soft, ns
 
     def _etsi_rx(self):
