@@ -45,6 +45,9 @@ enum {
 /* Sample formats of input arrays.  TETRA_SC16: interleaved int16 (I, Q), the BladeRF wire format,
  * scaled by 1/32768 as capture.py:241-269 does (exact in fp32); ETSI channel filter only. */
 enum { TETRA_CF32 = 0, TETRA_CF64 = 1, TETRA_SC16 = 2 };
+/* Real samples (float32 / float64), taken only by tetra_demod_dqpsk: the reference's
+ * demodulate_dqpsk on a real array (processor.py:124-140 with real scalars). */
+enum { TETRA_F32 = 3, TETRA_F64 = 4 };
 
 typedef struct tetra_ctx tetra_ctx;
 
@@ -145,7 +148,8 @@ int tetra_filtfilt(tetra_ctx *ctx, const tetra_compat_plan *plan, const void *iq
 /* extract_symbols (processor.py:168-219): sym [C][smax] in iq_fmt, nsym [C], best phase [C]. */
 int tetra_extract_symbols(tetra_ctx *ctx, const void *x, int fmt, size_t C, size_t N, int sps,
                           int phase_step, void *sym, int32_t *nsym, int32_t *best_phase, size_t smax);
-/* demodulate_dqpsk (processor.py:102-166): hard [C][S-1] for C rows of S symbols. */
+/* demodulate_dqpsk (processor.py:102-166): hard [C][S-1] for C rows of S symbols in TETRA_CF32 /
+ * TETRA_CF64, or real rows in TETRA_F32 / TETRA_F64. */
 int tetra_demod_dqpsk(tetra_ctx *ctx, const void *sym, int fmt, size_t C, size_t S,
                       const double *thr4, uint8_t *hard);
 

@@ -41,6 +41,8 @@ def test_compat_random_geometry_vs_oracle(seed):
     rng, fs, C, N, decimator, dtype, fo = _compat_case(seed)
     x = rng.uniform(0.05, 1.0) * (rng.standard_normal((C, N)) + 1j * rng.standard_normal((C, N)))
     x = (x.real if dtype == np.float32 else x).astype(dtype)   # real input: the reference accepts it too
+    if rng.uniform() < 0.15 and N:
+        x[:, rng.integers(0, N, size=max(1, N // 9))] = 0   # exact zeros: signed-zero products in the decision
     hard, soft, ns = SignalProcessor(fs, decimator=decimator).process_batch(x, fo)
     for c in range(C):
         o = O.SignalProcessor(fs, decimator=decimator)
@@ -173,3 +175,74 @@ def test_decoder_random_streams_vs_oracle(seed):
     assert got == want, (seed, nb, nbits)
     st = d.protocol_parser.stats
     assert (st["clear_mode_frames"], st["encrypted_frames"]) == (mp.n_clear, mp.n_enc), seed
+
+
+_DTYPES = (np.complex64, np.complex128, np.float32, np.float64)
+
+
+def _rand_samples(rng, n, dtype):
+    x = rng.uniform(0.01, 3.0) * (rng.standard_normal(n) + 1j * rng.standard_normal(n))
+    if rng.uniform() < 0.1 and n:
+        x[rng.integers(0, n, size=max(1, n // 7))] = 0   # exact zeros (|x| = 0, angle 0)
+    return (x if np.dtype(dtype).kind == "c" else x.real).astype(dtype)
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_direct_methods_random_vs_oracle(seed):
+    """The reference's SignalProcessor methods called directly (as modern.py / the tools do) on
+    random lengths, rates, bandwidths and all four sample dtypes: filter_signal bit-exact (fp64
+    DF-II-T, no libm), extract_symbols bit-exact, frequency_shift within 1e-12 (libm sin/cos),
+    demodulate_dqpsk bit-exact outside the tie band -- each with the oracle's output dtype."""
+    from tetraear.signal import SignalProcessor
+    rng = np.random.default_rng(5000 + seed)
+    fs = float(rng.choice([240e3, 1.0e6, 1.8e6, 2.4e6]))
+    p, o = SignalProcessor(fs), O.SignalProcessor(fs)
+    dtype = _DTYPES[int(rng.integers(0, 4))]
+    n = int(rng.integers(0, 40 if rng.uniform() < 0.25 else 20000))
+    x = _rand_samples(rng, n, dtype)
+    case = (seed, fs, dtype.__name__, n)
+    rate = None if rng.uniform() < 0.5 else float(rng.choice([240e3, 500e3, 1.0e6, 2.4e6]))
+    bw = float(rng.choice([25000, 12500, 50000, rng.uniform(1000, 400000)]))
+    got, want = p.filter_signal(x, bandwidth=bw, sample_rate=rate), o.filter_signal(x, bandwidth=bw, sample_rate=rate)
+    assert np.asarray(got).dtype == np.asarray(want).dtype and np.array_equal(got, want), case + ("filter", rate, bw)
+    off = float(rng.uniform(-20000, 20000))
+    got, want = p.frequency_shift(x, off, sample_rate=rate), o.frequency_shift(x, off, sample_rate=rate)
+    assert got.dtype == want.dtype and got.shape == want.shape, case + ("shift",)
+    if n:
+        assert np.max(np.abs(got - want)) <= 1e-12 * max(1.0, float(np.max(np.abs(want)))), case + ("shift", off)
+    got, want = p.extract_symbols(x, sample_rate=rate), o.extract_symbols(x, sample_rate=rate)
+    assert np.asarray(got).dtype == np.asarray(want).dtype and np.array_equal(got, want), case + ("extract", rate)
+    s = _rand_samples(rng, int(rng.integers(0, 3000)), dtype)
+    got, want = p.demodulate_dqpsk(s), o.demodulate_dqpsk(s)
+    assert got.dtype == want.dtype == np.uint8, case
+    _hard_equal(got, want, s if np.iscomplexobj(s) else s.astype(np.complex128))
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_scanner_counts_random_vs_oracle(seed):
+    """The scanner detector's counts (scanner.py:42-147, 204-231) on random batches: TETRA-like
+    chunks, noise, tones, silence, clipped and tiny rows at random rates and lengths, both complex
+    dtypes -- equal to the oracle's up to the counted decision-edge ulps (test_scanner.py)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import _signals
+    from test_scanner import _compare_counts
+    from tetraear.signal import scanner as S
+    rng = np.random.default_rng(6000 + seed)
+    fs = float(rng.choice([240e3, 1.0e6, 1.8e6, 2.4e6, 3.2e6]))
+    N = int(rng.integers(0, 300 if rng.uniform() < 0.2 else 150000))
+    rows = []
+    for _ in range(int(rng.integers(1, 7))):
+        kind = rng.choice(["tetra", "stress", "noise", "tone", "zero", "clip"])
+        if kind == "zero":
+            rows.append(np.zeros(N, np.complex64))
+        elif kind == "clip":
+            x = _signals.family("tetra", rng, N, fs)[0] * 40
+            rows.append((np.clip(x.real, -1, 1) + 1j * np.clip(x.imag, -1, 1)).astype(np.complex64))
+        else:
+            rows.append(_signals.family(str(kind), rng, N, fs)[0])
+    x = np.stack(rows).astype((np.complex64, np.complex128)[int(rng.integers(0, 2))])
+    st = S.scan_counts(x, fs)
+    for c in range(len(x)):
+        _compare_counts(st[c], x[c], fs)

@@ -1534,10 +1534,11 @@ __global__ __launch_bounds__(512) void k_extract_lat(const T *__restrict__ y, La
 }
 
 // ------------------------------------------------------------------ demodulate_dqpsk
-// sym rows [C][stride] complex T, S = nsym[ch] (or S_all).
+// sym rows [C][stride] complex T, S = nsym[ch] (or S_all); REAL: rows of real T (the reference
+// called on a real array: numpy's real division and product, np.imag(diff) = +0).
 // BS threads per channel: 64 for batches (one wave per channel), 1024 in the latency mode (a few
 // channels: ~1 symbol per thread).  The max is order-independent, so the result is the same.
-template <typename T, int BS>
+template <typename T, int BS, bool REAL = false>
 __global__ __launch_bounds__(BS) void k_demod(const T *__restrict__ sym, long stride, int C, const int32_t *__restrict__ nsym,
                                               long S_all, double t0, double t1, double t2, double t3,
                                               uint8_t *__restrict__ hard, long hstride) {
@@ -1546,11 +1547,11 @@ __global__ __launch_bounds__(BS) void k_demod(const T *__restrict__ sym, long st
     if (ch >= C) return;
     const long S = nsym ? nsym[ch] : S_all;
     if (S < 2) return;
-    const T *sp = sym + (size_t)ch * stride * 2;
+    const T *sp = sym + (size_t)ch * stride * (REAL ? 1 : 2);
     T m = (T)-INFINITY;
     bool any_nan = false;
     for (long k = lane; k < S; k += BS) {
-        const T a = np_cabs(sp[2 * k], sp[2 * k + 1]);
+        const T a = REAL ? fabs(sp[k]) : np_cabs(sp[2 * k], sp[2 * k + 1]);
         any_nan |= isnan(a);
         m = fmax(m, a);
     }
@@ -1579,6 +1580,20 @@ __global__ __launch_bounds__(BS) void k_demod(const T *__restrict__ sym, long st
     const T scl = norm ? (T)1 / (mx + (T)0 * rat) : (T)1;
     const T th0 = (T)t0, th1 = (T)t1, th2 = (T)t2, th3 = (T)t3;
     uint8_t *hp = hard + (size_t)ch * hstride;
+    if constexpr (REAL) {
+        // samples / max_power then sample * conj(prev) on real scalars: the product's sign (and
+        // signed zero) decides; arctan2(+0, dr) is 0 or pi
+        for (long k = 1 + lane; k < S; k += BS) {
+            T sr = sp[k], pr = sp[k - 1];
+            if (norm) {
+                sr = sr / mx;
+                pr = pr / mx;
+            }
+            const T ph = atan2((T)0, sr * pr);
+            hp[k - 1] = ph < th0 ? 3 : ph < th1 ? 2 : ph < th2 ? 0 : ph < th3 ? 1 : 3;
+        }
+        return;
+    }
     for (long k = 1 + lane; k < S; k += BS) {
         T sr = sp[2 * k], si = sp[2 * k + 1], pr = sp[2 * k - 2], pi = sp[2 * k - 1];
         if (norm) {
@@ -1823,16 +1838,16 @@ void launch_extract(tetra_ctx *ctx, const T *y, Lay ly, int C, long M, int sps, 
                            step, sym, smax, nsym, bph, (const T *)pw);
 }
 
-template <typename T>
+template <typename T, bool REAL = false>
 void launch_demod(tetra_ctx *ctx, const T *sym, long stride, int C, const int32_t *nsym, long S_all,
                   const double *thr, uint8_t *hard, long hstride) {
     PROF(ctx, "compat_demod");
     if (C <= SB_MAXC)   // a few channels: a workgroup of 1024 per channel
-        hipLaunchKernelGGL((k_demod<T, 1024>), dim3(C), dim3(1024), 0, ctx->stream, sym, stride, C, nsym, S_all, thr[0],
-                           thr[1], thr[2], thr[3], hard, hstride);
+        hipLaunchKernelGGL((k_demod<T, 1024, REAL>), dim3(C), dim3(1024), 0, ctx->stream, sym, stride, C, nsym, S_all,
+                           thr[0], thr[1], thr[2], thr[3], hard, hstride);
     else
-        hipLaunchKernelGGL((k_demod<T, 64>), dim3(C), dim3(64), 0, ctx->stream, sym, stride, C, nsym, S_all, thr[0], thr[1],
-                           thr[2], thr[3], hard, hstride);
+        hipLaunchKernelGGL((k_demod<T, 64, REAL>), dim3(C), dim3(64), 0, ctx->stream, sym, stride, C, nsym, S_all,
+                           thr[0], thr[1], thr[2], thr[3], hard, hstride);
 }
 
 int check_plan(tetra_ctx *ctx, const tetra_compat_plan *P) {
@@ -1950,13 +1965,19 @@ int tetra_extract_symbols(tetra_ctx *ctx, const void *x, int fmt, size_t C, size
 int tetra_demod_dqpsk(tetra_ctx *ctx, const void *sym, int fmt, size_t C, size_t S, const double *thr4, uint8_t *hard) {
     if (!ctx || !thr4) return TETRA_E_INVALID;
     if (S < 2 || C == 0) return TETRA_OK;
-    if (fmt != TETRA_CF32 && fmt != TETRA_CF64) return tetra_fail(ctx, TETRA_E_INVALID, "compat path takes cf32/cf64");
-    const size_t es = fmt == TETRA_CF64 ? 8 : 4;
+    const bool real = fmt == TETRA_F32 || fmt == TETRA_F64;
+    if (fmt != TETRA_CF32 && fmt != TETRA_CF64 && !real)
+        return tetra_fail(ctx, TETRA_E_INVALID, "demod_dqpsk takes cf32/cf64/f32/f64");
+    const size_t es = fmt == TETRA_CF64 || fmt == TETRA_F64 ? 8 : 4;
     Staging st(ctx);
-    const void *sd = st.in(sym, C * S * 2 * es);
+    const void *sd = st.in(sym, C * S * (real ? 1 : 2) * es);
     uint8_t *hd = (uint8_t *)st.out(hard, C * (S - 1));
     if (!sd || !hd) return st.finish();
-    if (fmt == TETRA_CF64)
+    if (fmt == TETRA_F64)
+        launch_demod<double, true>(ctx, (const double *)sd, (long)S, (int)C, nullptr, (long)S, thr4, hd, (long)(S - 1));
+    else if (fmt == TETRA_F32)
+        launch_demod<float, true>(ctx, (const float *)sd, (long)S, (int)C, nullptr, (long)S, thr4, hd, (long)(S - 1));
+    else if (fmt == TETRA_CF64)
         launch_demod<double>(ctx, (const double *)sd, (long)S, (int)C, nullptr, (long)S, thr4, hd, (long)(S - 1));
     else
         launch_demod<float>(ctx, (const float *)sd, (long)S, (int)C, nullptr, (long)S, thr4, hd, (long)(S - 1));

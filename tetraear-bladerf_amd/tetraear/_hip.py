@@ -14,6 +14,7 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TETRA_HIP_LIB", os.path.join(os.path.dirname(_PKG), "lib", "libtetra_hip.so"))
 
 TETRA_CF32, TETRA_CF64, TETRA_SC16 = 0, 1, 2
+TETRA_F32, TETRA_F64 = 3, 4   # real samples: tetra_demod_dqpsk only
 MAX_SYNC = 16
 F_POS, F_START, F_VALID, F_NBITS, F_NUMBER, F_BTYPE, F_CRC, F_HDR, F_FIELDS = range(9)
 (MAC_STATUS, MAC_PTYPE, MAC_MODE, MAC_FILL, MAC_ADDR, MAC_LENGTH, MAC_DATA_BITS, MAC_SYSINFO, MAC_MCC, MAC_MNC,

@@ -266,7 +266,11 @@ class SignalProcessor:
             return np.array([], dtype=np.uint8)
         x = np.asarray(samples)
         fmt = _fmt_of(x)
-        xc = _as_complex(x, fmt)
+        if np.iscomplexobj(x):
+            xc = _as_complex(x, fmt)
+        else:   # real samples: real division and product, as numpy runs them on a real array
+            fmt = _hip.TETRA_F32 if fmt == _hip.TETRA_CF32 else _hip.TETRA_F64
+            xc = np.ascontiguousarray(x, np.float32 if fmt == _hip.TETRA_F32 else np.float64)
         out = np.empty(len(x) - 1, np.uint8)
         thr = np.array(THRESHOLDS, np.float64)
         c = _hip.ctx()
@@ -340,6 +344,8 @@ class SignalProcessor:
             sym = soft[:n].copy()
         if real_in and freq_offset == 0:
             sym = sym.real.copy() if plan.filt else sym.real.astype(np.float32 if fmt == _hip.TETRA_CF32 else np.float64)
+            self.symbols = sym
+            return self.demodulate_dqpsk(sym)   # the reference decides real symbols with real arithmetic
         self.symbols = sym
         return hard[:max(0, n - 1)].copy()
 
@@ -413,6 +419,12 @@ class SignalProcessor:
                 "tetra_demod_compat")
         if f32.value:   # unfiltered cf32 without the mixer: complex64 symbols, rows smax apart
             soft = soft.reshape(-1).view(np.complex64)[:C * smax].reshape(C, smax).astype(np.complex128)
+        if real_in and not (afc or dev_offsets):
+            # real rows without the mixer keep real symbols in the reference: decide them as process() does
+            rt = np.float32 if (not plan.filt and fmt == _hip.TETRA_CF32) else np.float64
+            for r in np.flatnonzero(mo == 0):
+                if ns[r] >= 2:
+                    hard[r, :ns[r] - 1] = self.demodulate_dqpsk(soft[r, :ns[r]].real.astype(rt))
         if gate is not None:
             self.gate = {k: v.cpu().numpy() for k, v in gate.items()}
         return hard, soft, ns
