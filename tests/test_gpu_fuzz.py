@@ -246,3 +246,30 @@ def test_scanner_counts_random_vs_oracle(seed):
     st = S.scan_counts(x, fs)
     for c in range(len(x)):
         _compare_counts(st[c], x[c], fs)
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_wideband_channelize_random_vs_oracle(seed, monkeypatch):
+    """The C3 channeliser on random capture lengths (down to a few filter-bank blocks, ragged
+    tails), both filter-bank designs, every analysis form the host can pick and a random prefix
+    length: within test_wideband.py's Y_TOL of the float64 oracle, and a prefix request equal to the
+    full result's prefix."""
+    import wideband as W
+    from test_wideband import Y_TOL
+    from tetraear.signal.wideband import WidebandReceiver, synth_wideband
+    rng = np.random.default_rng(7000 + seed)
+    oversample = int(rng.choice([2, 4]))
+    form = str(rng.choice(["1", "2", "3", "4"] if oversample == 2 else ["1", "2"]))
+    monkeypatch.setenv("TETRA_WB_ANALYSIS", form)
+    Nw = int(rng.integers(1600, 5000 if rng.uniform() < 0.3 else 600000))
+    x = synth_wideband(Nw, seed=8000 + seed, snr_db=float(rng.uniform(5, 30)), oversample=oversample)[0]
+    d = W.design(oversample=oversample)
+    rx = WidebandReceiver(oversample=oversample)
+    y = rx.channelize(x)
+    want = W.channelize(x.astype(np.complex128), d)
+    case = (seed, oversample, form, Nw)
+    assert y.shape == want.shape, case
+    if y.size:
+        assert np.abs(y - want).max() <= Y_TOL * max(np.abs(want).max(), 1e-30), case
+        k = int(rng.integers(1, y.shape[1] + 1))
+        assert np.array_equal(rx.channelize(x, k), y[:, :k]), case + (k,)

@@ -110,6 +110,8 @@ class WidebandReceiver:
         _, n72 = self.plan.lengths(len(x))
         n_keep = n72 if n_keep is None else n_keep
         y = np.empty((self.plan.M, n_keep), np.complex64)
+        if n_keep == 0:   # a capture shorter than one 72 kHz output (the oracle's [M, 0])
+            return y
         c.check(c.lib.tetra_channelize(c.handle, self.plan.c, _hip.ptr(x), len(x), _hip.ptr(y), n_keep), "channelize")
         return y
 
@@ -122,6 +124,8 @@ class WidebandReceiver:
         n_keep = n72 if n_keep is None else n_keep
         y = np.empty((self.plan.M, n_keep), np.complex64)
         om = np.empty((self.plan.M, -(-n_keep // self.plan.c.up), 4), np.float32)
+        if n_keep == 0:
+            return y, om
         c.check(c.lib.tetra_channelize_om(c.handle, self.plan.c, _hip.ptr(x), len(x), _hip.ptr(y), n_keep,
                                           _hip.ptr(om)), "channelize_om")
         return y, om
