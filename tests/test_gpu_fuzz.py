@@ -273,3 +273,81 @@ def test_wideband_channelize_random_vs_oracle(seed, monkeypatch):
         assert np.abs(y - want).max() <= Y_TOL * max(np.abs(want).max(), 1e-30), case
         k = int(rng.integers(1, y.shape[1] + 1))
         assert np.array_equal(rx.channelize(x, k), y[:, :k]), case + (k,)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_afc_gate_random_vs_oracle(seed):
+    """The signal-present / AFC gate on random batches (tones anywhere in or beside the band,
+    TETRA-like bursts with CFO, noise at random levels, silence, chunks shorter than 2048 samples) at
+    the CLI rates, complex64 or complex128: statistics within test_spectrum.py's GATE_DB_TOL of the
+    float64 oracle; the decision, peak bin and AFC offset equal wherever the oracle's margins exceed
+    that tolerance (a random case may sit inside the band, the fixed ones do not)."""
+    import spectrum as SO
+    from test_spectrum import GATE_DB_TOL
+    from tetraear.signal.etsi import synth
+    from tetraear.signal.spectrum import afc_gate
+    rng = np.random.default_rng(9000 + seed)
+    fs = float(rng.choice([1.8e6, 1.9e6, 2.0e6, 2.1e6, 2.2e6, 2.3e6, 2.4e6]))
+    N = int(rng.integers(1000, 2100) if rng.uniform() < 0.15 else rng.integers(2048, 40000))
+    rows = []
+    n = np.arange(N)
+    for _ in range(int(rng.integers(1, 7))):
+        kind = rng.choice(["tone", "tetra", "noise", "zero"])
+        sig = 10 ** rng.uniform(-6, -1) * (rng.standard_normal(N) + 1j * rng.standard_normal(N))
+        if kind == "tone":
+            f = rng.uniform(-30000, 30000)
+            sig = sig + 10 ** rng.uniform(-4, 0) * np.exp(2j * np.pi * f * n / fs)
+        elif kind == "tetra":
+            sig = synth(1, 2 * ((N + 1) // 2), fs=fs, seed=int(rng.integers(1, 1 << 30)),
+                        snr_db=float(rng.uniform(0, 30)))[0][0][:N]
+        elif kind == "zero":
+            sig = np.zeros(N)
+        rows.append(sig)
+    x = np.stack(rows).astype((np.complex64, np.complex128)[int(rng.integers(0, 2))])
+    got = afc_gate(x, fs)
+    for i in range(len(x)):
+        want = SO.gate_iq(x[i], fs)
+        case = (seed, fs, N, i)
+        assert float(got["valid"][i]) == want["valid"], case
+        if not want["valid"]:
+            assert not got["present"][i] and float(got["afc"][i]) == 0.0, case
+            continue
+        for k in ("signal", "peak", "noise", "snr", "above"):
+            assert abs(float(got[k][i]) - want[k]) <= GATE_DB_TOL, case + (k, float(got[k][i]), want[k])
+        p = SO.frame_power(x[i], SO.N_FFT)
+        start, end, _, _ = SO.gate_bins(fs)
+        top = np.sort(np.asarray(p[start:end], np.float64))[::-1]
+        clear_peak = len(top) < 2 or top[0] - top[1] > 2 * GATE_DB_TOL
+        margins = min(abs(want["snr"] - 15), abs(want["peak"] + 70), abs(want["above"] - 3))
+        if clear_peak:
+            assert float(got["peak_bin"][i]) == want["peak_bin"], case
+            assert float(got["peak_freq"][i]) == want["peak_freq"], case
+        if margins > 2 * GATE_DB_TOL:
+            assert float(got["present"][i]) == want["present"], case + (want["snr"], want["peak"], want["above"])
+            if clear_peak:
+                assert float(got["afc"][i]) == want["afc"], case
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_compat_device_tensor_batches_equal_host(seed):
+    """process_batch on device tensors -- complex64 / complex128 [C, N] or float32 / float64
+    [C, N, 2], contiguous or a strided row selection, offsets on the host or as a device tensor --
+    returns exactly what the host-array call returns (the tensor path reads the tensor's
+    own format, made contiguous, never reinterpreted)."""
+    import torch
+    from tetraear.signal import SignalProcessor
+    rng = np.random.default_rng(9500 + seed)
+    fs = float(rng.choice([1.8e6, 2.4e6]))
+    C, N = int(rng.integers(1, 6)), int(rng.integers(100, 40000))
+    x = (0.3 * (rng.standard_normal((2 * C, N)) + 1j * rng.standard_normal((2 * C, N))))
+    x = x.astype((np.complex64, np.complex128)[int(rng.integers(0, 2))])
+    fo = np.where(rng.uniform(size=C) < 0.5, 0.0, rng.uniform(-3000, 3000, C))
+    host = x[::2]                                  # the rows the device call selects
+    want = SignalProcessor(fs).process_batch(np.ascontiguousarray(host), fo)
+    t = torch.from_numpy(x).cuda()[::2]            # non-contiguous: every other row
+    if rng.uniform() < 0.5:
+        t = torch.view_as_real(t.contiguous())     # [C, N, 2] real layout
+    offs = torch.from_numpy(fo).cuda() if rng.uniform() < 0.5 else fo
+    got = SignalProcessor(fs).process_batch(t, offs)
+    for g, w in zip(got, want):
+        assert np.array_equal(g, w), (seed, fs, C, N, x.dtype)
