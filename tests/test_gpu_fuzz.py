@@ -102,6 +102,21 @@ def test_etsi_random_geometry_vs_oracle(seed):
             assert len(f["blocks"]) == len(dec), case + (ch,)
             for b, (kind, bits, ok) in zip(f["blocks"], dec):
                 assert b["crc_ok"] == ok and np.array_equal(b["bits"], bits), case + (ch,)
+    # no cell given: acquisition from the BSCH (tetra_lmac_etsi_acquire) against the oracle's
+    from tetraear.core.etsi import UNKNOWN_CELL
+    lm = EtsiLowerMac()
+    res = lm.decode_batch(soft, hard, ns)
+    for ch in range(C):
+        n = int(ns[ch])
+        if n < 2:
+            assert res[ch] == [] and int(lm.cell_state[ch]) == UNKNOWN_CELL, case + (ch,)
+            continue
+        want, init = rx.lower_mac_acquire(soft[ch, :2 * (n - 1)], hard[ch, :n - 1], UNKNOWN_CELL)
+        assert int(lm.cell_state[ch]) == init, case + (ch,)
+        assert [(f["position"], f["burst_kind"]) for f in res[ch]] == [(s, k) for s, k, _ in want], case + (ch,)
+        for f, (_, _, dec) in zip(res[ch], want):
+            for b, (kind, bits, ok) in zip(f["blocks"], dec):
+                assert b["crc_ok"] == ok and np.array_equal(b["bits"], bits), case + (ch,)
 
 
 def _crc_burst_data(rng, fixed_tail):
