@@ -396,3 +396,25 @@ def test_etsi_components_random_vs_oracle(seed):
     if len(z) > 4 and rng.uniform() < 0.5:
         z[rng.integers(0, len(z), size=len(z) // 5)] = 0
     assert np.array_equal(p.demodulate_dqpsk(z), E.Receiver.decide(z)), (seed, len(z))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_compat_large_batches_vs_oracle(seed):
+    """Batches past the latency mode's 64 channels (the throughput kernels: banked decimator, one
+    wave per channel in filtfilt / extract / demod) at random rates, lengths and offsets: sampled
+    channels equal the oracle's sequential chain."""
+    from tetraear.signal import SignalProcessor
+    rng = np.random.default_rng(9700 + seed)
+    fs = COMPAT_RATES[1 + seed % (len(COMPAT_RATES) - 1)]
+    C, N = int(rng.integers(65, 300)), int(rng.integers(30, 30000))
+    x = (0.3 * (rng.standard_normal((C, N)) + 1j * rng.standard_normal((C, N)))).astype(np.complex64)
+    fo = np.where(rng.uniform(size=C) < 0.3, 0.0, rng.uniform(-4000, 4000, C))
+    hard, soft, ns = SignalProcessor(fs).process_batch(x, fo)
+    for c in sorted({0, C - 1, *rng.integers(0, C, 4).tolist()}):
+        o = O.SignalProcessor(fs)
+        h = o.process(x[c], fo[c])
+        case = (seed, fs, C, N, c)
+        assert ns[c] == len(o.symbols), case
+        if ns[c]:
+            assert np.max(np.abs(soft[c, :ns[c]] - o.symbols)) <= SOFT_TOL, case
+        _hard_equal(hard[c, :max(int(ns[c]) - 1, 0)], h, o.symbols)
