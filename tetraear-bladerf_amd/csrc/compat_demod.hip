@@ -718,10 +718,8 @@ __global__ __launch_bounds__(1024) void k_sosb_scan(const T *__restrict__ x, con
                                                     const T *__restrict__ zi, const double *__restrict__ phi,
                                                     const double *__restrict__ ends, double *__restrict__ states) {
     __shared__ double w[SB_MAXT][8];
-    __shared__ double ph[SB_NPOW * 64];   // the Phi^(2^r) table, read by every thread at every level
     const int k = threadIdx.x, s = blockIdx.x, ch = s >> 1, comp = s & 1;
     const bool on = k < G.Tn;
-    for (int i = k; i < SB_NPOW * 64; i += blockDim.x) ph[i] = phi[i];   // visible after the first level's barrier
     double v[8];
     if (on) {
         if (k == 0) {
@@ -753,7 +751,10 @@ __global__ __launch_bounds__(1024) void k_sosb_scan(const T *__restrict__ x, con
         }
         __syncthreads();
         if (upd) {
-            const double *P = ph + r * 64;
+            // the table straight from global memory at a wave-uniform address: scalar loads, SGPR
+            // operands (staged in LDS, its 36 broadcast reads per level cost ~2 us per scan:
+            // profiles/r05_ab_scan_sgpr.txt)
+            const double *P = phi + __builtin_amdgcn_readfirstlane(r) * 64;
             // the eight rows' sums side by side (each still j-ascending, no FMA: the same bits), then
             // the new state to LDS
 #pragma unroll
