@@ -4,7 +4,14 @@ The other GPU tests pin chosen geometries; this sweep draws the ones nobody chos
 chunk lengths, sample rates, offsets, SNRs, input formats -- from fixed seeds, so a failure names a
 reproducible case.  Bars are the same as the focused tests: compat soft symbols within 1e-5 and
 hard decisions bit-exact outside the 1e-9 rad tie band (test_gpu_compat.py); the ETSI chain bit-exact
-(symbols, soft bits, hard dibits, burst positions, decoded bits and CRC flags).
+(symbols, soft bits, hard dibits, burst positions, decoded bits and CRC flags); scanner counts up to
+the counted decision-edge ulps (test_scanner.py); gate statistics within GATE_DB_TOL and decisions
+outside that band (test_spectrum.py); the channeliser within Y_TOL (test_wideband.py).
+
+Covered: compat batches (latency and throughput kernels) and the direct SignalProcessor methods,
+compat decoder streams, the ETSI chain with its lower MAC (cell given and acquired) and its component
+methods, the scanner detector, the AFC gate, the wideband channeliser, device-tensor batches.  Each
+host-side bug the sweep found keeps its case here ("sweep").
 """
 import numpy as np
 import pytest
