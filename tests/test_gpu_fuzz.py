@@ -188,8 +188,11 @@ def test_decoder_random_streams_vs_oracle(seed):
         at = start + 510
     bits = bits[:nbits - nbits % 2]
     sym = (2 * bits[0::2] + bits[1::2]).astype(np.uint8)
-    if rng.uniform() < 0.15:   # the 8-PSK alphabet branch of symbols_to_bits (decoder.py:150-160)
+    u = rng.uniform()
+    if u < 0.15:   # the 8-PSK alphabet branch of symbols_to_bits (decoder.py:150-160)
         sym = rng.integers(0, 8, len(sym)).astype(np.uint8)
+    elif u < 0.25:   # wider integers, values outside both alphabets (mapped to 0 by the LUT branch)
+        sym = np.where(rng.uniform(size=len(sym)) < 0.05, rng.integers(-3, 12, len(sym)), sym).astype(np.int64)
     d = TetraDecoder(auto_decrypt=False)
     got = [decoded_view(f) for f in d.decode(sym)]
     mp = M.MacParser()
