@@ -22,6 +22,10 @@ from test_gpu_compat import SOFT_TOL, _hard_equal
 
 pytestmark = pytest.mark.gpu
 
+# TETRA_FUZZ_SCALE=k runs k times as many seeds of every sweep (exploration; the default is the
+# committed set the round-end suite runs)
+SCALE = max(1, int(__import__("os").environ.get("TETRA_FUZZ_SCALE", "1")))
+
 # reference rates: process() decimates by int(fs / 240e3) above 480 kHz (processor.py:245-256),
 # so these reach q = 1 (no decimation), 4, 7, 8, 10, 13 and 41
 COMPAT_RATES = [240e3, 1.0e6, 1.8e6, 2.0e6, 2.4e6, 3.2e6, 10e6]
@@ -42,7 +46,7 @@ def _compat_case(seed):
     return rng, fs, C, N, decimator, dtype, fo
 
 
-@pytest.mark.parametrize("seed", range(42))
+@pytest.mark.parametrize("seed", range(42 * SCALE))
 def test_compat_random_geometry_vs_oracle(seed):
     from tetraear.signal import SignalProcessor
     rng, fs, C, N, decimator, dtype, fo = _compat_case(seed)
@@ -69,7 +73,7 @@ def test_compat_random_geometry_vs_oracle(seed):
     _hard_equal(h1, o.process(x[0], fo[0]), o.symbols)
 
 
-@pytest.mark.parametrize("seed", range(42))
+@pytest.mark.parametrize("seed", range(42 * SCALE))
 def test_etsi_random_geometry_vs_oracle(seed):
     from tetraear.signal.etsi import EtsiReceiver, synth
     from tetraear.core.etsi import EtsiLowerMac
@@ -155,7 +159,7 @@ def _crc_burst_data(rng, fixed_tail):
     return d
 
 
-@pytest.mark.parametrize("seed", range(24))
+@pytest.mark.parametrize("seed", range(24 * SCALE))
 def test_decoder_random_streams_vs_oracle(seed):
     """Random symbol streams with bursts placed at random bit offsets: syncs with 0-4 bit errors,
     burst CRCs valid or 1-4 bits off (the reference accepts <= 2), both symbol alphabets -- the
@@ -212,7 +216,7 @@ def _rand_samples(rng, n, dtype):
     return (x if np.dtype(dtype).kind == "c" else x.real).astype(dtype)
 
 
-@pytest.mark.parametrize("seed", range(40))
+@pytest.mark.parametrize("seed", range(40 * SCALE))
 def test_direct_methods_random_vs_oracle(seed):
     """The reference's SignalProcessor methods called directly (as modern.py / the tools do) on
     random lengths, rates, bandwidths and all four sample dtypes: filter_signal bit-exact (fp64
@@ -243,7 +247,7 @@ def test_direct_methods_random_vs_oracle(seed):
     _hard_equal(got, want, s if np.iscomplexobj(s) else s.astype(np.complex128))
 
 
-@pytest.mark.parametrize("seed", range(16))
+@pytest.mark.parametrize("seed", range(16 * SCALE))
 def test_scanner_counts_random_vs_oracle(seed):
     """The scanner detector's counts (scanner.py:42-147, 204-231) on random batches: TETRA-like
     chunks, noise, tones, silence, clipped and tiny rows at random rates and lengths, both complex
@@ -273,7 +277,7 @@ def test_scanner_counts_random_vs_oracle(seed):
         _compare_counts(st[c], x[c], fs)
 
 
-@pytest.mark.parametrize("seed", range(10))
+@pytest.mark.parametrize("seed", range(10 * SCALE))
 def test_wideband_channelize_random_vs_oracle(seed, monkeypatch):
     """The C3 channeliser on random capture lengths (down to a few filter-bank blocks, ragged
     tails), both filter-bank designs, every analysis form the host can pick and a random prefix
@@ -300,7 +304,7 @@ def test_wideband_channelize_random_vs_oracle(seed, monkeypatch):
         assert np.array_equal(rx.channelize(x, k), y[:, :k]), case + (k,)
 
 
-@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("seed", range(12 * SCALE))
 def test_afc_gate_random_vs_oracle(seed):
     """The signal-present / AFC gate on random batches (tones anywhere in or beside the band,
     TETRA-like bursts with CFO, noise at random levels, silence, chunks shorter than 2048 samples) at
@@ -337,9 +341,14 @@ def test_afc_gate_random_vs_oracle(seed):
         if not want["valid"]:
             assert not got["present"][i] and float(got["afc"][i]) == 0.0, case
             continue
-        for k in ("signal", "peak", "noise", "snr", "above"):
-            assert abs(float(got[k][i]) - want[k]) <= GATE_DB_TOL, case + (k, float(got[k][i]), want[k])
+        # the fp32 FFT resolves a bin to ~1e-7 of the frame's largest one: where the frame spans more
+        # than ~100 dB (a strong tone outside the band over a -140 dB floor) the deep bins carry that
+        # error into the noise mean, so there the statistics are held to 5x the tolerance (measured
+        # 2.05e-3 dB at a 125 dB span, seed 44 of TETRA_FUZZ_SCALE=6); decisions unaffected
         p = SO.frame_power(x[i], SO.N_FFT)
+        tol = GATE_DB_TOL if float(np.max(p)) - want["noise"] < 100 else 5 * GATE_DB_TOL
+        for k in ("signal", "peak", "noise", "snr", "above"):
+            assert abs(float(got[k][i]) - want[k]) <= tol, case + (k, float(got[k][i]), want[k])
         start, end, _, _ = SO.gate_bins(fs)
         top = np.sort(np.asarray(p[start:end], np.float64))[::-1]
         clear_peak = len(top) < 2 or top[0] - top[1] > 2 * GATE_DB_TOL
@@ -353,7 +362,7 @@ def test_afc_gate_random_vs_oracle(seed):
                 assert float(got["afc"][i]) == want["afc"], case
 
 
-@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("seed", range(8 * SCALE))
 def test_compat_device_tensor_batches_equal_host(seed):
     """process_batch on device tensors -- complex64 / complex128 [C, N] or float32 / float64
     [C, N, 2], contiguous or a strided row selection, offsets on the host or as a device tensor --
@@ -378,7 +387,7 @@ def test_compat_device_tensor_batches_equal_host(seed):
         assert np.array_equal(g, w), (seed, fs, C, N, x.dtype)
 
 
-@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("seed", range(12 * SCALE))
 def test_etsi_components_random_vs_oracle(seed):
     """ETSI mode's component methods at random rates and lengths: filter_signal (the channel
     filter) and extract_symbols (timing) bit-identical to the oracle's chanfilt / timing, process()
@@ -408,7 +417,7 @@ def test_etsi_components_random_vs_oracle(seed):
     assert np.array_equal(p.demodulate_dqpsk(z), E.Receiver.decide(z)), (seed, len(z))
 
 
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", range(6 * SCALE))
 def test_compat_large_batches_vs_oracle(seed):
     """Batches past the latency mode's 64 channels (the throughput kernels: banked decimator, one
     wave per channel in filtfilt / extract / demod) at random rates, lengths and offsets: sampled
