@@ -86,7 +86,9 @@ def _compare_counts(st, x, fs):
     p = np.mean(np.abs(x.astype(np.complex128)) ** 2)
     assert abs(st[S.F_POW] - p) <= 1e-9 * p
     ws = len(x) // 5
-    for i in range(5):
+    # rows shorter than 5 samples have empty windows (np.mean -> nan); the detector's surface never
+    # reads them there (check_power_stability needs 5000 samples, scanner.py:80-87)
+    for i in range(5 if ws else 0):
         pw = np.mean(np.abs(x[i * ws:(i + 1) * ws].astype(np.complex128)) ** 2)
         assert abs(st[S.F_POW_W0 + i] - pw) <= 1e-9 * max(pw, 1e-30)
 
