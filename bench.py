@@ -73,30 +73,41 @@ def parse():
                          "--chunks consecutive chunks of each channel's capture, as a streaming receiver does), or "
                          "is given the synthesised cells up front")
     ap.add_argument("--chunks", type=int, default=None,
-                    help="etsi: each channel is one continuous capture of CHUNKS x --samples samples, resident as "
-                         "CHUNKS batches; step k decodes batch k mod CHUNKS (default: 8 with --cells acquire, so the "
-                         "cell state a step starts from was acquired from earlier chunks; 1 with --cells given)")
+                    help="etsi: each channel is one continuous capture of CHUNKS x --samples samples resident in "
+                         "HBM, decoded as one stream (CHUNKS > 1, fused demod: step k demodulates chunk k's window with "
+                         "the timing loops carried and resumes the lower MAC's burst scan on the previous step's "
+                         "unconsumed dibits; past the last chunk the capture restarts as a new one).  Default with "
+                         "--cells acquire: warmup + steps (>= 8, capped by free HBM), so the timed steps never restart "
+                         "it; 1 (each step the same chunk on its own) with --cells given")
     ap.add_argument("--demod", choices=("fused", "split"), default="fused",
                     help="etsi: fused channel filter + timing in one launch, or split (y through HBM, timing "
                          "launched separately -- beside the next batch's channel filter when pipelined)")
     return ap.parse_args()
 
 
-def traffic_from_profiles(kernel, workload_key):
+def traffic_from_profiles(kernel, workload_key, profiles=None):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of this
     workload (profiles/*_summary.json, written by tools/pmc_summary.py from separate FETCH_SIZE /
     WRITE_SIZE passes over the timed launches, with the gfx950 x2 FETCH correction, calibrated at
-    4-, 8- and 16-B loads: profiles/r05_fetch_calibration.json), or None."""
+    4-, 8- and 16-B loads: profiles/r05_fetch_calibration.json).
+
+    Only a summary of the CURRENT code counts: its entry must carry the kernel source's hash
+    (tools/pmc_summary.py: kernel_source -- the .hip file defining the kernel plus common.h) and that
+    hash must equal the file's hash now.  Otherwise {"bytes": None, "reason": ...} says why (no
+    summary of this workload, or only summaries of other code), never a stale number."""
     import glob
     import re
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    from pmc_summary import kernel_source
+    now = kernel_source(kernel)
 
     def age(f):   # (round, version): r02_x beats r01_x_v10, v10 beats v9 (not a string sort)
         b = os.path.basename(f)
         r, v = re.match(r"r(\d+)_", b), re.search(r"_v(\d+)_", b)
         return (int(r.group(1)) if r else 0, int(v.group(1)) if v else 0, b)
 
-    best = None
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_summary.json")), key=age):
+    best, stale = None, []
+    for f in sorted(glob.glob(os.path.join(profiles or os.path.join(REPO, "profiles"), "*_summary.json")), key=age):
         try:
             d = json.load(open(f))
         except ValueError:
@@ -107,9 +118,19 @@ def traffic_from_profiles(kernel, workload_key):
         ks.sort(key=lambda v: v.get("timed_launches", 0))
         k = ks[-1] if ks else {}
         if workload_key in d.get("workload", "") and k and (d.get("selection") != "markers" or "timed_launches" in k):
+            if now is None or k.get("source") != now:
+                stale.append(os.path.basename(f))
+                continue
             best = (k["hbm_bytes_per_launch"], os.path.basename(f), k.get("timed_avg_ns", k.get("avg_ns")))
     if best is None:
-        return None
+        if now is None:
+            why = f"no source file defines {kernel}"
+        elif stale:
+            why = (f"{len(stale)} summaries of this workload (newest {stale[-1]}) profiled other code than the "
+                   f"current {now['file']} (sha256 {now['sha256'][:12]}); re-profile with tools/profile_bench.sh")
+        else:
+            why = "no rocprofv3 PMC summary of this workload under profiles/"
+        return {"bytes": None, "source": None, "reason": why}
     # the same summary's rocprof average duration of the kernel (timed launches when recorded), so the
     # line's live launch_ms can be checked against the committed profile
     return {"bytes": best[0], "source": best[1], "rocprof_avg_ms": round(best[2] / 1e6, 4) if best[2] else None}
@@ -345,7 +366,16 @@ def main():
         C, N = 1, a.wb_samples   # units: wideband samples
     elif a.chain == "etsi":
         from tetraear.signal.etsi import BenchStep as EtsiStep
-        chunks = a.chunks if a.chunks is not None else (8 if a.cells == "acquire" else 1)
+        if a.chunks is not None:
+            chunks = a.chunks
+        elif a.cells == "acquire" and a.demod == "fused" and not a.host_input:
+            # one continuous capture per channel, long enough that the run never restarts it: the
+            # streaming receiver decodes it as one symbol stream (capped by the free HBM)
+            per = C * N * (4 if a.iq == "sc16" else 8)
+            free = torch.cuda.mem_get_info(dev)[0]
+            chunks = max(2, min(max(8, a.warmup + a.steps), int(0.8 * free) // per))
+        else:
+            chunks = 1
         step = EtsiStep(c, C, N, FS, seed=rank_seed(1000, rank), device=dev, iq_format=a.iq, demod=a.demod,
                         cells=a.cells, chunks=chunks)
         pipe = "off" if a.no_pipeline else a.pipeline

@@ -79,7 +79,8 @@ int tetra_profile_read(tetra_ctx *ctx, char *names, size_t names_len, double *ms
 int tetra_mark(tetra_ctx *ctx, int tag);
 
 /* =====================================================================================
- * Compat demod -- bit-compatible with SignalProcessor (processor.py:221-273)
+ * Compat demod -- bit-compatible with SignalProcessor (processor.py:221-273) in its default
+ * (sequential) form; the opt-in latency mode (TETRA_COMPAT_BLOCKED) is within fp32 noise only
  * ===================================================================================== */
 
 /* Filter design and control decisions are made by the host (the same scipy.signal design calls
@@ -104,15 +105,23 @@ typedef struct tetra_compat_plan {
     double thr[4];        /* -5*pi/8, -3*pi/8, 3*pi/8, 5*pi/8 as Python evaluates them */
 } tetra_compat_plan;
 
-/* tetra_compat_plan.flags.  The decimator of tetra_demod_compat runs either sequentially in time
- * (scipy's exact operation order: bit-identical to the reference) or time-blocked (tiles of 256
- * samples recursed in parallel, their start states composed in float64: within the cheby1 filter's
- * fp32 noise of scipy -- <= 3.4e-6 on .symbols over the reference fixtures at q <= 10, no decision
- * changed -- and 10-20x lower latency for a single channel).  Automatic (0): time-blocked for
- * C <= 64 channels, decimation q <= 16 and N + 54 <= 262144 samples, else sequential.  The component
- * entry point tetra_decimate is always sequential. */
-#define TETRA_COMPAT_SEQUENTIAL 1   /* force the scipy-exact sequential decimator */
-#define TETRA_COMPAT_BLOCKED    2   /* force the time-blocked decimator (TETRA_E_INVALID outside its limits) */
+/* tetra_compat_plan.flags.  The decimator and filtfilt of tetra_demod_compat run sequentially in
+ * time by default (0, or TETRA_COMPAT_SEQUENTIAL): scipy's exact operation order, bit-identical to
+ * the reference.  TETRA_COMPAT_BLOCKED opts into the latency mode: tiles of 256 (decimator) / 128
+ * (filtfilt) samples recursed in parallel, their start states composed in float64, for C <= 64
+ * channels, q <= 16 and N + 54 <= 262144 samples (TETRA_E_INVALID outside those limits); ~40x lower
+ * latency for one channel but NOT bit-exact: the decimator ends up to ~1.5e-5 from scipy's fp32
+ * state near the chunk start, so a decision whose phase margin is ~1e-6 rad can flip (measured: 3 in
+ * 1.6 M symbols).  The component entry point tetra_decimate is always sequential. */
+#define TETRA_COMPAT_SEQUENTIAL 1   /* the scipy-exact sequential passes (the default) */
+#define TETRA_COMPAT_BLOCKED    2   /* the time-blocked latency mode (opt-in, not bit-exact) */
+
+/* Host-only (no device needed): the kernels tetra_demod_compat would run for `plan` on a [C][N]
+ * batch, as TETRA_FORM_* bits in *forms. */
+#define TETRA_FORM_DEC_BLOCKED  1   /* decimate: time-blocked (else scipy's sequential order) */
+#define TETRA_FORM_LF_BLOCKED   2   /* filtfilt: time-blocked (else scipy's sequential order) */
+#define TETRA_FORM_POW_PREPASS  4   /* extract_symbols: |y|^2 first in parallel (exact either way) */
+int tetra_compat_forms(const tetra_compat_plan *plan, size_t C, size_t N, int32_t *forms);
 
 /* Fused process() over a batch of C equal-length chunks.
  *   iq        [C][N] complex, format iq_fmt (TETRA_CF32 for SC16-derived capture data)
@@ -365,6 +374,60 @@ int tetra_lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard,
 int tetra_lmac_etsi_acquire(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard, const int32_t *nsym,
                             size_t C, size_t smax, uint32_t *cell_init, int32_t *nburst, int32_t *bursts,
                             int32_t *nblock, int32_t *blocks, uint8_t *type1);
+/* ---------------------------------------------------------------- streaming (one continuous capture)
+ * The reference's callers stream a continuous capture in chunks (modern.py:1901-1919,
+ * continuous_capture.py:20); these entry points decode consecutive chunks of each channel as ONE
+ * symbol stream, so no burst is lost at a chunk seam (oracle/etsi.py: Stream restates them).
+ *   1. tetra_etsi_stream_window: where chunk k's channel-filter window starts.  The window re-reads
+ *      the previous chunk's last samples from s, a multiple of P = q1 * down input samples, so its
+ *      filter phases equal a run over the whole capture; yoff = its first new 72 kHz output.
+ *   2. tetra_demod_etsi_stream: the fused demod over the window (rows of `ld` samples: a capture
+ *      resident as [C][ld] is windowed in place) with each channel's timing loop carried in track.
+ *   3. tetra_lmac_etsi_stream: the lower MAC over rows that hold the previous chunk's unconsumed
+ *      dibits in front of the new ones; the greedy burst scan resumes at the bit it stopped at. */
+typedef struct tetra_etsi_track {
+    float base;       /* next symbol's Gardner base position, 72 kHz samples from the end of the last chunk's outputs */
+    float delta;      /* block-Gardner loop offset */
+    float prev_re, prev_im;   /* the last symbol of the previous chunk (dibit 0 of the next spans the seam) */
+    int32_t acquired;         /* 0: the next chunk acquires the phase (Oerder-Meyr) and starts a new chain */
+    int32_t reserved[3];
+} tetra_etsi_track;
+#define TETRA_ETSI_RESERVE 256   /* dibits ahead of a streaming output row (the lower MAC's carried tail) */
+#define TETRA_ETSI_MARGIN 8      /* 72 kHz samples a window re-computes before its first new output */
+
+/* Host-only window arithmetic: for a stream of x_total samples already received (y_done 72 kHz
+ * outputs produced) and a next chunk of n samples: *s = the window's first sample (global index),
+ * *W = its length (x_total + n - s), *yoff = the window index of output y_done, *y_done_next. */
+int tetra_etsi_stream_window(const tetra_etsi_plan *plan, int64_t x_total, int64_t y_done, int64_t n, int64_t *s,
+                             int64_t *W, int64_t *yoff, int64_t *y_done_next);
+/* Fused demod of one window per channel: iq points at the window's first sample of channel 0, rows
+ * ld samples apart (ld >= W, a multiple of 4 for SC16); track [C] (in/out, host or device).  Outputs
+ * as tetra_demod_etsi_fmt, rows `ostride` symbols apart with capacity smax: with track[c].acquired,
+ * symbol 0 is the carried last symbol of the previous chunk, so the nsym-1 dibits start with the one
+ * across the seam. */
+int tetra_demod_etsi_stream(tetra_ctx *ctx, const tetra_etsi_plan *plan, const void *iq, int iq_fmt, size_t C,
+                            size_t ld, size_t W, int yoff, tetra_etsi_track *track, void *soft, int8_t *softbits,
+                            uint8_t *hard, int32_t *nsym, size_t smax, size_t ostride, float *diag);
+/* Lower MAC over streaming rows: row c of hard (softbits) is `stride` dibits (2 stride bytes); this
+ * chunk's nsym[c]-1 dibits start at TETRA_ETSI_RESERVE, the previous chunk's tail is in front of
+ * them and lead[c] (in/out) is the row bit the scan starts at (2 * TETRA_ETSI_RESERVE for a new
+ * stream).  After the scan the unconsumed dibits (from the first bit not examined) are copied in
+ * front of TETRA_ETSI_RESERVE in next_soft / next_hard (the rows the next chunk's demod writes;
+ * they may be these rows) and lead[c] set for the next chunk.  bursts[.][0] is the burst's start
+ * bit relative to this chunk's first new dibit (negative: it began in the carried tail).
+ * cell_init: NULL (configured cells) or the acquisition state, as tetra_lmac_etsi_acquire. */
+int tetra_lmac_etsi_stream(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard, const int32_t *nsym,
+                           size_t C, size_t stride, int32_t *lead, int8_t *next_soft, uint8_t *next_hard,
+                           uint32_t *cell_init, int32_t *nburst, int32_t *bursts, int32_t *nblock, int32_t *blocks,
+                           uint8_t *type1);
+
+/* The ETSI receiver's AFC mixer on a streaming window: out [C][N] cf32 = iq (cf32 rows ld samples
+ * apart) x exp(-j 2 pi f (n0 + n) / fs), n0 = the window's first sample in the capture (frequency_shift's
+ * float64 arithmetic, processor.py:85-100, with one continuous phase across windows); mix_c [C] as
+ * tetra_demod_compat's (the imaginary part of -1j*2*pi*f). */
+int tetra_etsi_mix(tetra_ctx *ctx, const void *iq, size_t C, size_t ld, size_t N, const double *mix_c, double fs,
+                   int64_t n0, void *out);
+
 /* Component: decode F type-5 soft blocks of one kind (K = 432/216/120): type1 [F][n1], crc_ok [F]. */
 int tetra_etsi_decode_blocks(tetra_ctx *ctx, const int8_t *soft5, size_t F, int kind,
                              const uint32_t *scramb_init, uint8_t *type1, uint8_t *crc_ok);

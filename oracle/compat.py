@@ -44,6 +44,10 @@ def lib():
         L.orc_sosfilt_f32.argtypes = [f32p, ctypes.c_int, f32p, f32p, ctypes.c_long]
         L.orc_sosfilt_f64.argtypes = [f64p, ctypes.c_int, f64p, f64p, ctypes.c_long]
         L.orc_lfilter_f64.argtypes = [f64p, f64p, ctypes.c_int, f64p, f64p, ctypes.c_long]
+        vp = ctypes.c_void_p
+        for nm in ("orc_sos_tiles_f32", "orc_sos_tiles_f64"):
+            getattr(L, nm).argtypes = [vp, ctypes.c_int, vp, ctypes.c_long, ctypes.c_int, vp, vp, vp]
+        L.orc_lf_tiles_f64.argtypes = [vp, vp, ctypes.c_int, vp, ctypes.c_long, ctypes.c_int, vp, vp, vp]
         L.orc_sync_counts.argtypes = [u8p, ctypes.c_long, u8p, u8p]
         L.orc_find_sync_greedy.argtypes = [u8p, u8p, ctypes.c_long, ctypes.c_int, i64p, ctypes.c_int,
                                            ctypes.POINTER(ctypes.c_int)]
@@ -189,14 +193,15 @@ def _blocked_pass(coef, zi, c, real_t, tab):
     w_k += Phi^d w_{k-d}, every tile again from its start state."""
     L = len(c)
     Tn = -(-L // SB_B)
-    fn = lib().orc_sosfilt_f32 if real_t is np.float32 else lib().orc_sosfilt_f64
+    tiles = lib().orc_sos_tiles_f32 if real_t is np.float32 else lib().orc_sos_tiles_f64
+    c = np.ascontiguousarray(c, real_t)
+    coef = np.ascontiguousarray(coef, real_t)
     s0 = np.ascontiguousarray(zi * c[0], dtype=real_t)
     w = np.zeros((Tn, 8), np.float64)
     w[0] = s0.astype(np.float64)
-    for k in range(Tn - 1):
-        z = np.zeros(8, real_t)
-        fn(coef, 4, z, np.array(c[k * SB_B:(k + 1) * SB_B], real_t), SB_B)
-        w[k + 1] = z.astype(np.float64)
+    # every tile from zero state -> its end state (compat_oracle.c: orc_sos_tiles_*, the loop
+    # "for k < Tn - 1: sosfilt(tile k, z = 0); w[k + 1] = z")
+    tiles(coef.ctypes.data, 4, c.ctypes.data, L, SB_B, w.ctypes.data, None, None)
     r = 0
     while (1 << r) < Tn:
         d = 1 << r
@@ -207,10 +212,8 @@ def _blocked_pass(coef, zi, c, real_t, tab):
         w[d:] = acc
         r += 1
     out = np.empty(L, real_t)
-    for k in range(Tn):
-        t = np.array(c[k * SB_B:(k + 1) * SB_B], real_t)
-        fn(coef, 4, w[k].astype(real_t), t, len(t))
-        out[k * SB_B:k * SB_B + len(t)] = t
+    w = np.ascontiguousarray(w)
+    tiles(coef.ctypes.data, 4, c.ctypes.data, L, SB_B, None, w.ctypes.data, out.ctypes.data)   # tile k from w[k]
     return out
 
 
@@ -287,12 +290,10 @@ def _lf_blocked_pass(bb, aa, zi, c, tab):
     """lfilter of one real float64 sequence c from state zi * c[0], time-blocked (tiles of LB_B)."""
     L = len(c)
     Tn = -(-L // LB_B)
+    c = np.ascontiguousarray(c, np.float64)
     w = np.zeros((Tn, LB_NS), np.float64)
     w[0] = zi * c[0]
-    for k in range(Tn - 1):
-        z = np.zeros(LB_NS, np.float64)
-        lib().orc_lfilter_f64(bb, aa, len(bb), z, np.array(c[k * LB_B:(k + 1) * LB_B], np.float64), LB_B)
-        w[k + 1] = z
+    lib().orc_lf_tiles_f64(bb.ctypes.data, aa.ctypes.data, len(bb), c.ctypes.data, L, LB_B, w.ctypes.data, None, None)
     r = 0
     while (1 << r) < Tn:
         d = 1 << r
@@ -303,10 +304,9 @@ def _lf_blocked_pass(bb, aa, zi, c, tab):
         w[d:] = acc
         r += 1
     out = np.empty(L, np.float64)
-    for k in range(Tn):
-        t = np.array(c[k * LB_B:(k + 1) * LB_B], np.float64)
-        lib().orc_lfilter_f64(bb, aa, len(bb), w[k].copy(), t, len(t))
-        out[k * LB_B:k * LB_B + len(t)] = t
+    w = np.ascontiguousarray(w)
+    lib().orc_lf_tiles_f64(bb.ctypes.data, aa.ctypes.data, len(bb), c.ctypes.data, L, LB_B, None, w.ctypes.data,
+                           out.ctypes.data)
     return out
 
 
@@ -346,8 +346,9 @@ class SignalProcessor:
         self.symbol_rate = 18000
         self.samples_per_symbol = int(sample_rate / self.symbol_rate)
         self.symbols = None
-        # "sequential": the reference's decimate; "blocked": the product's latency-mode decimator;
-        # "auto": blocked where tetra_demod_compat picks it for one channel (blocked_fits)
+        # "sequential" / "auto": the reference's decimate and filtfilt (the product's default form);
+        # "blocked": the product's opt-in latency mode (time-blocked decimate and filtfilt where
+        # they fit one channel: blocked_fits / lf_blocked_fits)
         self.decimator = decimator
 
     def filter_signal(self, samples, bandwidth=25000, sample_rate=None):
@@ -429,15 +430,14 @@ class SignalProcessor:
             q = int(rate / 240000)
             if q > 1:
                 try:
-                    blk = self.decimator == "blocked" or (self.decimator == "auto" and
-                                                          blocked_fits(1, len(samples), q))
+                    blk = self.decimator == "blocked"   # (the product refuses it past blocked_fits)
                     samples = decimate_blocked(samples, q) if blk else decimate(samples, q)
                     rate = rate / q
                 except Exception:
                     pass
         if freq_offset != 0:
             samples = self.frequency_shift(samples, freq_offset, sample_rate=rate)
-        if self.decimator != "sequential" and lf_blocked_fits(1, len(samples)):   # one chunk: latency mode
+        if self.decimator == "blocked" and lf_blocked_fits(1, len(samples)):   # opt-in latency mode
             filtered = self._filter_blocked(samples, rate)
         else:
             filtered = self.filter_signal(samples, bandwidth=25000, sample_rate=rate)

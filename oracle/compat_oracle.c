@@ -37,6 +37,37 @@
 void orc_sosfilt_f32(const float *sos, int ns, float *zi, float *x, long len) { SOSFILT_BODY(float) }
 void orc_sosfilt_f64(const double *sos, int ns, double *zi, double *x, long len) { SOSFILT_BODY(double) }
 
+/* The product's opt-in latency-mode decimator, tile passes (oracle/compat.py: _blocked_pass; not a
+ * reference function): w[k+1] = the end state of tile k (B samples of c from zero state) as double,
+ * k < Tn - 1; then every tile again from its start state w[k] cast to T, outputs to out. */
+#define SOS_TILES_BODY(T, FILT)                                                          \
+    long Tn = (L + B - 1) / B;                                                           \
+    T tmp[4096];                                                                         \
+    if (B > 4096 || ns > 4) return;                                                      \
+    if (w) {                                                                             \
+        for (long k = 0; k + 1 < Tn; ++k) {                                              \
+            T z[8] = {0};                                                                \
+            memcpy(tmp, c + k * B, sizeof(T) * B);                                       \
+            FILT(sos, ns, z, tmp, B);                                                    \
+            for (int i = 0; i < 2 * ns; ++i) w[(k + 1) * 2 * ns + i] = (double)z[i];     \
+        }                                                                                \
+    }                                                                                    \
+    if (out) {                                                                           \
+        for (long k = 0; k < Tn; ++k) {                                                  \
+            long n = L - k * B < B ? L - k * B : B;                                      \
+            T z[8];                                                                      \
+            for (int i = 0; i < 2 * ns; ++i) z[i] = (T)st[k * 2 * ns + i];               \
+            memcpy(tmp, c + k * B, sizeof(T) * n);                                       \
+            FILT(sos, ns, z, tmp, n);                                                    \
+            memcpy(out + k * B, tmp, sizeof(T) * n);                                     \
+        }                                                                                \
+    }
+
+void orc_sos_tiles_f32(const float *sos, int ns, const float *c, long L, int B, double *w, const double *st,
+                       float *out) { SOS_TILES_BODY(float, orc_sosfilt_f32) }
+void orc_sos_tiles_f64(const double *sos, int ns, const double *c, long L, int B, double *w, const double *st,
+                       double *out) { SOS_TILES_BODY(double, orc_sosfilt_f64) }
+
 /* One real component through lfilter's DF-II-T loop (a[0] == 1), in place; zi has nt-1 entries. */
 void orc_lfilter_f64(const double *b, const double *a, int nt, double *zi, double *x, long len)
 {
@@ -48,6 +79,33 @@ void orc_lfilter_f64(const double *b, const double *a, int nt, double *zi, doubl
         zi[nt - 2] = xn * b[nt - 1] - yn * a[nt - 1];
         x[n] = yn;
     }
+}
+
+/* The latency mode's time-blocked filtfilt, tile passes (oracle/compat.py: _lf_blocked_pass), as
+ * orc_sos_tiles_* with lfilter's nt - 1 states. */
+void orc_lf_tiles_f64(const double *b, const double *a, int nt, const double *c, long L, int B, double *w,
+                      const double *st, double *out)
+{
+    long Tn = (L + B - 1) / B;
+    double tmp[4096];
+    const int K = nt - 1;
+    if (B > 4096 || K > 8) return;
+    if (w)
+        for (long k = 0; k + 1 < Tn; ++k) {
+            double z[8] = {0};
+            memcpy(tmp, c + k * B, sizeof(double) * B);
+            orc_lfilter_f64(b, a, nt, z, tmp, B);
+            for (int i = 0; i < K; ++i) w[(k + 1) * K + i] = z[i];
+        }
+    if (out)
+        for (long k = 0; k < Tn; ++k) {
+            long n = L - k * B < B ? L - k * B : B;
+            double z[8];
+            for (int i = 0; i < K; ++i) z[i] = st[k * K + i];
+            memcpy(tmp, c + k * B, sizeof(double) * n);
+            orc_lfilter_f64(b, a, nt, z, tmp, n);
+            memcpy(out + k * B, tmp, sizeof(double) * n);
+        }
 }
 
 static const uint8_t TS1[22] = {1,1,0,1,0,0,0,0,1,1,1,0,1,0,0,1,1,1,0,1,0,0};

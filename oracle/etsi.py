@@ -19,6 +19,12 @@ FS_NOMINAL = 2.4e6
 SYMBOL_RATE = 18000.0
 KIND = {"SCH/F": 0, "SCH/HD": 1, "BSCH": 2}
 KIND_PARAMS = {0: (432, 103, 288, 268), 1: (216, 101, 144, 124), 2: (120, 11, 80, 60)}  # K, a, n2, n1
+# eo_track / tetra_etsi_track: the streaming receiver's per-channel timing state
+TRACK = np.dtype([("base", np.float32), ("delta", np.float32), ("pr", np.float32), ("pi", np.float32),
+                  ("acquired", np.int32), ("reserved", np.int32, 3)])
+MAXB = 8          # bursts per chunk row (ETSI_MAXB)
+RESERVE = 256     # dibits ahead of a streaming row: the previous chunk's unconsumed tail (<= 509 bits)
+MARGIN = 8        # y samples a streaming window re-computes before the first new output
 BURST_NDB_N, BURST_NDB_P, BURST_SB = 0, 1, 2
 
 Q_BITS = np.array([1, 0, 1, 1, 0, 1, 1, 1, 0, 0, 0, 0, 0, 1, 1, 0, 1, 0, 1, 1, 0, 1], np.uint8)
@@ -62,6 +68,11 @@ def lib():
         L.eo_om_grouped.argtypes = [f32p, ctypes.c_long, ctypes.c_int, ctypes.c_int, f32p, f32p]
         L.eo_sync.argtypes = [u8p, ctypes.c_int, i32p, i32p, ctypes.c_int]
         L.eo_sync.restype = ctypes.c_int
+        L.eo_sync_from.argtypes = [u8p, ctypes.c_int, ctypes.c_int, i32p, i32p, ctypes.c_int, i32p]
+        L.eo_sync_from.restype = ctypes.c_int
+        L.eo_timing_stream.argtypes = [f32p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_float,
+                                       ctypes.c_float, f32p, f32p, i8p, u8p, ctypes.c_int, f32p]
+        L.eo_timing_stream.restype = ctypes.c_int
         L.eo_decide.argtypes = [f32p, ctypes.c_int, u8p]
         _bound = True
     return L
@@ -259,6 +270,22 @@ class Receiver:
     def demod(self, x):
         return self.timing(self.chanfilt(x))
 
+    def timing_stream(self, y, yoff, trk):
+        """eo_timing_stream: the timing stage on one streaming window (trk: a TRACK record, updated)."""
+        d = self.d
+        yv = np.ascontiguousarray(np.asarray(y, np.complex64)).view(np.float32)
+        M2 = len(yv) // 2
+        smax = M2 // 4 + 3
+        sym = np.zeros(2 * smax, np.float32)
+        dscr = np.zeros(2 * smax, np.float32)
+        soft = np.zeros(2 * smax, np.int8)
+        hard = np.zeros(smax, np.uint8)
+        diag = np.zeros(4, np.float32)
+        S = lib().eo_timing_stream(yv, M2, int(yoff), trk.ctypes.data, d["gain"], d["soft_scale"], sym, dscr, soft,
+                                   hard, smax, diag)
+        return (sym[:2 * S].view(np.complex64).copy(), soft[:2 * max(S - 1, 0)].copy(),
+                hard[:max(S - 1, 0)].copy(), diag)
+
     @staticmethod
     def om_quarters(y):
         """Oerder-Meyr class sums of one chunk in the fused demod's order (eo_om_quarters)."""
@@ -337,6 +364,30 @@ class Receiver:
             out.append((s, bk, dec))
         return out
 
+    def sync_from(self, hard, start, maxb=MAXB):
+        """eo_sync_from over a row's dibits from bit `start`: ([(start, kind)], first position not examined)."""
+        bits = np.ascontiguousarray(self.hard_bits(hard))
+        starts = np.zeros(maxb, np.int32)
+        kinds = np.zeros(maxb, np.int32)
+        stop = np.zeros(1, np.int32)
+        n = lib().eo_sync_from(bits, len(bits), int(start), starts, kinds, maxb, stop)
+        return list(zip(starts[:n].tolist(), kinds[:n].tolist())), int(stop[0])
+
+    def decode_bursts(self, softbits, bursts, cell_init):
+        cell = scramble_seq(cell_init, 432)
+        bsch = scramble_seq(3, 120)
+        sb = np.asarray(softbits, np.int8)
+        out = []
+        for s, bk in bursts:
+            if bk == BURST_NDB_N:
+                blocks = [(0, np.concatenate([sb[s + 14:s + 230], sb[s + 282:s + 498]]), cell)]
+            elif bk == BURST_NDB_P:
+                blocks = [(1, sb[s + 14:s + 230], cell), (1, sb[s + 282:s + 498], cell)]
+            else:
+                blocks = [(2, sb[s + 94:s + 214], bsch), (1, sb[s + 282:s + 498], cell)]
+            out.append((s, bk, [(k,) + self.decode_block(v, k, scr) for k, v, scr in blocks]))
+        return out
+
     def lower_mac_acquire(self, softbits, hard, cell_init):
         """Cell acquisition: the chunk's BSCH blocks first (colour code 0); the last CRC-good one
         sets the cell, with which every SCH block of the chunk is then decoded.  Returns
@@ -350,3 +401,77 @@ class Receiver:
                 if ok:
                     init = bsch_cell_init(t)
         return self.lower_mac(softbits, hard, init), init
+
+
+# ------------------------------------------------------------------------------ streaming receiver
+
+def stream_lengths(d, n):
+    """(M1, M2) of the first n samples of a stream (tetra_etsi_lengths)."""
+    m1 = (n - d["L1"]) // d["q1"] + 1 if n >= d["L1"] else 0
+    num = d["up"] * m1 - 1 - (d["Lp"] - 1)
+    return m1, (num // d["down"] + 1 if num >= 0 else 0)
+
+
+class Stream:
+    """CPU restatement of the streaming receiver (tetra_etsi_stream_window + tetra_demod_etsi_stream +
+    tetra_lmac_etsi_stream) for one channel: consecutive chunks of one continuous capture decode as
+    one symbol stream -- the channel filter over a window that re-reads the previous chunk's last
+    samples (aligned so the polyphase phases equal a run over the whole capture), the timing loop
+    (base, delta, last symbol) carried, and the lower MAC's greedy burst scan resumed at the bit it
+    stopped at with the unconsumed dibits of the previous chunk in front of the new ones.
+
+    The window of a chunk: with P = q1 down input samples per `up` outputs, s = P floor((y_done -
+    MARGIN) / up) (0 for the first chunk), window = capture[s, x_total), yoff = y_done - up s / P."""
+
+    def __init__(self, fs=FS_NOMINAL, cell_init=None):
+        self.rx = Receiver(fs)
+        d = self.rx.d
+        self.P, self.up = d["q1"] * d["down"], d["up"]
+        self.buf = np.zeros(0, np.complex64)
+        self.x_total = self.y_done = 0
+        self.trk = np.zeros(1, TRACK)
+        self.tail_hard = np.zeros(0, np.uint8)
+        self.tail_soft = np.zeros(0, np.int8)
+        self.phase = 0
+        self.acquire = cell_init is None
+        self.cell = 0 if cell_init is None else int(cell_init)
+
+    def window(self, n):
+        """(s, W, yoff, y_start) of the next chunk of n samples (global sample / y indices)."""
+        s = self.P * ((self.y_done - MARGIN) // self.up) if self.y_done > 0 else 0
+        s = max(s, 0)
+        y_start = self.up * s // self.P
+        return s, self.x_total + n - s, self.y_done - y_start, y_start
+
+    def push(self, x):
+        """One chunk (complex64, even length) -> dict(y, symbols, soft, hard, bursts, stop, ...)."""
+        x = np.asarray(x, np.complex64)
+        s, W, yoff, y_start = self.window(len(x))
+        self.buf = np.concatenate([self.buf, x])
+        self.x_total += len(x)
+        y = self.rx.chanfilt(self.buf[s:self.x_total])
+        _, m_hi = stream_lengths(self.rx.d, self.x_total)
+        assert len(y) == max(m_hi - y_start, 0), (len(y), m_hi, y_start)
+        sym, soft, hard, diag = self.rx.timing_stream(y, yoff, self.trk[0:1])
+        self.y_done = max(m_hi, self.y_done)
+        # the lower MAC: the tail dibits, then the new ones; scan from the carried phase
+        T = len(self.tail_hard)
+        row_h = np.concatenate([self.tail_hard, hard])
+        row_s = np.concatenate([self.tail_soft, soft])
+        if self.acquire:   # BSCH first (colour code 0): the last CRC-good one sets the cell
+            bursts, stop = self.rx.sync_from(row_h, self.phase)
+            for b0, bk in bursts:
+                if bk == BURST_SB:
+                    t1, ok = self.rx.decode_block(row_s[b0 + 94:b0 + 214], 2, scramble_seq(3, 120))
+                    if ok:
+                        self.cell = bsch_cell_init(t1)
+        bursts, stop = self.rx.sync_from(row_h, self.phase)
+        dec = self.rx.decode_bursts(row_s, bursts, self.cell)
+        d0 = stop // 2
+        th, ts, ph = row_h[d0:], row_s[2 * d0:], stop & 1
+        if len(th) > RESERVE:   # (only past MAXB bursts in one row) keep the last RESERVE dibits
+            th, ts, ph = th[-RESERVE:], ts[-2 * RESERVE:], 0
+        self.tail_hard, self.tail_soft, self.phase = th.copy(), ts.copy(), ph
+        return dict(y=y, yoff=yoff, window=(s, W), symbols=sym, soft=soft, hard=hard, diag=diag,
+                    bursts=[(b - 2 * T, k, dd) for b, k, dd in dec], cell=self.cell, stop=stop - 2 * T,
+                    track=self.trk.copy())

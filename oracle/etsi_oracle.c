@@ -341,25 +341,58 @@ void eo_om_grouped(const float *row, long s, int M2, int U, const float *P, floa
     }
 }
 
-/* eo_timing with the Oerder-Meyr class sums given (om != NULL) or computed in the quarter order. */
-int eo_timing_om(const float *y, int M2, const float *om, float gain, float soft_scale, float *soft_sym, float *dscr,
-                 int8_t *softbits, uint8_t *hard, int smax, float *diag)
+/* Streaming state of one channel across consecutive chunks (include/tetra_hip.h tetra_etsi_track):
+ * base = the next symbol's Gardner base position in y samples relative to the END of the previous
+ * chunk's outputs, delta = the loop offset, (pr, pi) = the last symbol, acquired = 0 until the
+ * Oerder-Meyr acquisition has run. */
+typedef struct {
+    float base, delta, pr, pi;
+    int32_t acquired, reserved[3];
+} eo_track;
+
+/* The timing stage on one window of y (4 samples/symbol, M2 samples).
+ *   trk == NULL or !trk->acquired: Oerder-Meyr feed-forward phase over the window, delta = 0, the
+ *     first symbol starts a new differential chain (the non-streaming receiver);
+ *   trk->acquired: the loop continues: base = trk->base + yoff (yoff = window index of the first
+ *     output the previous chunk did not have), delta carried, symbol 0 of the output is the carried
+ *     last symbol, so dibit 0 spans the chunk seam.
+ * Then block-Gardner tracking (64 symbols per block) and the per-chunk CFO / soft scale.  soft_sym
+ * [smax] cf32 symbol-spaced samples; softbits [2*smax] int8; hard [smax] dibits; diag[0..3] = base,
+ * final delta, rotation (re, im).  Returns S = symbols in the output (dibits = S-1); trk (if given)
+ * is updated for the next chunk. */
+static int timing_core(const float *y, int M2, const float *om, int yoff, eo_track *trk, float gain, float soft_scale,
+                       float *soft_sym, float *dscr, int8_t *softbits, uint8_t *hard, int smax, float *diag)
 {
-    if (M2 < 16) return 0;
-    float acc[4];
-    if (om)
-        memcpy(acc, om, sizeof acc);
-    else
-        eo_om_quarters(y, M2, acc);
-    float Xr = acc[0] - acc[2], Xi = acc[3] - acc[1];
-    float p = -0.63661977236758134f * pat2(Xi, Xr);   /* -(2/pi) arg X */
-    float base = p < 0.0f ? p + 4.0f : p;
-    if (base >= 4.0f) base -= 4.0f;
-    int kstart = base >= 3.0f ? 0 : 1;
-    float delta = 0.0f;
-    int S = 0;
-    float prev_r = 0.f, prev_i = 0.f;
-    int have_prev = 0;
+    const int acq = trk && trk->acquired;
+    if (M2 < 16) {
+        if (acq) trk->base = trk->base + (float)(yoff - M2);
+        return 0;
+    }
+    float base, delta;
+    int kstart, J0;
+    if (acq) {
+        base = trk->base + (float)yoff;
+        delta = trk->delta;
+        kstart = 0;
+        J0 = 1;
+    } else {
+        float acc[4];
+        if (om)
+            memcpy(acc, om, sizeof acc);
+        else
+            eo_om_quarters(y, M2, acc);
+        float Xr = acc[0] - acc[2], Xi = acc[3] - acc[1];
+        float p = -0.63661977236758134f * pat2(Xi, Xr);   /* -(2/pi) arg X */
+        base = p < 0.0f ? p + 4.0f : p;
+        if (base >= 4.0f) base -= 4.0f;
+        kstart = base >= 3.0f ? 0 : 1;
+        delta = 0.0f;
+        J0 = 0;
+    }
+    int S = J0;
+    float prev_r = acq ? trk->pr : 0.f, prev_i = acq ? trk->pi : 0.f;
+    int have_prev = J0;
+    if (J0 && smax > 0) { soft_sym[0] = prev_r; soft_sym[1] = prev_i; }
     for (int kb = kstart;; kb += 64) {
         float off = base + delta;
         float on[64][2], mid[64][2], ev[64], pv[64];
@@ -411,7 +444,7 @@ int eo_timing_om(const float *y, int M2, const float *om, float gain, float soft
     float zr[64], zi[64], am[64];
     for (int l = 0; l < 64; ++l) { zr[l] = 0.f; zi[l] = 0.f; am[l] = 0.f; }
     for (int j = 1; j < S; ++j) {
-        int l = j & 63;
+        int l = (j - J0) & 63;   /* the tracking lane of d_j: symbols J0 + 64 b + l */
         float dr = dscr[2 * (j - 1)], di = dscr[2 * (j - 1) + 1];
         float sr = fmaf(dr, dr, -(di * di)), si = (dr * di) * 2.0f;
         float qr = fmaf(sr, sr, -(si * si)), qi = (sr * si) * 2.0f;
@@ -442,7 +475,31 @@ int eo_timing_om(const float *y, int M2, const float *om, float gain, float soft
         hard[j - 1] = (uint8_t)(((xi < 0.0f) << 1) | (xr < 0.0f));
     }
     if (diag) { diag[0] = base; diag[1] = delta; diag[2] = rr; diag[3] = ri; }
+    if (trk) {
+        const int Snew = S - J0;
+        if (acq || S > 0) {
+            trk->base = base + (float)(4 * (kstart + Snew) - M2);
+            trk->delta = delta;
+            trk->pr = prev_r;
+            trk->pi = prev_i;
+            trk->acquired = 1;
+        }
+    }
     return S;
+}
+
+/* eo_timing with the Oerder-Meyr class sums given (om != NULL) or computed in the quarter order. */
+int eo_timing_om(const float *y, int M2, const float *om, float gain, float soft_scale, float *soft_sym, float *dscr,
+                 int8_t *softbits, uint8_t *hard, int smax, float *diag)
+{
+    return timing_core(y, M2, om, 0, NULL, gain, soft_scale, soft_sym, dscr, softbits, hard, smax, diag);
+}
+
+/* The streaming form (tetra_demod_etsi_stream's timing): trk carried from chunk to chunk. */
+int eo_timing_stream(const float *y, int M2, int yoff, eo_track *trk, float gain, float soft_scale, float *soft_sym,
+                     float *dscr, int8_t *softbits, uint8_t *hard, int smax, float *diag)
+{
+    return timing_core(y, M2, NULL, yoff, trk, gain, soft_scale, soft_sym, dscr, softbits, hard, smax, diag);
 }
 
 int eo_timing(const float *y, int M2, float gain, float soft_scale, float *soft_sym, float *dscr, int8_t *softbits,
@@ -467,10 +524,11 @@ static int match_at(const uint8_t *bits, int pos, const uint8_t *pat, int n)
 /* Burst detection over hard bits: kinds 0 NDB(n) -> SCH/F, 1 NDB(p) -> 2xSCH/HD, 2 SB -> BSCH+SCH/HD.
  * Score = head q11..q22 @0 + training @244 (n/p) or @214 (y) + tail q1..q10 @500.
  * Greedy scan: first start with NDB >= 40/44 or SB >= 54/60, then skip 500 bits. */
-int eo_sync(const uint8_t *bits, int nbits, int *starts, int *kinds, int maxb)
+int eo_sync_from(const uint8_t *bits, int nbits, int start, int *starts, int *kinds, int maxb, int *stop)
 {
     int nb = 0;
-    for (int s = 0; s + 510 <= nbits && nb < maxb;) {
+    int s = start;
+    for (; s + 510 <= nbits && nb < maxb;) {
         int ht = match_at(bits, s, Q_BITS + 10, 12) + match_at(bits, s + 500, Q_BITS, 10);
         int mn = ht + match_at(bits, s + 244, N_BITS, 22);
         int mp = ht + match_at(bits, s + 244, P_BITS, 22);
@@ -488,7 +546,13 @@ int eo_sync(const uint8_t *bits, int nbits, int *starts, int *kinds, int maxb)
             ++s;
         }
     }
+    if (stop) *stop = s;   /* the first position not examined: the streaming tail starts here */
     return nb;
+}
+
+int eo_sync(const uint8_t *bits, int nbits, int *starts, int *kinds, int maxb)
+{
+    return eo_sync_from(bits, nbits, 0, starts, kinds, maxb, NULL);
 }
 
 /* Differential decision on given symbol-spaced samples (interleaved re/im, n samples): hard[n-1]

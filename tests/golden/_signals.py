@@ -116,3 +116,28 @@ def scanner_input(z, i):
         return (q[:, 0].astype(np.float32) / 32768 + 1j * (q[:, 1].astype(np.float32) / 32768)).astype(np.complex64)
     rep, off = (int(v) for v in z[f"r_{i}"])
     return np.repeat(z[f"p_{i}"][z[f"k_{i}"]], rep)[off:]
+
+
+# ---------------------------------------------------------------- compat form sweep
+SWEEP_FAMILIES = ("tetra", "tetra_clean", "noise", "tone", "stress")
+SWEEP_AFC = 2.4e6 / 2048   # the AFC bin of /root/reference/tetraear/ui/modern.py:1956-1974
+
+
+def sweep_chunks(seed, n_chunks=40, n=131072, fs=2.4e6):
+    """The GUI's call pattern (modern.py:1919,2029: one 131072-sample chunk per process() call, an AFC
+    offset of k bins, |k| <= 10) as a seeded stream: default_rng(777000 + seed) draws, per chunk, a
+    family, an offset and the family's samples, in that order.  Yields (chunk, family, offset,
+    complex64 samples, int16 [n, 2] SC16 image)."""
+    rng = np.random.default_rng(777000 + seed)
+    for k in range(n_chunks):
+        fam = SWEEP_FAMILIES[int(rng.integers(0, len(SWEEP_FAMILIES)))]
+        fo = SWEEP_AFC * int(rng.integers(-10, 11))
+        x, iq = family(fam, rng, n, fs)
+        yield k, fam, fo, x, iq
+
+
+def sweep_chunk(seed, chunk, n=131072, fs=2.4e6):
+    """One chunk of sweep_chunks (the stream is regenerated up to it)."""
+    for k, fam, fo, x, iq in sweep_chunks(seed, chunk + 1, n, fs):
+        if k == chunk:
+            return fam, fo, x, iq

@@ -78,6 +78,9 @@ def run_chain(fs, x, freq_offset):
     return out
 
 
+SWEEP_CASES = ((0, 2), (28, 15), (33, 13), (15, 3), (24, 22), (34, 27), (36, 25))
+
+
 def g1():
     rng = np.random.default_rng(20260130)
     cases = []
@@ -104,6 +107,22 @@ def g1():
         for key in keys:
             arrays[f"c{i}_{key}"] = np.asarray(r[key])
         meta.append(dict(family=fam, fs=fs, n=n, freq_offset=off, q=r["q"], dec_ok=r["dec_ok"],
+                         dtypes={k: str(np.asarray(r[k]).dtype) for k in
+                                 ("hard", "symbols", "decimated", "shifted", "filtered")}))
+    # round 6: GUI chunks from the compat form sweep (_signals.sweep_chunks,
+    # tests/test_compat_default_form.py) where the opt-in time-blocked decimator leaves the 1e-5 bar
+    # or flips a decision -- (seed, chunk) 0/2, 28/15, 33/13 of this generator -- and the four
+    # (seed, chunk) indices VERDICT r5 named for its own generator (15/3, 24/22, 34/27, 36/25),
+    # regenerated with this one: the reference's own outputs on them
+    for seed, chunk in SWEEP_CASES:
+        fam, off, x, iq = _signals.sweep_chunk(seed, chunk)
+        r = run_chain(2.4e6, x, off)
+        i = len(meta)
+        arrays[f"c{i}_iq"] = iq
+        for key in ("hard", "symbols", "decimated"):
+            arrays[f"c{i}_{key}"] = np.asarray(r[key])
+        meta.append(dict(family=fam, fs=2.4e6, n=len(x), freq_offset=off, q=r["q"], dec_ok=r["dec_ok"],
+                         sweep=[seed, chunk],
                          dtypes={k: str(np.asarray(r[k]).dtype) for k in
                                  ("hard", "symbols", "decimated", "shifted", "filtered")}))
     # direct method calls as the reference tests make them (test_signal_processor.py)
@@ -315,7 +334,7 @@ def g2(g1_arrays, g1_meta):
     rng = np.random.default_rng(7)
     streams = crafted_streams(rng)
     for i, m in enumerate(g1_meta):
-        if len(g1_arrays[f"c{i}_hard"]) >= 255:
+        if len(g1_arrays[f"c{i}_hard"]) >= 255 and "sweep" not in m:   # (the round-6 sweep cases: g1 only)
             streams.append(g1_arrays[f"c{i}_hard"])
     streams += mac_streams(np.random.default_rng(20261017))   # round 3: decode_frame's MAC stage
     arrays = {}

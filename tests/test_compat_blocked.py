@@ -2,13 +2,14 @@
 decimate_blocked) against the reference's own fixtures, on the CPU.
 
 The blocked form is not scipy's operation order, so it cannot be bit-exact with the reference; the
-bar is: on every G1 case it would serve, .symbols within 1e-5
-of the reference's and no hard decision different outside a 1e-6 rad band around the decision
-thresholds (the count of positions in that band is reported), so the sync positions and frames
-decode() finds equal the reference's.  tetra_demod_compat serves it by default for C <= 64
-channels and q <= 16 (oracle.blocked_fits); the one G1 case at q = 83 (20 MSps), where the cheby1
-band is narrow enough for the noise to reach 5.7e-5, keeps the sequential decimator -- checked here
-too, so the limit is measured, not assumed."""
+bar it was held to in round 5 is: on every G1 case it would serve, .symbols within
+1e-5 of the reference's and no hard decision different outside a 1e-6 rad band around the decision
+thresholds.  The G1 fixtures meet it; a wider sweep does not (1.45e-5 and 3 flips in 1.61 M
+symbols, tests/test_compat_default_form.py), so since round 6 the latency form is opt-in only
+(decimator="blocked", TETRA_COMPAT_BLOCKED) and these tests pin what it computes, not a default.
+The one G1 case at q = 83 (20 MSps), where the cheby1 band is narrow enough for the noise to reach
+5.7e-5, is outside its limits (the product refuses it there) -- checked here too, so the limit is
+measured, not assumed."""
 import numpy as np
 import pytest
 
@@ -34,10 +35,19 @@ def test_blocked_oracle_within_the_fp32_noise_of_the_reference(g1):
     z, meta = g1
     served = ties = 0
     worst = 0.0
+    outside = []
     for i, m in enumerate(meta):
         x = iq_to_c64(z[f"c{i}_iq"])
         q = int(m["q"])
         if not m["dec_ok"] or q < 2:
+            continue
+        if "sweep" in m:   # round 6: the reference's outputs on the sweep chunks the bar fails on
+            p = O.SignalProcessor(m["fs"], decimator="blocked")
+            hard = p.process(x, m["freq_offset"])
+            err = float(np.max(np.abs(p.symbols - z[f"c{i}_symbols"])))
+            flips = int(np.sum(hard != z[f"c{i}_hard"]))
+            if err > 1e-5 or flips:
+                outside.append((tuple(m["sweep"]), err, flips))
             continue
         p = O.SignalProcessor(m["fs"], decimator="blocked")
         hard = p.process(x, m["freq_offset"])
@@ -54,8 +64,12 @@ def test_blocked_oracle_within_the_fp32_noise_of_the_reference(g1):
             ties += int(nb.sum())
         else:
             assert q > O.SB_MAXQ and err > 1e-5, (i, m, err)   # the measured reason for the limit
-    print(f"blocked decimator: {served} G1 cases served, worst |d symbols| {worst:.2e}, {ties} tie-band positions")
+    print(f"blocked decimator: {served} G1 cases served, worst |d symbols| {worst:.2e}, {ties} tie-band positions; "
+          f"outside the bar on the reference's sweep chunks: {outside}")
     assert served >= 20 and worst < 5e-6
+    # why the latency form is opt-in only: against the reference itself it leaves the bar on three
+    # GUI chunks of the round-6 sweep (a flip at symbol 817 / 867, 1.008e-5 on .symbols)
+    assert {o[0] for o in outside} >= {(0, 2), (28, 15), (33, 13)}, outside
 
 
 def test_library_table_equals_the_oracle_table():
@@ -92,15 +106,18 @@ def test_blocked_edges_against_sequential(n):
 
 
 def test_blocked_chain_within_float64_rounding_of_filtfilt(g1):
-    """The latency mode's whole chain (oracle, decimator="auto" as one process() call runs it):
-    time-blocked decimate where it fits and time-blocked filtfilt, against the reference fixtures --
+    """The latency mode's whole chain (oracle, decimator="blocked" within its limits as the product
+    runs it): time-blocked decimate where it fits and time-blocked filtfilt, against the reference fixtures --
     the filtfilt part is float64, so with a sequential decimator (the 20 MSps case) it stays within
     1e-12 of the reference; every served case within 1e-5 and no decision off outside the band."""
     z, meta = g1
     n = 0
     for i, m in enumerate(meta):
+        if "sweep" in m:
+            continue   # outside the bar by construction (previous test)
         x = iq_to_c64(z[f"c{i}_iq"])
-        p = O.SignalProcessor(m["fs"], decimator="auto")
+        fits = m["dec_ok"] and m["q"] >= 2 and O.blocked_fits(1, len(x), m["q"])
+        p = O.SignalProcessor(m["fs"], decimator="blocked" if fits or not m["dec_ok"] or m["q"] < 2 else "sequential")
         hard = p.process(x, m["freq_offset"])
         want, wh = z[f"c{i}_symbols"], z[f"c{i}_hard"]
         assert p.symbols.dtype == want.dtype and p.symbols.shape == want.shape, (i, m)

@@ -124,3 +124,40 @@ print("ok")
     r = subprocess.run([sys.executable, "-c", code, os.path.join(REPO, "tetraear-bladerf_amd")], cwd="/",
                        env=_clean_env(), capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr[-3000:] + r.stdout
+
+
+def test_second_copy_of_the_build_is_not_the_reference(tmp_path):
+    """a second copy of this build on sys.path (an installed wheel beside the source tree)
+    must not be taken for the reference -- its parser would delegate back to the overlay and recurse.
+    TETRAEAR_OVERLAY=0 turns the path scan off (only TETRAEAR_REFERENCE_ROOT is then consulted)."""
+    import shutil
+    copy = tmp_path / "site"
+    shutil.copytree(os.path.join(REPO, "tetraear-bladerf_amd", "tetraear"), copy / "tetraear",
+                    ignore=shutil.ignore_patterns("__pycache__", "*.so"))
+    fake = tmp_path / "ref"
+    (fake / "tetraear").mkdir(parents=True)
+    (fake / "tetraear" / "__init__.py").write_text("")
+    code = r"""
+import os, sys
+sys.path.insert(0, sys.argv[1])
+sys.path.append(sys.argv[2])
+from tetraear import _overlay
+pk = _overlay.reference_packages()
+assert not any(os.path.isfile(os.path.join(p, "_overlay.py")) for p in pk), pk
+if sys.argv[3] == "scan":
+    assert pk == [os.path.realpath(os.path.join(sys.argv[4], "tetraear"))], pk
+else:
+    assert pk == [], pk
+print("ok")
+"""
+    pkg = os.path.join(REPO, "tetraear-bladerf_amd")
+    for mode, env in (("scan", _clean_env()), ("off", _clean_env(TETRAEAR_OVERLAY="0"))):
+        r = subprocess.run([sys.executable, "-c", code, pkg, str(copy), mode, str(fake)], cwd="/",
+                           env=env, capture_output=True, text=True, timeout=120)
+        # the fake reference sits after the copy on the path in "scan" mode
+        if mode == "scan":
+            r = subprocess.run([sys.executable, "-c", code.replace("sys.path.append(sys.argv[2])",
+                                                                   "sys.path.append(sys.argv[2]); sys.path.append(sys.argv[4])"),
+                                pkg, str(copy), mode, str(fake)], cwd="/", env=env, capture_output=True, text=True,
+                               timeout=120)
+        assert r.returncode == 0 and r.stdout.strip() == "ok", (mode, r.stderr[-3000:] + r.stdout)

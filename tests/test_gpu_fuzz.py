@@ -8,7 +8,8 @@ hard decisions bit-exact outside the 1e-9 rad tie band (test_gpu_compat.py); the
 the counted decision-edge ulps (test_scanner.py); gate statistics within GATE_DB_TOL and decisions
 outside that band (test_spectrum.py); the channeliser within Y_TOL (test_wideband.py).
 
-Covered: compat batches (latency and throughput kernels) and the direct SignalProcessor methods,
+Covered: the default compat process() against the sequential (reference-order) oracle, compat
+batches (latency and throughput kernels) and the direct SignalProcessor methods,
 compat decoder streams, the ETSI chain with its lower MAC (cell given and acquired) and its component
 methods, the scanner detector, the AFC gate, the wideband channeliser, device-tensor batches.  Each
 host-side bug the sweep found keeps its case here ("sweep").
@@ -71,6 +72,37 @@ def test_compat_random_geometry_vs_oracle(seed):
         assert np.max(np.abs(p.symbols - soft[0, :ns[0]])) <= SOFT_TOL
     o = O.SignalProcessor(fs, decimator=decimator)
     _hard_equal(h1, o.process(x[0], fo[0]), o.symbols)
+
+
+@pytest.mark.parametrize("seed", range(10 * SCALE))
+def test_default_process_vs_reference_order(seed):
+    """Cross-form: what an unchanged caller gets -- SignalProcessor(fs).process()
+    on one GUI chunk and process_batch on a few -- against the SEQUENTIAL oracle (scipy's order,
+    pinned to the reference's fixtures), never against the oracle of the same form.  Chunks of the
+    round-6 form sweep (_signals.sweep_chunks: the GUI's chunk size, families and AFC offsets);
+    soft symbols within 1e-5 and every hard decision equal, no tie band.  A time-blocked default
+    fails this on the sweep's known cases (tests/test_compat_default_form.py)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import _signals
+    from tetraear.signal import SignalProcessor
+    chunks = list(_signals.sweep_chunks(seed, 4))
+    p = SignalProcessor(2.4e6)
+    want = []
+    for k, fam, fo, x, _ in chunks:
+        o = O.SignalProcessor(2.4e6, decimator="sequential")
+        h = o.process(x, fo)
+        want.append((h, o.symbols))
+        got = p.process(x, fo)
+        case = (seed, k, fam, fo)
+        assert p.symbols.dtype == o.symbols.dtype and len(p.symbols) == len(o.symbols), case
+        assert np.max(np.abs(p.symbols - o.symbols)) <= SOFT_TOL, case
+        assert np.array_equal(got, h), case + (np.flatnonzero(got != h)[:8],)
+    hard, soft, ns = p.process_batch(np.stack([c[3] for c in chunks]), [c[2] for c in chunks])
+    for (h, sym), k in zip(want, range(len(chunks))):
+        assert ns[k] == len(sym) and np.max(np.abs(soft[k, :ns[k]] - sym)) <= SOFT_TOL, (seed, k)
+        assert np.array_equal(hard[k, :ns[k] - 1], h), (seed, k)
 
 
 @pytest.mark.parametrize("seed", range(42 * SCALE))

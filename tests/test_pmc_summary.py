@@ -92,10 +92,43 @@ def test_no_markers_falls_back_to_last_k(tmp_path):
     assert d["kernels"][K16]["timed_launches"] == 2 and d["kernels"][K16]["timed_avg_ns"] == 1100
 
 
-def test_bench_lookup_prefers_in_window_entry():
+def test_bench_lookup_prefers_in_window_entry(tmp_path):
     """bench.traffic_from_profiles picks, among a short name's full-name entries, the one with timed
-    launches (the committed r05 summaries)."""
+    launches."""
     sys.path.insert(0, REPO)
     import bench
-    t = bench.traffic_from_profiles("k_chanfilt_r", "8192 channels x 131072 cf32")
-    assert t is not None and t["source"].startswith("r0") and t["bytes"] > 8e9
+    launches = [(K16B, 900), (K16B, 900), (K16, 1000), (K16, 1200)]
+    d = _run(str(tmp_path), launches, {K16: (1000.0, 10.0), K16B: (5000.0, 0.0)})
+    d["workload"] = "wl"
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    json.dump(d, open(prof / "r09_y_summary.json", "w"))
+    t = bench.traffic_from_profiles("k_chanfilt_r", "wl", profiles=str(prof))
+    assert t["bytes"] == 1024 * (2 * 1000 + 10) and t["rocprof_avg_ms"] == 0.0011
+
+
+def test_summaries_carry_source_provenance_and_bench_rejects_stale(tmp_path):
+    """a summary names the hash of the source its kernels were built from, and
+    bench.traffic_from_profiles cites it only while that source is unchanged -- else bytes None with
+    the reason (no silent fallback to an older profile of other code)."""
+    sys.path.insert(0, REPO)
+    import bench
+    src = P.kernel_source("k_chanfilt_r")
+    assert src and src["file"] == "etsi_rx.hip" and len(src["sha256"]) == 64
+    assert P.kernel_source("k_sos_fwd_bank")["file"] == "compat_demod.hip"
+    assert P.kernel_source("no_such_kernel") is None
+    launches = [(K16, 500), (K16, 500), (K16, 1000), (K16, 1200)]
+    d = _run(str(tmp_path), launches, {K16: (1000.0, 10.0)})
+    assert d["kernels"][K16]["source"] == src
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    d["workload"] = "C5 shard: 8 channels x 4 cf32"
+    json.dump(d, open(prof / "r09_x_summary.json", "w"))
+    t = bench.traffic_from_profiles("k_chanfilt_r", "8 channels x 4 cf32", profiles=str(prof))
+    assert t["bytes"] == 1024 * (2 * 1000 + 10) and t["source"] == "r09_x_summary.json"
+    d["kernels"][K16]["source"] = dict(src, sha256="0" * 64)   # profiled on other code
+    json.dump(d, open(prof / "r09_x_summary.json", "w"))
+    t = bench.traffic_from_profiles("k_chanfilt_r", "8 channels x 4 cf32", profiles=str(prof))
+    assert t["bytes"] is None and "other code" in t["reason"]
+    t = bench.traffic_from_profiles("k_chanfilt_r", "no such workload", profiles=str(prof))
+    assert t["bytes"] is None and "no rocprofv3" in t["reason"]

@@ -22,6 +22,7 @@ struct DevBuf {
 enum Slot {
     S_IN0 = 0, S_IN1, S_IN2, S_IN3, S_IN4, S_IN5,          // staged host inputs
     S_OUT0, S_OUT1, S_OUT2, S_OUT3, S_OUT4, S_OUT5,        // staged host outputs
+    S_OUT6, S_OUT7, S_OUT8, S_OUT9,                        // (the streaming lower MAC stages nine)
     S_W0, S_W1, S_W2, S_W3, S_W4, S_W5, S_W6, S_W7,        // kernel workspaces
     S_W8, S_W9, S_W10,                                     // wideband channeliser
     S_W11,                                                 // waterfall window + twiddles
@@ -62,8 +63,9 @@ struct tetra_ctx {
     void (*fft_free)(void *) = nullptr;
     bool wf_tables_ready = false;      // waterfall tables uploaded to slot S_W11
     std::vector<double> sosb_tab;      // compat time-blocked decimator: Phi^(2^r) table as last uploaded
-    int sosb_key = -1;                 // ... for this (q, precision)
-    const void *sosb_dev = nullptr;    // ... to this address (slot S_W16)
+    double sosb_coef[24] = {0};        // ... built from these SOS rows (the plan is a public struct:
+    bool sosb_valid = false;           //     the same q may come with other coefficients)
+    const void *sosb_dev = nullptr;    // ... to this address (slot S_W16; cleared when ws() reallocates it)
     void *pin = nullptr;               // pinned host arena: small staged copies go through it (Staging)
     size_t pin_cap = 0;
     bool pin_busy = false;             // a copy through the arena may still be in flight
@@ -151,5 +153,5 @@ __device__ __forceinline__ uint2 ld_nt(const uint2 *p) {
 // the launch (y [C][M2] to HBM), and the kernel symbol (tetra_etsi_kernel_info).
 const char *etsi_generic_unsupported(const tetra_etsi_plan *P);
 int launch_chanfilt_generic(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *x, int fmt, size_t C, size_t N,
-                            int64_t M1, int64_t M2, float2 *y);
+                            int64_t M1, int64_t M2, float2 *y, size_t ld = 0);   // ld: row pitch (0: N)
 const void *chanfilt_generic_fn(int fmt);

@@ -1241,6 +1241,26 @@ __global__ __launch_bounds__(256) void k_mix(const TIn *__restrict__ x, Lay lx, 
     op[1] = mixed_val(xp, lx.s_n, n, 1, mix, mixc[ch], fs);
 }
 
+// The ETSI receiver's AFC mixer on a streaming window (tetra_etsi_mix): frequency_shift's
+// arithmetic (mixed_val: theta = c (n / fs) in float64, sincos, numpy's complex product) with n the
+// GLOBAL sample index n0 + i of the capture, rounded to cf32 -- so consecutive windows of one capture
+// are mixed with one continuous phase, and the first (n0 = 0) equals the chunk mixed from its start.
+__global__ __launch_bounds__(256) void k_mix_at(const float *__restrict__ x, long ld, int C, long N,
+                                                const double *__restrict__ mixc, double fs, long n0,
+                                                float *__restrict__ out) {
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int ch = (int)(gid / N);
+    const long i = gid - (long)ch * N;
+    if (ch >= C) return;
+    const float *xp = x + 2 * ((size_t)ch * ld + i);
+    const double xr = (double)xp[0], xi = (double)xp[1];
+    const double th = mixc[ch] * ((double)(n0 + i) / fs);
+    double sn, co;
+    sincos(th, &sn, &co);
+    out[2 * ((size_t)ch * N + i)] = (float)fma(xr, co, -(xi * sn));
+    out[2 * ((size_t)ch * N + i) + 1] = (float)fma(xr, sn, xi * co);
+}
+
 // ------------------------------------------------------------------ extract_symbols
 // numpy complex |z| (SIMD kernel): larger*sqrt(fma(r, r, 1)), r = smaller/larger.
 template <typename T>
@@ -1716,13 +1736,15 @@ int run_decimate_blocked(tetra_ctx *ctx, const tetra_compat_plan *P, const T *x,
         dc[i] = (double)hc[i];
     }
     for (int i = 0; i < 8; ++i) hc[24 + i] = std::is_same<T, float>::value ? (T)P->zi_f32[i] : (T)P->zi_f64[i];
-    const int key = P->q * 2 + (std::is_same<T, float>::value ? 0 : 1);
-    if (ctx->sosb_key != key || ctx->sosb_dev != (const void *)phi) {
+    // the table is a function of the 24 SOS coefficients alone (in the working precision): key the
+    // upload on them, not on q, so a caller's own plan with other coefficients never reuses it
+    if (!ctx->sosb_valid || ctx->sosb_dev != (const void *)phi || std::memcmp(ctx->sosb_coef, dc, sizeof dc) != 0) {
         ctx->sosb_tab.resize(SB_NPOW * 64);
         blocked_table(dc, ctx->sosb_tab.data());
         HIP_TRY(ctx, hipMemcpyAsync(phi, ctx->sosb_tab.data(), SB_NPOW * 64 * sizeof(double), hipMemcpyHostToDevice,
                                     ctx->stream));
-        ctx->sosb_key = key;
+        std::memcpy(ctx->sosb_coef, dc, sizeof dc);
+        ctx->sosb_valid = true;
         ctx->sosb_dev = phi;
     }
     HIP_TRY(ctx, hipMemcpyAsync(coef, hc, sizeof hc, hipMemcpyHostToDevice, ctx->stream));
@@ -1851,6 +1873,22 @@ void launch_demod(tetra_ctx *ctx, const T *sym, long stride, int C, const int32_
                            thr[0], thr[1], thr[2], thr[3], hard, hstride);
 }
 
+// Which kernels tetra_demod_compat runs for this plan and batch shape (TETRA_FORM_* bits).
+// The default (flags 0 or TETRA_COMPAT_SEQUENTIAL) is scipy's sequential operation order in both
+// recursions -- bit-identical to the reference; the time-blocked forms only under
+// TETRA_COMPAT_BLOCKED (the blocked decimator drifts up to 1.45e-5 from scipy's fp32
+// state and can flip decisions whose margin is ~1e-6 rad, so it must be asked for).
+unsigned compat_forms(const tetra_compat_plan *P, size_t C, size_t N) {
+    unsigned f = 0;
+    const long M = P->q > 1 ? ceil_div((long)N, P->q) : (long)N;
+    if (P->flags & TETRA_COMPAT_BLOCKED) {
+        if (P->q > 1 && blocked_fits((int)std::min<size_t>(C, 1 << 30), (long)N, P->q)) f |= TETRA_FORM_DEC_BLOCKED;
+        if (P->filt && lf_blocked_fits((int)std::min<size_t>(C, 1 << 30), M, P->ntaps)) f |= TETRA_FORM_LF_BLOCKED;
+    }
+    if (C >= 1 && C <= SB_MAXC) f |= TETRA_FORM_POW_PREPASS;
+    return f;
+}
+
 int check_plan(tetra_ctx *ctx, const tetra_compat_plan *P) {
     if (!P) return tetra_fail(ctx, TETRA_E_INVALID, "plan is NULL");
     if (P->sps < 1 || P->phase_step < 1) return tetra_fail(ctx, TETRA_E_INVALID, "bad sps/phase_step");
@@ -1860,6 +1898,12 @@ int check_plan(tetra_ctx *ctx, const tetra_compat_plan *P) {
 }  // namespace
 
 extern "C" {
+
+int tetra_compat_forms(const tetra_compat_plan *P, size_t C, size_t N, int32_t *forms) {
+    if (!P || !forms) return TETRA_E_INVALID;
+    *forms = (int32_t)compat_forms(P, C, N);
+    return TETRA_OK;
+}
 
 int tetra_compat_blocked_table(const tetra_compat_plan *P, int which, double *table) {
     if (!P || !table || which < 0 || which > 2) return TETRA_E_INVALID;
@@ -1918,6 +1962,20 @@ int tetra_frequency_shift(tetra_ctx *ctx, const void *iq, int fmt, size_t C, siz
     else
         hipLaunchKernelGGL(k_mix<float>, dim3(grid_for(C * N, blk)), dim3(blk), 0, ctx->stream, (const float *)x,
                            row_major(N), (int)C, (long)N, mc, (const uint8_t *)nullptr, fs, (double *)o, row_major(N));
+    return st.finish();
+}
+
+int tetra_etsi_mix(tetra_ctx *ctx, const void *iq, size_t C, size_t ld, size_t N, const double *mix_c, double fs,
+                   int64_t n0, void *out) {
+    if (!ctx || C == 0 || ld < N) return TETRA_E_INVALID;
+    if (N == 0) return TETRA_OK;
+    Staging st(ctx);
+    const float *x = (const float *)st.in(iq, ((C - 1) * ld + N) * 8);
+    const double *mc = (const double *)st.in(mix_c, C * sizeof(double));
+    float *o = (float *)st.out(out, C * N * 8);
+    if (!x || !mc || !o) return st.finish();
+    hipLaunchKernelGGL(k_mix_at, dim3(grid_for(C * N, 256)), dim3(256), 0, ctx->stream, x, (long)ld, (int)C, (long)N,
+                       mc, fs, (long)n0, o);
     return st.finish();
 }
 
@@ -2025,11 +2083,11 @@ int tetra_demod_compat(tetra_ctx *ctx, const tetra_compat_plan *P, const void *i
     if (dec) {
         void *db = ws(ctx, S_W1, grouped_elems((int)C, M) * es);
         if (!db) return TETRA_E_NOMEM;
-        // latency mode: a few channels decimate time-blocked (parallel in time, within the filter's
-        // fp32 noise of scipy); TETRA_COMPAT_SEQUENTIAL keeps the scipy-exact sequential passes
-        const bool blocked = (P->flags & TETRA_COMPAT_BLOCKED) ||
-                             (!(P->flags & TETRA_COMPAT_SEQUENTIAL) && blocked_fits((int)C, (long)N, P->q));
-        if (blocked && !blocked_fits((int)C, (long)N, P->q))
+        // scipy's sequential operation order unless the caller opts into the latency mode
+        // (TETRA_COMPAT_BLOCKED: parallel in time, within the filter's fp32 noise of scipy, not
+        // bit-exact -- see compat_forms)
+        const bool blocked = compat_forms(P, C, N) & TETRA_FORM_DEC_BLOCKED;
+        if ((P->flags & TETRA_COMPAT_BLOCKED) && !blocked_fits((int)C, (long)N, P->q))
             return tetra_fail(ctx, TETRA_E_INVALID, "time-blocked decimator: C <= %d, q <= %d, N + 54 <= %d samples",
                               SB_MAXC, SB_MAXQ, SB_MAXT * SB_B);
         if (blocked)
@@ -2050,15 +2108,16 @@ int tetra_demod_compat(tetra_ctx *ctx, const tetra_compat_plan *P, const void *i
     const void *y = d;
     Lay ly = ld;
     bool y_f64 = fmt == TETRA_CF64;
-    // latency mode (a few channels): the filtfilt passes time-blocked too, and extract_symbols'
-    // |y|^2 computed in parallel before its per-phase sums
-    const bool latency = (P->flags & TETRA_COMPAT_BLOCKED) || (!(P->flags & TETRA_COMPAT_SEQUENTIAL) && C <= SB_MAXC);
+    // latency mode (opt-in): the filtfilt passes time-blocked too (float64, ~1e-12 from scipy's
+    // order); a few channels in any mode: extract_symbols' |y|^2 computed in parallel before its
+    // per-phase sums (the same products and the same pairwise order: exact)
+    const unsigned forms = compat_forms(P, C, N);
     if (P->filt || any_mix) {
         double *fb = (double *)ws(ctx, S_W3, grouped_elems((int)C, M) * 8);
         if (!fb) return TETRA_E_NOMEM;
         if (P->filt) {
-            const bool lfb = latency && lf_blocked_fits((int)C, M, P->ntaps);
-            if ((P->flags & TETRA_COMPAT_BLOCKED) && !lfb)
+            const bool lfb = forms & TETRA_FORM_LF_BLOCKED;
+            if ((P->flags & TETRA_COMPAT_BLOCKED) && !lf_blocked_fits((int)C, M, P->ntaps))
                 return tetra_fail(ctx, TETRA_E_INVALID, "time-blocked filtfilt: C <= %d, M + 30 <= %d samples",
                                   SB_MAXC, SB_MAXT * LB_B);
             if (lfb)
@@ -2085,7 +2144,7 @@ int tetra_demod_compat(tetra_ctx *ctx, const tetra_compat_plan *P, const void *i
     }
     // stage 3+4: extract_symbols + demodulate_dqpsk (processor.py:267-271)
     void *pw = nullptr;
-    if (latency) {
+    if (forms & TETRA_FORM_POW_PREPASS) {
         pw = ws(ctx, S_W18, (size_t)C * M * (y_f64 ? 8 : 4));
         if (!pw) return TETRA_E_NOMEM;
     }

@@ -18,6 +18,7 @@ void *ws(tetra_ctx *ctx, int s, size_t bytes) {
     DevBuf &b = ctx->slot[s];
     if (bytes == 0) bytes = 16;
     if (b.bytes >= bytes) return b.p;
+    if (s == S_W16) ctx->sosb_valid = false;   // the uploaded Phi table lives in this slot
     if (b.p) {
         (void)hipStreamSynchronize(ctx->stream);
         (void)hipFree(b.p);
@@ -69,6 +70,11 @@ const void *Staging::in(const void *p, size_t bytes) {
     if (bytes == 0) return p ? p : ws(ctx, next_in++, 16);
     if (is_device_ptr(p)) return p;
     host_touched = true;
+    if (next_in > S_IN5) {
+        failed = true;
+        tetra_fail(ctx, TETRA_E_INVALID, "more than %d staged host inputs", S_IN5 - S_IN0 + 1);
+        return nullptr;
+    }
     void *d = ws(ctx, next_in++, bytes);
     void *h = d ? pin_take(bytes) : nullptr;
     if (h) memcpy(h, p, bytes);
@@ -85,6 +91,11 @@ void *Staging::out(void *p, size_t bytes) {
     if (bytes == 0) return p ? p : ws(ctx, next_out++, 16);
     if (is_device_ptr(p)) return p;
     host_touched = true;
+    if (next_out > S_OUT9) {   // never into the kernels' workspace slots
+        failed = true;
+        tetra_fail(ctx, TETRA_E_INVALID, "more than %d staged host outputs", S_OUT9 - S_OUT0 + 1);
+        return nullptr;
+    }
     void *d = ws(ctx, next_out++, bytes);
     if (!d) {
         failed = true;

@@ -28,7 +28,7 @@ __host__ __device__ inline long mstart(long kb, int up, int down) {   // first m
 }
 
 template <bool SC16>
-__global__ __launch_bounds__(256) void k_chanfilt_g(const void *__restrict__ iq, long N, int M1, int M2, int q1,
+__global__ __launch_bounds__(256) void k_chanfilt_g(const void *__restrict__ iq, long ld, int M1, int M2, int q1,
                                                     int L1, int up, int down, int Lp, int S1, int ntiles,
                                                     const float *__restrict__ taps, float2 *__restrict__ y) {
     __shared__ float2 xin[RIN];
@@ -42,20 +42,21 @@ __global__ __launch_bounds__(256) void k_chanfilt_g(const void *__restrict__ iq,
     const long m0 = mstart(k0, up, down), m1 = last ? M2 : min((long)M2, mstart(k0 + S1, up, down));
     for (int i = tid; i < L1; i += 256) h1s[i] = taps[i];
     for (int i = tid; i < Lp; i += 256) hps[i] = taps[RL1 + i];
-    // the tile's input: samples [q1 k0, q1 (k0 + nk - 1) + L1) of the channel's row
+    // the tile's input: samples [q1 k0, q1 (k0 + nk - 1) + L1) of the channel's row (rows ld samples
+    // apart: a streaming window inside a resident capture, tetra_demod_etsi_stream)
     const long base = (long)q1 * k0;
     const int nin = q1 * (nk - 1) + L1;
     if constexpr (SC16) {
         // SC16 (capture.py:241-269 wire format): int16 I/Q scaled by 1/32768 -- exact, so the
         // filter sees the cf32 values of the oracle's input
-        const uint32_t *row = reinterpret_cast<const uint32_t *>(iq) + (size_t)ch * N;
+        const uint32_t *row = reinterpret_cast<const uint32_t *>(iq) + (size_t)ch * ld;
         const float s = 1.0f / 32768.0f;
         for (int i = tid; i < nin; i += 256) {
             const uint32_t v = row[base + i];
             xin[i] = make_float2((float)(int16_t)(v & 0xFFFFu) * s, (float)(int16_t)(v >> 16) * s);
         }
     } else {
-        const float2 *row = reinterpret_cast<const float2 *>(iq) + (size_t)ch * N;
+        const float2 *row = reinterpret_cast<const float2 *>(iq) + (size_t)ch * ld;
         for (int i = tid; i < nin; i += 256) xin[i] = row[base + i];
     }
     __syncthreads();
@@ -100,7 +101,8 @@ const char *etsi_generic_unsupported(const tetra_etsi_plan *P) {
 }
 
 int launch_chanfilt_generic(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *x, int fmt, size_t C, size_t N,
-                            int64_t M1, int64_t M2, float2 *y) {
+                            int64_t M1, int64_t M2, float2 *y, size_t ld) {
+    if (ld == 0) ld = N;
     const int S1 = RT1 - ((P->Lp - 1) / P->up + 2);
     const long ntiles = (M1 + S1 - 1) / S1;
     if (ntiles <= 0 || (size_t)ntiles * C > 0x7FFFFFFFu) return tetra_fail(ctx, TETRA_E_INVALID, "grid too large");
@@ -118,10 +120,10 @@ int launch_chanfilt_generic(tetra_ctx *ctx, const tetra_etsi_plan *P, const void
     PROF(ctx, "etsi_chanfilt_g");
     const dim3 g((unsigned)(ntiles * C)), b(256);
     if (fmt == TETRA_SC16)
-        hipLaunchKernelGGL(k_chanfilt_g<true>, g, b, 0, ctx->stream, x, (long)N, (int)M1, (int)M2, P->q1, P->L1, P->up,
+        hipLaunchKernelGGL(k_chanfilt_g<true>, g, b, 0, ctx->stream, x, (long)ld, (int)M1, (int)M2, P->q1, P->L1, P->up,
                            P->down, P->Lp, S1, (int)ntiles, dt, y);
     else
-        hipLaunchKernelGGL(k_chanfilt_g<false>, g, b, 0, ctx->stream, x, (long)N, (int)M1, (int)M2, P->q1, P->L1,
+        hipLaunchKernelGGL(k_chanfilt_g<false>, g, b, 0, ctx->stream, x, (long)ld, (int)M1, (int)M2, P->q1, P->L1,
                            P->up, P->down, P->Lp, S1, (int)ntiles, dt, y);
     HIP_TRY(ctx, hipGetLastError());
     return TETRA_OK;

@@ -183,7 +183,36 @@ __device__ __forceinline__ float2 csqrt_p(float x, float y) {
 struct TrackOut {
     int S;
     float rr, ri, sc, base, delta;
+    int kstart, J0;   // first block's k; 1 when symbol 0 is the carried previous one (streaming)
+    float pr, pi;     // the last symbol
 };
+
+// Streaming input of one channel's timing (tetra_etsi_track + the window's yoff): acq = 0 is the
+// non-streaming receiver (Oerder-Meyr acquisition on the chunk, a new differential chain).
+struct TrackIn {
+    int acq;
+    float base, delta, pr, pi;
+    int yoff;
+};
+__device__ __forceinline__ TrackIn track_in(const tetra_etsi_track *t, int yoff) {
+    if (!t) return TrackIn{0, 0.f, 0.f, 0.f, 0.f, 0};
+    return TrackIn{t->acquired, t->base, t->delta, t->prev_re, t->prev_im, yoff};
+}
+// The state for the next chunk (oracle/etsi_oracle.c timing_core): the next symbol's base relative
+// to this window's end, the loop offset and the last symbol.
+__device__ __forceinline__ void track_store(tetra_etsi_track *t, const TrackIn &ti, const TrackOut &o, int M2) {
+    if (M2 < 16) {
+        if (ti.acq) t->base = ti.base + (float)(ti.yoff - M2);
+        return;
+    }
+    if (ti.acq || o.S > 0) {
+        t->base = o.base + (float)(4 * (o.kstart + o.S - o.J0) - M2);
+        t->delta = o.delta;
+        t->prev_re = o.pr;
+        t->prev_im = o.pi;
+        t->acquired = 1;
+    }
+}
 
 constexpr int CPOL_SC1 = 16;   // gfx940+ cache-policy bits: sc0 1, nt 2, sc1 16 (copy_out)
 
@@ -253,8 +282,9 @@ template <bool SPLIT = false, int RING = 0, bool LEAN = false, bool OMC = false>
 __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float gain, float soft_scale, float2 *sp,
                                                  float2 *dp, int smax, int lane, int *prog = nullptr,
                                                  const float *om = nullptr, float2 *ring = nullptr,
-                                                 uint32_t *clk = nullptr, float4 omc = float4{}) {
-    TrackOut o{0, 1.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+                                                 uint32_t *clk = nullptr, float4 omc = float4{},
+                                                 TrackIn ti = TrackIn{}) {
+    TrackOut o{0, 1.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0, 0, 0.0f, 0.0f};
     if (M2 < 16) {
         if constexpr (SPLIT) {
             if (lane == 0) __hip_atomic_store(prog, PROG_DONE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -263,9 +293,11 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
     }
     // Oerder-Meyr: class sums of |y|^2 over n mod 4, per lane as four partial sums over quarters of
     // the blocks added in order (om_part; the oracle's order) -- precomputed by four waves (om)
-    // or computed here one after the other
-    float A0, A1, A2, A3;
-    if constexpr (OMC) {
+    // or computed here one after the other.  Streaming with the loop acquired: no acquisition, the
+    // carried base (plus the window's yoff) and delta continue (oracle timing_core)
+    float A0 = 0.f, A1 = 0.f, A2 = 0.f, A3 = 0.f;
+    if (ti.acq) {
+    } else if constexpr (OMC) {
         A0 = omc.x;
         A1 = omc.y;
         A2 = omc.z;
@@ -290,15 +322,25 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
         A3 = lane_f(s, 3);
     }
     if (clk && lane == 0) clk[1] = (uint32_t)wall_clock64();   // probe: the Oerder-Meyr pass done
-    const float Xr = A0 - A2, Xi = A3 - A1;
-    const float p = -0.63661977236758134f * pat2(Xi, Xr);
-    float base = p < 0.0f ? p + 4.0f : p;
-    if (base >= 4.0f) base -= 4.0f;
-    const int kstart = base >= 3.0f ? 0 : 1;
-    float delta = 0.0f;
-    int S = 0;
-    float2 prev = make_float2(0.f, 0.f);
-    bool have_prev = false;
+    float base, delta;
+    int kstart;
+    const int J0 = ti.acq ? 1 : 0;
+    if (ti.acq) {
+        base = ti.base + (float)ti.yoff;
+        delta = ti.delta;
+        kstart = 0;
+    } else {
+        const float Xr = A0 - A2, Xi = A3 - A1;
+        const float p = -0.63661977236758134f * pat2(Xi, Xr);
+        base = p < 0.0f ? p + 4.0f : p;
+        if (base >= 4.0f) base -= 4.0f;
+        kstart = base >= 3.0f ? 0 : 1;
+        delta = 0.0f;
+    }
+    int S = J0;   // symbol 0 of a continued stream is the carried last symbol
+    float2 prev = J0 ? make_float2(ti.pr, ti.pi) : make_float2(0.f, 0.f);
+    bool have_prev = J0 != 0;
+    if (J0 && lane == 0 && smax > 0) sp[0] = prev;
     float zr = 0.f, zi = 0.f, am = 0.f;   // CFO sums over this lane's d_j
     int rel = -1;   // SPLIT: progress not yet released (published after the next block's LDS reads)
     float2 pre[4], pre2[4];   // RING: the next block's 256 samples in flight (RING 2: and the one after)
@@ -416,6 +458,10 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
     o.S = S;
     o.base = base;
     o.delta = delta;
+    o.kstart = kstart;
+    o.J0 = J0;
+    o.pr = prev.x;
+    o.pi = prev.y;
     if constexpr (SPLIT) return o;   // rr, ri, sc: cfo_consumer's
     // CFO rotation conj((-Z/|Z|)^(1/4)) and the soft scale from the mean |d|
     const float Zr = wave_sum(zr), Zi = wave_sum(zi), A = wave_sum(am);
@@ -437,9 +483,12 @@ __device__ __forceinline__ TrackOut timing_track(const float2 *y, int M2, float 
 // sums the 4th powers and magnitudes of d_j, j = l mod 64, block after block as the progress word
 // releases them -- the same per-lane order, so the same bits -- then the rotation and the soft
 // scale into *o (rr, ri, sc).
-__device__ __forceinline__ void cfo_consumer(const float2 *dp, float soft_scale, int *prog, TrackOut *o, int lane) {
+__device__ __forceinline__ void cfo_consumer(const float2 *dp, float soft_scale, int *prog, TrackOut *o, int lane,
+                                             int j0 = 0) {
+    // lane l sums d_j for j = j0 + l mod 64 (j0 = 1 when symbol 0 is a continued stream's carried one):
+    // the tracking wave's lane order
     float zr = 0.f, zi = 0.f, am = 0.f;
-    int jb = 0, S = 0;
+    int jb = j0, S = 0;
     for (;;) {
         const int v = __hip_atomic_load(prog, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
         S = v & (PROG_DONE - 1);
@@ -532,10 +581,12 @@ template <int RING = 0, bool LEAN = false, bool OMC = false>
 __device__ __forceinline__ void timing_wave(const float2 *y, int M2, float gain, float soft_scale, float2 *sp,
                                             float2 *dp, int8_t *sb, uint8_t *hp, int32_t *nsym_ch, float4 *diag_ch,
                                             int smax, int lane, float2 *ring = nullptr, uint32_t *clk = nullptr,
-                                            float4 omc = float4{}) {
+                                            float4 omc = float4{}, tetra_etsi_track *trk = nullptr, int yoff = 0) {
     if (!OMC && clk && lane == 0) clk[0] = (uint32_t)wall_clock64();   // OMC: stamped before the class sums
+    const TrackIn ti = track_in(trk, yoff);
     const TrackOut o = timing_track<false, RING, LEAN, OMC>(y, M2, gain, soft_scale, sp, dp, smax, lane, nullptr,
-                                                            nullptr, ring, clk, omc);
+                                                            nullptr, ring, clk, omc, ti);
+    if (trk && lane == 0) track_store(trk, ti, o, M2);
     if (clk && lane == 0) clk[2] = (uint32_t)wall_clock64();
     __threadfence_block();   // dp / sp written by other lanes is read below
     if constexpr (LEAN)
@@ -594,7 +645,8 @@ __global__ __launch_bounds__(64) void k_timing(const float2 *__restrict__ yall, 
                                                float2 *__restrict__ sym, float2 *__restrict__ dscr,
                                                int8_t *__restrict__ softbits, uint8_t *__restrict__ hard,
                                                int32_t *__restrict__ nsym, int smax, float4 *__restrict__ diag,
-                                               int probe, const float4 *__restrict__ om, int nchunk, int ngrp, int U) {
+                                               int probe, const float4 *__restrict__ om, int nchunk, int ngrp, int U,
+                                               tetra_etsi_track *__restrict__ trk, int yoff, int ostride) {
     __shared__ float2 ring[RING ? TRING : 1];
     const int ch = blockIdx.x;
     uint32_t *clk = probe && diag ? reinterpret_cast<uint32_t *>(diag + ch) : nullptr;
@@ -603,16 +655,18 @@ __global__ __launch_bounds__(64) void k_timing(const float2 *__restrict__ yall, 
         if (clk && threadIdx.x == 0) clk[0] = (uint32_t)wall_clock64();
         omc = om_grouped(yall, om, ch, M2, nchunk, ngrp, U, threadIdx.x);
     }
-    timing_wave<RING, LEAN, OMG>(yall + (size_t)ch * M2, M2, gain, soft_scale, sym + (size_t)ch * smax,
-                                 dscr + (size_t)ch * smax, softbits + (size_t)ch * 2 * smax, hard + (size_t)ch * smax,
-                                 nsym + ch, diag ? diag + ch : nullptr, smax, threadIdx.x, ring, clk, omc);
+    const size_t os = ostride ? (size_t)ostride : (size_t)smax;   // output rows (streaming: reserve + smax)
+    timing_wave<RING, LEAN, OMG>(yall + (size_t)ch * M2, M2, gain, soft_scale, sym + (size_t)ch * os,
+                                 dscr ? dscr + (size_t)ch * smax : nullptr, softbits + (size_t)ch * 2 * os,
+                                 hard + (size_t)ch * os, nsym + ch, diag ? diag + ch : nullptr, smax, threadIdx.x, ring,
+                                 clk, omc, trk ? trk + ch : nullptr, yoff);
 }
 // k_timing's form (same-box A/B): TETRA_TIMING_RING = 0 (the Gardner windows read straight from
 // global memory), 1 (one block ahead, default) or 2 (two); TETRA_TIMING_LEAN = 0 keeps om_part per
 // quarter for the Oerder-Meyr pass and the d_j round trip through dscr (default 1: om_all, d_j
 // recomputed from the symbols)
 using timing_fn = void (*)(const float2 *, int, float, float, float2 *, float2 *, int8_t *, uint8_t *, int32_t *, int,
-                           float4 *, int, const float4 *, int, int, int);
+                           float4 *, int, const float4 *, int, int, int, tetra_etsi_track *, int, int);
 // TETRA_TIMING_PROBE=1: with a diag buffer, each chunk's diag entry holds four 32-bit wall-clock stamps
 // (start, Oerder-Meyr done, Gardner done, end) instead of the diagnostics -- a latency probe
 static int timing_probe() {
@@ -647,7 +701,8 @@ template <> struct CfCfg<uint2> { static constexpr int s2_every = 8, lr = 2312; 
 constexpr int TPP = 107;        // RRC taps per polyphase branch (Lp = 321 = 3 x 107)
 constexpr int PFD = 2;          // k_chanfilt: input tiles in flight per workgroup (register prefetch
                                 // depth, pa/pb; 3 and 4 measured no faster)
-constexpr int YLDS = 3904;      // cf32: stage-2 outputs held in LDS (a 131072-sample chunk has 3899)
+constexpr int YLDS = 3968;      // cf32: stage-2 outputs held in LDS (a 131072-sample chunk has 3899; a
+                                // streaming window of one, the previous chunk's last samples included, <= 3945)
 // Stage 2 on the matrix cores (v_mfma_f32_16x16x4_f32: bit-for-bit a k-ordered fmaf chain).  One
 // MFMA tile: 16 columns = 8 segments x (re, im), each segment S2Q consecutive triples; row
 // i = 3q + c of a column is output 3(U + q) + c; A[i][s] = tap of x240[10U + s] for that output
@@ -695,6 +750,9 @@ struct TimingOut {
     float4 *diag;
     int smax;
     int probe;   // TETRA_TIMING_PROBE: diag holds wall-clock stamps (start, tail start, tracking done, end)
+    int ostride;                // row stride of sym / hard (softbits: 2x) -- 0: smax (streaming: reserve + smax)
+    int yoff;                   // streaming: the window index of the first new 72 kHz output
+    tetra_etsi_track *track;    // streaming: the channels' timing state (in/out), or null
 };
 
 // LDS -> global copy of n bytes by the workgroup's 256 threads, as device-scope (sc1) stores
@@ -744,27 +802,31 @@ struct TailStage {
 __device__ __forceinline__ void timing_tail(const float2 *ly, float2 *scr, const TimingOut &to, int M2, int ch,
                                             int tid, TrackOut *tro, int *prog, const TailStage *stage = nullptr,
                                             float *om = nullptr, uint32_t t0 = 0) {
-    const size_t so = (size_t)ch * to.smax;
+    const size_t so = (size_t)ch * (to.ostride ? to.ostride : to.smax);
     const bool probe = to.probe && to.diag;
     uint32_t t1 = 0, t2 = 0;
     if (probe && tid == 0) t1 = (uint32_t)wall_clock64();
-    if (om && M2 >= 16) om[tid] = om_part(ly, M2, tid >> 6, tid & 63);   // the four Oerder-Meyr parts at once
+    const TrackIn ti = track_in(to.track ? to.track + ch : nullptr, to.yoff);
+    // the four Oerder-Meyr parts at once (not for a continued stream: no acquisition)
+    if (om && M2 >= 16 && !ti.acq) om[tid] = om_part(ly, M2, tid >> 6, tid & 63);
     if (tid == 0) *prog = 0;
     __syncthreads();
     if (tid < 64) {
         __builtin_amdgcn_s_setprio(3);
         // S <= M2 / 4 + 1 < the staging size either way: the bound only guards the LDS buffer
         const TrackOut o = timing_track<true>(ly, M2, to.gain, to.soft_scale, stage ? stage->sym : to.sym + so, scr,
-                                              stage ? min(to.smax, M2 / 4 + 2) : to.smax, tid, prog, om);
+                                              stage ? min(to.smax, M2 / 4 + 3) : to.smax, tid, prog, om, nullptr,
+                                              nullptr, float4{}, ti);
         if (tid == 0) {
             tro->S = o.S;
             tro->base = o.base;
             tro->delta = o.delta;
             to.nsym[ch] = o.S;
+            if (to.track) track_store(to.track + ch, ti, o, M2);
             if (probe) t2 = (uint32_t)wall_clock64();
         }
     } else if (tid < 128) {
-        cfo_consumer(scr, to.soft_scale, prog, tro, tid & 63);
+        cfo_consumer(scr, to.soft_scale, prog, tro, tid & 63, ti.acq ? 1 : 0);
     }
     __syncthreads();
     const TrackOut o = *tro;
@@ -797,7 +859,7 @@ template <typename In> constexpr int cf_waves() { return std::is_same<In, float4
 template <typename In, bool FUSE>
 __global__ __launch_bounds__(256, cf_waves<In>()) void k_chanfilt(const In *__restrict__ iq, long N, int M1, int M2,
                                                   const float *__restrict__ h1, const float *__restrict__ afrag,
-                                                  float2 *__restrict__ y, TimingOut to) {
+                                                  float2 *__restrict__ y, TimingOut to, long ld) {
     constexpr bool YL = std::is_same<In, float4>::value;
     // cf32 keeps y in LDS (yb, 72 KB: two workgroups per CU, no y traffic); SC16 streams half the
     // bytes per sample and is bound by the workgroup's own LDS/issue chain instead, so it keeps
@@ -818,7 +880,7 @@ __global__ __launch_bounds__(256, cf_waves<In>()) void k_chanfilt(const In *__re
     const int ch = blockIdx.x;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;
-    const In *xp = iq + (size_t)ch * (N / 2);   // N even: 2 complex samples per load
+    const In *xp = iq + (size_t)ch * (ld / 2);   // N, ld even: 2 complex samples per load; rows ld apart
     float2 *yp = y + (size_t)ch * M2;           // (YL && FUSE: unused)
     int ybase = 0;   // y index of yb[0]
     // Stage-2 outputs collect in yb and go out in one coalesced burst when the channel is done (or
@@ -1056,8 +1118,9 @@ constexpr int WLR = 568;                    // wave stage-1 buffer (float2): < 5
                                             // <= 265 in the channel's last (seam) burst
 constexpr int SEAM = 112;                   // >= the 104 outputs a left neighbour's last triples need
 constexpr int UMIN = 16;                    // triples per wave at least (10 UMIN >= SEAM)
-static_assert(sizeof(TrackOut) + sizeof(int) <= 32 && (4 * WLR + 3 * SEAM) % 2 == 0, "per-wave demod LDS carving");
-constexpr int WTAIL_SM = YLDS / 4 + 2;      // the fused tail's symbols per channel at most
+static_assert(sizeof(TrackOut) + sizeof(int) <= 48 && (4 * WLR + 3 * SEAM) % 2 == 0, "per-wave demod LDS carving");
+constexpr int WTAIL_SM = YLDS / 4 + 3;      // the fused tail's symbols per channel at most (+1: a continued
+                                            // stream's carried symbol 0)
 
 // cross-lane LDS hand-off inside one wave: a wave's LDS instructions execute in order, so only the
 // compiler has to be kept from moving accesses across this point (no s_waitcnt, no s_barrier)
@@ -1095,7 +1158,7 @@ template <typename In> constexpr int r_chunks() { return 10 * r_tk<In>() * RCfg<
 // written into slot (t + 1) & 1 as they arrive, so no halo copy) + the tile's 10 TK samples
 template <typename In> constexpr int r_img16() { return (2 * RHALO + 10 * r_tk<In>()) * RCfg<In>::bps / 16; }
 template <typename In> constexpr int r_smem4() {
-    return 2 + 4 * r_img16<In>() + (4 * RCfg<In>::wlr + 3 * SEAM + YLDS) / 2;
+    return 3 + 4 * r_img16<In>() + (4 * RCfg<In>::wlr + 3 * SEAM + YLDS) / 2;
 }
 // tail staging over the freed images + stage-1 buffers: d_j, soft bits, hard dibits, O-M parts, symbols
 constexpr int r_tail_bytes() { return 19 * WTAIL_SM + 48 + 1024; }
@@ -1333,7 +1396,7 @@ __device__ __forceinline__ void fmac_rows(float &ar, float &ai, const float *xr,
 template <typename In, bool FUSE>
 __global__ __launch_bounds__(256, 2) void k_chanfilt_r(const In *__restrict__ iq, long N, int M1, int M2,
                                                        const float *__restrict__ h1, const float *__restrict__ afrag,
-                                                       float2 *__restrict__ y, TimingOut to) {
+                                                       float2 *__restrict__ y, TimingOut to, long ld) {
     constexpr bool SC16 = std::is_same<In, uint4>::value;
     constexpr int BPS = RCfg<In>::bps, PF = RCfg<In>::pf, NCH = r_chunks<In>(), NL = (NCH + 63) / 64;
     constexpr int NB = RCfg<In>::nb, TK = r_tk<In>(), TIN = 10 * TK, LR = RCfg<In>::wlr;
@@ -1342,8 +1405,8 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_r(const In *__restrict__ iq
     constexpr int IMGB = r_img16<In>() * 16;   // image bytes per wave
     using Pair = typename std::conditional<SC16, uint2, float4>::type;   // two samples
     __shared__ float4 smem[r_smem4<In>()];
-    TrackOut *tro = reinterpret_cast<TrackOut *>(smem);                        // + prog: 2 float4
-    uint8_t *img_all = reinterpret_cast<uint8_t *>(smem + 2);                  // 4 wave images
+    TrackOut *tro = reinterpret_cast<TrackOut *>(smem);                        // + prog: 3 float4
+    uint8_t *img_all = reinterpret_cast<uint8_t *>(smem + 3);                  // 4 wave images
     float2 *lin_all = reinterpret_cast<float2 *>(img_all + 4 * IMGB);          // 4 stage-1 buffers
     float2 *seam = lin_all + 4 * LR;
     const int ch = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
@@ -1382,7 +1445,7 @@ __global__ __launch_bounds__(256, 2) void k_chanfilt_r(const In *__restrict__ iq
     // it return 0 without touching memory.
     const long s0 = 10L * K0;
     const long slast = active ? min(10L * (K1 - 1) + 47, N - 1) : s0;
-    const uint8_t *xp = reinterpret_cast<const uint8_t *>(iq) + ((size_t)ch * N + s0) * BPS;
+    const uint8_t *xp = reinterpret_cast<const uint8_t *>(iq) + ((size_t)ch * ld + s0) * BPS;   // rows ld apart
     const int nbytes = active ? (int)(((slast - s0 + 1) * BPS + 15) & ~15L) : 0;
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(xp), 0, nbytes, 0x00020000);
     const int ro = lane >> 4, li = lane & 15;
@@ -1640,10 +1703,15 @@ struct SyncLds {
     unsigned long long block_old;
 };
 
+// Streaming (lead != null, tetra_lmac_etsi_stream): row c holds the previous chunk's unconsumed
+// dibits in front of column R and this chunk's from R; the scan starts at row bit lead[c] and
+// afterwards the dibits from the first bit not examined move in front of column R of the next rows
+// (nsoft / nhard), lead[c] pointing at their first bit -- oracle/etsi.py Stream.
 __device__ __forceinline__ void sync_group(SyncLds &L, int grp, const uint8_t *__restrict__ hard,
                                            const int32_t *__restrict__ nsym, int smax, int32_t *__restrict__ nburst,
                                            int32_t *__restrict__ bursts, int32_t *__restrict__ nblock,
-                                           unsigned long long *__restrict__ jcount, Job *__restrict__ jobs, int C) {
+                                           unsigned long long *__restrict__ jcount, Job *__restrict__ jobs, int C,
+                                           const int8_t *soft, int32_t *lead, int R, int8_t *nsoft, uint8_t *nhard) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ch = grp * SYNC_WAVES + wv;
     auto &words_all = L.words_all;
@@ -1654,9 +1722,18 @@ __device__ __forceinline__ void sync_group(SyncLds &L, int grp, const uint8_t *_
     uint64_t *words = words_all[wv];
     int *bstart = bstart_all[wv], *bkind = bkind_all[wv];
     const int S = ch < C ? nsym[ch] : 0;
-    int nbits = 2 * (S > 1 ? S - 1 : 0);
+    const int nd = S > 1 ? S - 1 : 0;
+    int d0 = 0, cur0 = 0, nrow = nd;   // the scan's first dibit / bit, the row's dibits from d0
+    if (lead) {
+        const int b = ch < C ? min(max(lead[ch], 0), 2 * R) : 2 * R;
+        d0 = b >> 1;
+        cur0 = b & 1;
+        nrow = R + nd - d0;
+    }
+    int nbits = 2 * nrow;
     if (nbits > LMAC_MAXBITS) nbits = LMAC_MAXBITS;
-    const uint8_t *hp = hard + (size_t)ch * smax;
+    const uint8_t *hp = hard + (size_t)ch * smax + d0;
+    const int lim = smax - d0;   // the row's symbols from hp
     // pack hard bits with ballots: a word holds 32 dibit symbols (bit 2i = b1, 2i+1 = b2), so lane j
     // of the ballot contributes bit j of the word: component j & 1 of symbol j >> 1.  Two ballots per
     // 64 symbols and no bit interleave (interleaving two 32-bit ballots was ~80 scalar 64-bit ops per
@@ -1671,8 +1748,8 @@ __device__ __forceinline__ void sync_group(SyncLds &L, int grp, const uint8_t *_
 #pragma unroll
     for (int u = 0; u < PK; ++u) {
         const int s = s00 + 64 * u + sl;
-        hA[u] = hp[min(s, smax - 1)];   // unconditional (in the row): no branch join waits per load
-        hB[u] = hp[min(s + 32, smax - 1)];
+        hA[u] = hp[min(s, lim - 1)];   // unconditional (in the row): no branch join waits per load
+        hB[u] = hp[min(s + 32, lim - 1)];
     }
 #pragma unroll
     for (int u = 0; u < PK; ++u) {
@@ -1690,7 +1767,8 @@ __device__ __forceinline__ void sync_group(SyncLds &L, int grp, const uint8_t *_
     }
     __syncthreads();
     int nb = 0;
-    for (int cur = 0; cur + 510 <= nbits && nb < ETSI_MAXB;) {
+    int nextpos = cur0;   // the first position not examined (streaming: where the next chunk resumes)
+    for (int cur = cur0; cur + 510 <= nbits && nb < ETSI_MAXB;) {
         const int s = cur + lane;
         int kind = -1;
         if (s + 510 <= nbits) {
@@ -1714,9 +1792,42 @@ __device__ __forceinline__ void sync_group(SyncLds &L, int grp, const uint8_t *_
             if (lane == 0) { bstart[nb] = cur + first; bkind[nb] = k; }
             ++nb;
             cur = cur + first + 500;
+            nextpos = cur;
         } else {
             cur += 64;
+            nextpos = min(cur, nbits - 509);
         }
+    }
+    if (lead && ch < C) {   // the unconsumed tail in front of the next rows' column R
+        int td0 = d0 + (nextpos >> 1), ph = nextpos & 1;
+        int T = R + nd - td0;
+        if (T > R) { td0 = nd; T = R; ph = 0; }   // (past ETSI_MAXB bursts only) keep the last R dibits
+        if (T < 0) { td0 = R + nd; T = 0; ph = 0; }
+        const uint8_t *hrow = hard + (size_t)ch * smax;
+        const int8_t *srow = soft + (size_t)ch * 2 * smax;
+        uint8_t hv[4];
+        int8_t s0[4], s1[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = lane + 64 * u;
+            hv[u] = i < T ? hrow[td0 + i] : 0;
+            s0[u] = i < T ? srow[2 * (td0 + i)] : 0;
+            s1[u] = i < T ? srow[2 * (td0 + i) + 1] : 0;
+        }
+        __builtin_amdgcn_s_waitcnt(0);   // every read done before a write (the rows may be these rows)
+        __builtin_amdgcn_wave_barrier();
+        uint8_t *nh = nhard + (size_t)ch * smax;
+        int8_t *ns = nsoft + (size_t)ch * 2 * smax;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = lane + 64 * u;
+            if (i < T) {
+                nh[R - T + i] = hv[u];
+                ns[2 * (R - T + i)] = s0[u];
+                ns[2 * (R - T + i) + 1] = s1[u];
+            }
+        }
+        if (lane == 0) lead[ch] = 2 * (R - T) + ph;
     }
     __syncthreads();
     int per[3] = {0, 0, 0};
@@ -1747,8 +1858,8 @@ __device__ __forceinline__ void sync_group(SyncLds &L, int grp, const uint8_t *_
         }
         int q = 0;
         for (int b = 0; b < nb; ++b) {
-            const int s = bstart[b], k = bkind[b];
-            bursts[((size_t)ch * ETSI_MAXB + b) * 2] = s;
+            const int s = 2 * d0 + bstart[b], k = bkind[b];   // row bit (= the soft-bit row index)
+            bursts[((size_t)ch * ETSI_MAXB + b) * 2] = s - 2 * R * (lead != nullptr);   // from the chunk's first new dibit
             bursts[((size_t)ch * ETSI_MAXB + b) * 2 + 1] = k;
             if (k == 0) {
                 jobs[next[0]++] = Job{ch, q, b, 0, 0, s + 14}; ++q;
@@ -1769,11 +1880,12 @@ __global__ __launch_bounds__(64 * SYNC_WAVES) void k_etsi_sync(const uint8_t *__
                                                   int smax, int32_t *__restrict__ nburst, int32_t *__restrict__ bursts,
                                                   int32_t *__restrict__ nblock,
                                                   unsigned long long *__restrict__ jcount, Job *__restrict__ jobs,
-                                                  int C) {
+                                                  int C, const int8_t *soft, int32_t *lead, int R, int8_t *nsoft,
+                                                  uint8_t *nhard) {
     __shared__ SyncLds L;
     const int ng = (C + SYNC_WAVES - 1) / SYNC_WAVES;
     for (int g = blockIdx.x; g < ng; g += gridDim.x) {
-        sync_group(L, g, hard, nsym, smax, nburst, bursts, nblock, jcount, jobs, C);
+        sync_group(L, g, hard, nsym, smax, nburst, bursts, nblock, jcount, jobs, C, soft, lead, R, nsoft, nhard);
         __syncthreads();   // L is reused by the next group
     }
 }
@@ -2198,6 +2310,13 @@ __global__ void k_encode_blocks(const uint8_t *__restrict__ type1, int F, int ki
 
 }  // namespace
 
+// A streaming window too short for the channel filter (M2 <= 0): no symbols, the acquired loops'
+// positions move to the end of the (empty) window (track_store's M2 < 16 rule).
+__global__ __launch_bounds__(256) void k_track_skip(tetra_etsi_track *__restrict__ tr, int C, int yoff, int M2) {
+    const int ch = blockIdx.x * 256 + threadIdx.x;
+    if (ch < C && tr[ch].acquired) tr[ch].base = tr[ch].base + (float)(yoff - M2);
+}
+
 // --------------------------------------------------------------------------- host side
 static void scramble_seq(uint32_t r, int n, uint8_t *out) {
     for (int i = 0; i < n; ++i) {
@@ -2256,8 +2375,11 @@ static const char *const CF_NAMES[] = {"k_chanfilt_r", "k_chanfilt_r", "k_chanfi
 
 // Stage-1 taps and the per-branch stage-2 tap table (k_chanfilt), then the launch.
 static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *x, int fmt, size_t C, size_t N,
-                           int64_t M1, int64_t M2, float2 *y, const TimingOut *fused = nullptr) {
-    if (!canonical(P)) return fused ? TETRA_E_INVALID : launch_chanfilt_generic(ctx, P, x, fmt, C, N, M1, M2, y);
+                           int64_t M1, int64_t M2, float2 *y, const TimingOut *fused = nullptr, size_t ld = 0,
+                           size_t Nk = 0) {
+    if (ld == 0) ld = N;   // row pitch in samples (streaming windows inside a resident capture: > N)
+    if (Nk == 0) Nk = N;   // the length the kernel choice sees (N + 1 keeps SC16 off the per-wave kernel)
+    if (!canonical(P)) return fused ? TETRA_E_INVALID : launch_chanfilt_generic(ctx, P, x, fmt, C, N, M1, M2, y, ld);
     static_assert(sizeof(ctx->coef_etsi) == CF_COEF * sizeof(float), "tap image size");
     float *coef = (float *)ws(ctx, S_W12, CF_COEF * 4);   // slot of its own: the image persists
     if (!coef) return TETRA_E_NOMEM;
@@ -2281,7 +2403,7 @@ static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void 
         HIP_TRY(ctx, hipMemcpyAsync(coef, ctx->coef_etsi, CF_COEF * 4, hipMemcpyHostToDevice, ctx->stream));
         ctx->coef_etsi_dev = coef;
     }
-    const CfKernel kind = chanfilt_kernel(fmt, M2, N, fused != nullptr);
+    const CfKernel kind = chanfilt_kernel(fmt, M2, Nk, fused != nullptr);
     PROF(ctx, fused ? "etsi_demod" : "etsi_chanfilt");
     const TimingOut to = fused ? *fused : TimingOut{};
     const dim3 g((unsigned)C), b(256);
@@ -2289,34 +2411,34 @@ static int launch_chanfilt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void 
     case CF_R_FUSED:
         if (fmt == TETRA_CF32)
             hipLaunchKernelGGL((k_chanfilt_r<float4, true>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1,
-                               (int)M2, coef, coef + 128, y, to);
+                               (int)M2, coef, coef + 128, y, to, (long)ld);
         else
             hipLaunchKernelGGL((k_chanfilt_r<uint4, true>), g, b, 0, ctx->stream, (const uint4 *)x, (long)N, (int)M1,
-                               (int)M2, coef + 64, coef + 128, y, to);
+                               (int)M2, coef + 64, coef + 128, y, to, (long)ld);
         break;
     case CF_R:
         if (fmt == TETRA_CF32)
             hipLaunchKernelGGL((k_chanfilt_r<float4, false>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1,
-                               (int)M2, coef, coef + 128, y, to);
+                               (int)M2, coef, coef + 128, y, to, (long)ld);
         else
             hipLaunchKernelGGL((k_chanfilt_r<uint4, false>), g, b, 0, ctx->stream, (const uint4 *)x, (long)N, (int)M1,
-                               (int)M2, coef + 64, coef + 128, y, to);
+                               (int)M2, coef + 64, coef + 128, y, to, (long)ld);
         break;
     case CF_SC16_FUSED:
         hipLaunchKernelGGL((k_chanfilt<uint2, true>), g, b, 0, ctx->stream, (const uint2 *)x, (long)N, (int)M1, (int)M2,
-                           coef, coef + 128, y, to);
+                           coef, coef + 128, y, to, (long)ld);
         break;
     case CF_SC16:
         hipLaunchKernelGGL((k_chanfilt<uint2, false>), g, b, 0, ctx->stream, (const uint2 *)x, (long)N, (int)M1,
-                           (int)M2, coef, coef + 128, y, to);
+                           (int)M2, coef, coef + 128, y, to, (long)ld);
         break;
     case CF_F4_FUSED:
         hipLaunchKernelGGL((k_chanfilt<float4, true>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1,
-                           (int)M2, coef, coef + 128, y, to);
+                           (int)M2, coef, coef + 128, y, to, (long)ld);
         break;
     default:
         hipLaunchKernelGGL((k_chanfilt<float4, false>), g, b, 0, ctx->stream, (const float4 *)x, (long)N, (int)M1,
-                           (int)M2, coef, coef + 128, y, to);
+                           (int)M2, coef, coef + 128, y, to, (long)ld);
     }
     HIP_TRY(ctx, hipGetLastError());
     return TETRA_OK;
@@ -2411,7 +2533,7 @@ int tetra_etsi_timing(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *y, s
         PROF(ctx, "etsi_timing");
         hipLaunchKernelGGL(timing_kernel(M2, smax), dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yd, (int)M2, P->gain,
                            P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg, timing_probe(),
-                           nullptr, 0, 0, 0);
+                           nullptr, 0, 0, 0, nullptr, 0, 0);
     }
     return st.finish();
 }
@@ -2438,7 +2560,8 @@ int tetra_etsi_timing_om(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *y
         hipLaunchKernelGGL(timing_kernel(M2, smax, true), dim3((unsigned)C), dim3(64), 0, ctx->stream,
                            // no d_j scratch: the LEAN form recomputes d_j from the stored symbols
                            (const float2 *)yd, (int)M2, P->gain, P->soft_scale, (float2 *)so, nullptr, sbo, ho, no,
-                           (int)smax, (float4 *)dg, timing_probe(), (const float4 *)omd, (int)nchunk, (int)ngrp, U);
+                           (int)smax, (float4 *)dg, timing_probe(), (const float4 *)omd, (int)nchunk, (int)ngrp, U,
+                           nullptr, 0, 0);
     }
     return st.finish();
 }
@@ -2488,7 +2611,89 @@ int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *i
         PROF(ctx, "etsi_timing");
         hipLaunchKernelGGL(timing_kernel(M2, smax), dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yb, (int)M2, P->gain,
                            P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg, timing_probe(),
-                           nullptr, 0, 0, 0);
+                           nullptr, 0, 0, 0, nullptr, 0, 0);
+    }
+    return st.finish();
+}
+
+int tetra_etsi_stream_window(const tetra_etsi_plan *P, int64_t x_total, int64_t y_done, int64_t n, int64_t *s,
+                             int64_t *W, int64_t *yoff, int64_t *y_done_next) {
+    if (!P || !s || !W || !yoff || !y_done_next || x_total < 0 || y_done < 0 || n < 0 || P->q1 < 1 || P->up < 1 ||
+        P->down < 1)
+        return TETRA_E_INVALID;
+    // P = q1 down input samples carry `up` outputs: a window starting at a multiple of P has the
+    // polyphase phases of a run over the whole capture, its output m is global output m + up s / P
+    const int64_t per = (int64_t)P->q1 * P->down;
+    int64_t st = 0;
+    if (y_done > 0) {
+        const int64_t a = y_done - TETRA_ETSI_MARGIN;
+        st = per * (a >= 0 ? a / P->up : -((-a + P->up - 1) / P->up));   // floor division
+        if (st < 0) st = 0;
+    }
+    int64_t m1, m2, sm;
+    tetra_etsi_lengths(P, (size_t)(x_total + n), &m1, &m2, &sm);
+    *s = st;
+    *W = x_total + n - st;
+    *yoff = y_done - P->up * (st / per);
+    *y_done_next = m2 > y_done ? m2 : y_done;
+    return TETRA_OK;
+}
+
+int tetra_demod_etsi_stream(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *iq, int fmt, size_t C, size_t ld,
+                            size_t W, int yoff, tetra_etsi_track *track, void *soft, int8_t *softbits, uint8_t *hard,
+                            int32_t *nsym, size_t smax, size_t ostride, float *diag) {
+    if (!ctx) return TETRA_E_INVALID;
+    int rc = etsi_check(ctx, P);
+    if (rc) return rc;
+    int64_t M1, M2, sm;
+    tetra_etsi_lengths(P, W, &M1, &M2, &sm);
+    if (!track || C == 0 || W % 2 || ld < W || yoff < 0 || ostride < smax)
+        return tetra_fail(ctx, TETRA_E_INVALID, "demod_etsi_stream: track, W even <= ld, yoff >= 0, ostride >= smax");
+    if (fmt != TETRA_CF32 && fmt != TETRA_SC16) return tetra_fail(ctx, TETRA_E_INVALID, "iq_fmt must be cf32 or sc16");
+    if (fmt == TETRA_SC16 && ld % 2) return tetra_fail(ctx, TETRA_E_INVALID, "SC16 rows: ld even");
+    if ((int64_t)smax < sm + 1) return tetra_fail(ctx, TETRA_E_INVALID, "smax < %ld", (long)sm + 1);
+    const size_t bps = fmt == TETRA_SC16 ? 4 : 8;
+    Staging st(ctx);
+    tetra_etsi_track *tr = (tetra_etsi_track *)st.inout(track, C * sizeof(tetra_etsi_track));
+    if (M2 <= 0) {   // a window too short for the channel filter: no outputs; the loop's position moves on
+        int32_t *no = (int32_t *)st.out(nsym, C * 4);
+        if (!tr || !no) return st.finish();
+        HIP_TRY(ctx, hipMemsetAsync(no, 0, C * 4, ctx->stream));
+        hipLaunchKernelGGL(k_track_skip, dim3(grid_for(C, 256)), dim3(256), 0, ctx->stream, tr, (int)C, yoff, (int)M2);
+        return st.finish();
+    }
+    const void *x = st.in(iq, ((C - 1) * ld + W) * bps);
+    void *so = st.out(soft, C * ostride * 8);
+    int8_t *sbo = (int8_t *)st.out(softbits, C * ostride * 2);
+    uint8_t *ho = (uint8_t *)st.out(hard, C * ostride);
+    int32_t *no = (int32_t *)st.out(nsym, C * 4);
+    float *dg = diag ? (float *)st.out(diag, C * 16) : nullptr;
+    if (!tr || !x || !so || !sbo || !ho || !no) return st.finish();
+    // SC16's per-wave kernel loads 16-B groups of 4 samples: rows (ld) and the window (W) in whole groups
+    const size_t Wk = (fmt == TETRA_SC16 && ld % 4) ? W + 1 : W;   // (an odd row pitch: not per-wave)
+    const bool fuse = canonical(P) && fused_fits(fmt, M2, sm + 1, Wk);
+    if (fuse) {
+        float2 *ys = nullptr;
+        if (fmt == TETRA_SC16 && !per_wave(fmt, M2, Wk) && !(ys = (float2 *)ws(ctx, S_W3, C * (size_t)M2 * 8)))
+            return st.finish();
+        TimingOut to{P->gain, P->soft_scale, (float2 *)so, sbo, ho, no, (float4 *)dg, (int)smax, timing_probe()};
+        to.ostride = (int)ostride;
+        to.yoff = yoff;
+        to.track = tr;
+        rc = launch_chanfilt(ctx, P, x, fmt, C, W, M1, M2, ys, &to, ld, Wk);
+        if (rc) return rc;
+        return st.finish();
+    }
+    float2 *yb = (float2 *)ws(ctx, S_W3, C * (size_t)M2 * 8);
+    float2 *dscr = (float2 *)ws(ctx, S_W4, C * smax * 8);
+    if (!yb || !dscr) return st.finish();
+    rc = launch_chanfilt(ctx, P, x, fmt, C, W, M1, M2, yb, nullptr, ld, Wk);
+    if (rc) return rc;
+    {
+        PROF(ctx, "etsi_timing");
+        hipLaunchKernelGGL(timing_kernel(M2, smax), dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yb,
+                           (int)M2, P->gain, P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg,
+                           timing_probe(), nullptr, 0, 0, 0, tr, yoff, (int)ostride);
     }
     return st.finish();
 }
@@ -2555,7 +2760,8 @@ int tetra_etsi_encode_blocks(tetra_ctx *ctx, const uint8_t *type1, size_t F, int
 // The lower MAC's launch sequence; cell_init (device) selects acquisition, else the configured cells.
 static int lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard, const int32_t *nsym, size_t C,
                      size_t smax, uint32_t *cell_init, int32_t *nburst, int32_t *bursts, int32_t *nblock,
-                     int32_t *blocks, uint8_t *type1) {
+                     int32_t *blocks, uint8_t *type1, int32_t *lead = nullptr, int8_t *next_soft = nullptr,
+                     uint8_t *next_hard = nullptr) {
     if (!ctx || C == 0) return TETRA_E_INVALID;
     if (!cell_init && ctx->cells < C)
         return tetra_fail(ctx, TETRA_E_INVALID, "tetra_etsi_set_cells() for %zu channels first", C);
@@ -2565,8 +2771,21 @@ static int lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard
         return tetra_fail(ctx, TETRA_E_INVALID, "too many channels for one tetra_lmac_etsi call (%zu)", C);
     Staging st(ctx);
     uint32_t *ci = cell_init ? (uint32_t *)st.inout(cell_init, C * 4) : nullptr;
-    const int8_t *sb = (const int8_t *)st.in(softbits, C * smax * 2);
-    const uint8_t *hd = (const uint8_t *)st.in(hard, C * smax);
+    // streaming into the input rows themselves: host rows are staged in and back out (with the tail)
+    const bool alias = lead && next_soft == softbits;
+    const int8_t *sb = alias ? (const int8_t *)st.inout(const_cast<int8_t *>(softbits), C * smax * 2)
+                             : (const int8_t *)st.in(softbits, C * smax * 2);
+    const uint8_t *hd = alias ? (const uint8_t *)st.inout(const_cast<uint8_t *>(hard), C * smax)
+                              : (const uint8_t *)st.in(hard, C * smax);
+    // streaming: the scan state and the rows the tail goes to
+    int32_t *ld_ = lead ? (int32_t *)st.inout(lead, C * 4) : nullptr;
+    int8_t *nsb = nullptr;
+    uint8_t *nhd = nullptr;
+    if (lead) {
+        nsb = next_soft == softbits ? const_cast<int8_t *>(sb) : (int8_t *)st.inout(next_soft, C * smax * 2);
+        nhd = next_hard == hard ? const_cast<uint8_t *>(hd) : (uint8_t *)st.inout(next_hard, C * smax);
+        if (!ld_ || !nsb || !nhd) return st.finish();
+    }
     const int32_t *ns = (const int32_t *)st.in(nsym, C * 4);
     int32_t *nbo = (int32_t *)st.out(nburst, C * 4);
     int32_t *bo = (int32_t *)st.out(bursts, C * ETSI_MAXB * 2 * 4);
@@ -2599,7 +2818,8 @@ static int lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard
         HIP_TRY(ctx, hipMemsetAsync(jcount, 0, 16, ctx->stream));
         const unsigned ngrp = (unsigned)((C + SYNC_WAVES - 1) / SYNC_WAVES);
         hipLaunchKernelGGL(k_etsi_sync, dim3(ngrp), dim3(64 * SYNC_WAVES), 0,
-                           ctx->stream, hd, ns, (int)smax, nbo, bo, nko, jcount, jobs, (int)C);
+                           ctx->stream, hd, ns, (int)smax, nbo, bo, nko, jcount, jobs, (int)C, sb, ld_,
+                           lead ? TETRA_ETSI_RESERVE : 0, nsb, nhd);
     }
     // grids: the waves each kind's job capacity needs (16 blocks per trellis wave, 64 per traceback wave)
     auto vgrid = [&](int m) {
@@ -2645,6 +2865,18 @@ int tetra_lmac_etsi_acquire(tetra_ctx *ctx, const int8_t *softbits, const uint8_
                             int32_t *nblock, int32_t *blocks, uint8_t *type1) {
     if (!cell_init) return tetra_fail(ctx, TETRA_E_INVALID, "cell_init is NULL");
     return lmac_etsi(ctx, softbits, hard, nsym, C, smax, cell_init, nburst, bursts, nblock, blocks, type1);
+}
+
+int tetra_lmac_etsi_stream(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard, const int32_t *nsym,
+                           size_t C, size_t stride, int32_t *lead, int8_t *next_soft, uint8_t *next_hard,
+                           uint32_t *cell_init, int32_t *nburst, int32_t *bursts, int32_t *nblock, int32_t *blocks,
+                           uint8_t *type1) {
+    if (!lead || !next_soft || !next_hard || stride <= TETRA_ETSI_RESERVE)
+        return tetra_fail(ctx, TETRA_E_INVALID, "lmac_etsi_stream: lead, next rows and stride > TETRA_ETSI_RESERVE");
+    if ((next_soft == softbits) != (next_hard == hard))
+        return tetra_fail(ctx, TETRA_E_INVALID, "lmac_etsi_stream: next rows must both alias the inputs or neither");
+    return lmac_etsi(ctx, softbits, hard, nsym, C, stride, cell_init, nburst, bursts, nblock, blocks, type1, lead,
+                     next_soft, next_hard);
 }
 
 }  // extern "C"

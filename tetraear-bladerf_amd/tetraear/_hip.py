@@ -39,7 +39,8 @@ class CompatPlan(ctypes.Structure):
     ]
 
 
-COMPAT_SEQUENTIAL, COMPAT_BLOCKED = 1, 2   # tetra_compat_plan.flags: decimator form (0: automatic)
+COMPAT_SEQUENTIAL, COMPAT_BLOCKED = 1, 2   # tetra_compat_plan.flags: 0 = sequential (scipy-exact), 2 = latency mode
+FORM_DEC_BLOCKED, FORM_LF_BLOCKED, FORM_POW_PREPASS = 1, 2, 4   # tetra_compat_forms bits
 ETSI_FORCE_GENERIC = 1   # tetra_etsi_plan.flags: run a canonical plan on the generic-rate kernel
 
 
@@ -62,6 +63,10 @@ class WbPlan(ctypes.Structure):
 
 
 ETSI_MAXB, ETSI_MAXJ = 8, 16
+ETSI_RESERVE, ETSI_MARGIN = 256, 8   # streaming rows: dibits ahead of a chunk's; window re-computed outputs
+# struct tetra_etsi_track (include/tetra_hip.h): one channel's carried timing loop
+ETSI_TRACK = __import__("numpy").dtype([("base", "<f4"), ("delta", "<f4"), ("prev_re", "<f4"), ("prev_im", "<f4"),
+                                       ("acquired", "<i4"), ("reserved", "<i4", (3,))])
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -88,6 +93,7 @@ def _bind(L):
         "tetra_profile_read": (_i32, [_vp, ctypes.c_char_p, _sz, _vp, _vp, _i32, _i32p]),
         "tetra_compat_symbols": (ctypes.c_int64, [ctypes.POINTER(CompatPlan), _sz]),
         "tetra_compat_blocked_table": (_i32, [ctypes.POINTER(CompatPlan), _i32, _vp]),
+        "tetra_compat_forms": (_i32, [ctypes.POINTER(CompatPlan), _sz, _sz, _i32p]),
         "tetra_demod_compat": (_i32, [_vp, ctypes.POINTER(CompatPlan), _vp, _i32, _sz, _sz, _vp, _vp, _vp, _vp, _vp,
                                       _sz, _i32p]),
         "tetra_decimate": (_i32, [_vp, ctypes.POINTER(CompatPlan), _vp, _i32, _sz, _sz, _vp]),
@@ -117,6 +123,12 @@ def _bind(L):
         "tetra_etsi_kernel_info": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _i32, _sz, _i32, ctypes.c_char_p, _sz, _vp]),
         "tetra_lmac_etsi": (_i32, [_vp, _vp, _vp, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp]),
         "tetra_lmac_etsi_acquire": (_i32, [_vp, _vp, _vp, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp]),
+        "tetra_etsi_stream_window": (_i32, [ctypes.POINTER(EtsiPlan), ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                            _vp, _vp, _vp, _vp]),
+        "tetra_demod_etsi_stream": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _i32, _sz, _sz, _sz, ctypes.c_int,
+                                           _vp, _vp, _vp, _vp, _vp, _sz, _sz, _vp]),
+        "tetra_lmac_etsi_stream": (_i32, [_vp, _vp, _vp, _vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+        "tetra_etsi_mix": (_i32, [_vp, _vp, _sz, _sz, _sz, _vp, ctypes.c_double, ctypes.c_int64, _vp]),
         "tetra_etsi_decode_blocks": (_i32, [_vp, _vp, _sz, _i32, _vp, _vp, _vp]),
         "tetra_etsi_encode_blocks": (_i32, [_vp, _vp, _sz, _i32, _vp, _vp]),
         "tetra_wb_lengths": (_i32, [ctypes.POINTER(WbPlan), _sz, _vp, _vp]),

@@ -39,23 +39,36 @@ class ReferenceUnavailable(ImportError):
 _scan = (None, ())
 
 
+# files only a copy of THIS build has: such a package is never taken for the reference (a second
+# checkout or an installed wheel beside the source tree would otherwise load its own parser as "the
+# reference's" and recurse through this module again)
+_BUILD_MARKERS = ("_overlay.py", "_hip.py")
+
+
+def _is_build_copy(d):
+    return any(os.path.isfile(os.path.join(d, m)) for m in _BUILD_MARKERS)
+
+
 def reference_packages():
     """The reference's ``tetraear/`` directories: ``$TETRAEAR_REFERENCE_ROOT/tetraear`` first, then
-    every other ``tetraear`` package on ``sys.path``, in path order (never this build's own).  Cached
-    until sys.path or the variable changes (upper_mac asks once per frame)."""
+    (unless ``TETRAEAR_OVERLAY=0``) every other ``tetraear`` package on ``sys.path``, in path order --
+    never this build's own nor another copy of it.  Cached until sys.path or the variables change
+    (upper_mac asks once per frame)."""
     global _scan
-    key = (os.environ.get("TETRAEAR_REFERENCE_ROOT"), tuple(p for p in sys.path if isinstance(p, str)))
+    scan = os.environ.get("TETRAEAR_OVERLAY", "1") != "0"
+    key = (os.environ.get("TETRAEAR_REFERENCE_ROOT"), scan, tuple(p for p in sys.path if isinstance(p, str)))
     if _scan[0] == key:
         return list(_scan[1])
     roots = []
     env = os.environ.get("TETRAEAR_REFERENCE_ROOT")
     if env:
         roots.append(env)
-    roots += [p or os.getcwd() for p in sys.path if isinstance(p, str)]
+    if scan:
+        roots += [p or os.getcwd() for p in sys.path if isinstance(p, str)]
     out = []
     for r in roots:
         d = os.path.realpath(os.path.join(r, "tetraear"))
-        if d != _HERE and d not in out and os.path.isfile(os.path.join(d, "__init__.py")):
+        if d != _HERE and d not in out and os.path.isfile(os.path.join(d, "__init__.py")) and not _is_build_copy(d):
             out.append(d)
     _scan = (key, tuple(out))
     return out

@@ -56,6 +56,11 @@ class EtsiLowerMac:
         # [C] bool: a CRC-good BSCH has been decoded on the channel.  Kept apart from cell_state,
         # because an all-zero cell (MCC = MNC = CC = 0) has the init of UNKNOWN_CELL.
         self.acquired = None
+        self.reset_stream()
+
+    def reset_stream(self):
+        """decode_stream / decode start a new capture: no carried dibits."""
+        self._rows = None   # (soft rows [C, 2 stride], hard rows [C, stride], lead [C]): the carried tails
 
     @property
     def cells(self):
@@ -110,6 +115,64 @@ class EtsiLowerMac:
             c.check(c.lib.tetra_lmac_etsi(c.handle, _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(nsym), C, smax,
                                           _hip.ptr(nb), _hip.ptr(bursts), _hip.ptr(nk), _hip.ptr(blocks), _hip.ptr(t1)),
                     "tetra_lmac_etsi")
+        return self._frames(C, nb, bursts, nk, blocks, t1)
+
+    def _run_stream(self, c, C, nb, bursts, nk, blocks, t1, cells, stream):
+        """tetra_lmac_etsi_stream over stream = (soft rows, hard rows, nsym, stride, lead), with the
+        receiver's cell handling (acquisition state or configured cells) as decode_batch's."""
+        if self.acquire and cells is None:
+            if self.cell_state is None or len(self.cell_state) != C:
+                self.cell_state = np.full(C, UNKNOWN_CELL, np.uint32)
+                self.acquired = np.zeros(C, bool)
+            if self.acquired is None or len(self.acquired) != C:   # cell_state handed in from outside
+                self.acquired = np.zeros(C, bool)
+            ci = _hip.ptr(self.cell_state)
+        else:
+            cells = np.full(C, self.cell if self.cell is not None else UNKNOWN_CELL, np.uint32) if cells is None \
+                else np.ascontiguousarray(cells, np.uint32)
+            c.check(c.lib.tetra_etsi_set_cells(c.handle, _hip.ptr(cells), C), "tetra_etsi_set_cells")
+            ci = None
+        srow, hrow, ns, stride, lead = stream
+        c.check(c.lib.tetra_lmac_etsi_stream(c.handle, _hip.ptr(srow), _hip.ptr(hrow), _hip.ptr(ns), C, stride,
+                                             _hip.ptr(lead), _hip.ptr(srow), _hip.ptr(hrow), ci, _hip.ptr(nb),
+                                             _hip.ptr(bursts), _hip.ptr(nk), _hip.ptr(blocks), _hip.ptr(t1)),
+                "tetra_lmac_etsi_stream")
+        if ci is not None:
+            self.acquired |= acquired_channels(nk, blocks)
+
+    def decode_stream(self, soft, hard, nsym, cells=None):
+        """decode_batch for consecutive chunks of C continuous streams (EtsiStream.demod rows):
+        each channel's dibits the previous call left unconsumed -- from the first bit its burst scan
+        did not examine -- go in front of this chunk's, and the scan resumes there
+        (tetra_lmac_etsi_stream), so a burst across the seam is decoded whole.  Positions are
+        relative to this chunk's first dibit (negative: the burst began in the carried tail)."""
+        soft = np.ascontiguousarray(soft, np.int8)
+        hard = np.ascontiguousarray(hard, np.uint8)
+        nsym = np.ascontiguousarray(nsym, np.int32)
+        C, smax = hard.shape
+        R = _hip.ETSI_RESERVE
+        if self._rows is None or self._rows[1].shape[0] != C or self._rows[1].shape[1] < R + smax:
+            stride = R + max(smax, self._rows[1].shape[1] - R if self._rows is not None and
+                             self._rows[1].shape[0] == C else 0)
+            srow, hrow = np.zeros((C, 2 * stride), np.int8), np.zeros((C, stride), np.uint8)
+            lead = np.full(C, 2 * R, np.int32)
+            if self._rows is not None and self._rows[1].shape[0] == C:   # keep the carried tails
+                srow[:, :2 * R], hrow[:, :R] = self._rows[0][:, :2 * R], self._rows[1][:, :R]
+                lead = self._rows[2]
+            self._rows = (srow, hrow, lead)
+        srow, hrow, lead = self._rows
+        stride = hrow.shape[1]
+        hrow[:, R:R + smax] = hard
+        srow[:, 2 * R:2 * R + 2 * smax] = soft
+        nb = np.zeros(C, np.int32)
+        bursts = np.zeros((C, _hip.ETSI_MAXB, 2), np.int32)
+        nk = np.zeros(C, np.int32)
+        blocks = np.zeros((C, _hip.ETSI_MAXJ, 4), np.int32)
+        t1 = np.zeros((C, _hip.ETSI_MAXJ, 268), np.uint8)
+        self._run_stream(_hip.ctx(), C, nb, bursts, nk, blocks, t1, cells, (srow, hrow, nsym, stride, lead))
+        return self._frames(C, nb, bursts, nk, blocks, t1)
+
+    def _frames(self, C, nb, bursts, nk, blocks, t1):
         out = []
         for ch in range(C):
             frames = []
@@ -128,8 +191,12 @@ class EtsiLowerMac:
             out.append(frames)
         return out
 
-    def decode(self, symbols, soft_bits=None):
-        """One stream of hard dibit symbols (process() output in etsi mode carries soft_bits)."""
+    def decode(self, symbols, soft_bits=None, stream=True):
+        """One chunk of hard dibit symbols (process() output in etsi mode carries soft_bits).
+        ``stream`` (default): the chunk continues the stream of the previous calls (decode_stream;
+        TetraDecoder(mode='etsi').decode behind SignalProcessor(mode='etsi').process, as the
+        reference's capture loop calls them chunk after chunk); reset_stream() starts a new one.
+        ``stream=False``: the chunk on its own (decode_batch)."""
         h = np.asarray(symbols, np.uint8)
         sb = soft_bits if soft_bits is not None else getattr(symbols, "soft_bits", None)
         if sb is None:   # hard decisions only: +-64 soft values
@@ -141,4 +208,6 @@ class EtsiLowerMac:
         hard[0, :n] = h
         soft = np.zeros((1, 2 * smax), np.int8)
         soft[0, :2 * n] = np.asarray(sb, np.int8)[:2 * n]
+        if stream:
+            return self.decode_stream(soft, hard, np.array([n + 1], np.int32))[0]
         return self.decode_batch(soft, hard, np.array([n + 1], np.int32))[0]

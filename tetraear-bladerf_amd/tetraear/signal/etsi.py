@@ -103,11 +103,115 @@ class SoftSymbols(np.ndarray):
         self.soft_bits = getattr(obj, "soft_bits", None)
 
 
+RESERVE, MARGIN = _hip.ETSI_RESERVE, _hip.ETSI_MARGIN
+TRACK = _hip.ETSI_TRACK
+
+
+def stream_window(plan, x_total, y_done, n):
+    """tetra_etsi_stream_window: (s, W, yoff, y_done_next) of the next chunk of n samples."""
+    v = [ctypes.c_int64() for _ in range(4)]
+    rc = _hip.lib().tetra_etsi_stream_window(plan, int(x_total), int(y_done), int(n), *[ctypes.byref(x) for x in v])
+    if rc:
+        raise ValueError("tetra_etsi_stream_window: invalid arguments")
+    return tuple(x.value for x in v)
+
+
+class EtsiStream:
+    """The demod half of the streaming receiver: consecutive chunks of C channels' continuous
+    captures (the reference's capture loops, /root/reference/tetraear/ui/modern.py:1901-1919,
+    continuous_capture.py:20) demodulated as ONE symbol stream per channel.
+
+    Each chunk's channel filter runs over a window that starts before the chunk -- the previous
+    chunks' last samples are kept here (``HIST``) -- at a multiple of q1 * down input samples, so its
+    polyphase phases are those of a run over the whole capture (tetra_etsi_stream_window); the timing
+    loop of every channel is carried in ``track`` (tetra_etsi_track: base, delta, last symbol); the
+    AFC mixer (``freq_offsets``) runs on the window with the capture's global sample index, so its
+    phase is continuous too.  Row c of the outputs holds the carried last symbol of the previous
+    chunk first (once the channel's loop is acquired), so its nsym-1 dibits start with the one across
+    the seam -- exactly the row layout demod_batch returns, ready for EtsiLowerMac.decode_stream.
+    oracle/etsi.py Stream restates it."""
+
+    HIST = 4096   # input samples kept per channel (a window re-reads < 1600 at every supported rate)
+
+    def __init__(self, sample_rate=2.4e6, channels=1):
+        self.sample_rate = sample_rate
+        self.plan = etsi_plan(sample_rate)
+        self.C = int(channels)
+        self.reset()
+
+    def reset(self):
+        """A new capture: the next chunk acquires timing (Oerder-Meyr) and starts the chains."""
+        self.track = np.zeros(self.C, TRACK)
+        self.x_total = self.y_done = 0
+        self.hist = None
+        self.diag = None
+
+    def demod(self, iq, freq_offsets=None):
+        """[C, n] complex or [C, n, 2] int16 SC16 (n even) -> (hard [C, smax] u8, soft_bits
+        [C, 2*smax] i8, symbols [C, smax] c64, nsym [C]) of this chunk, rows as described above."""
+        iq = np.asarray(iq)
+        if iq.dtype == np.int16:
+            if iq.ndim != 3 or iq.shape[-1] != 2:
+                raise ValueError("SC16 input must be [C, N, 2] int16")
+            fmt, x = _hip.TETRA_SC16, np.ascontiguousarray(iq)
+        else:
+            fmt, x = _hip.TETRA_CF32, np.ascontiguousarray(iq, dtype=np.complex64)
+        if x.shape[0] != self.C:
+            raise ValueError(f"EtsiStream of {self.C} channels given {x.shape[0]}")
+        n = x.shape[1]
+        if n % 2:
+            raise ValueError("streaming chunks must hold an even number of samples")
+        if freq_offsets is not None and fmt == _hip.TETRA_SC16:   # the mixer takes cf32 (SC16 -> cf32 is exact)
+            x = ((x[..., 0].astype(np.float32) + 1j * x[..., 1].astype(np.float32)) / np.float32(32768)).astype(
+                np.complex64)
+            fmt = _hip.TETRA_CF32
+        if self.hist is not None and self.hist.dtype != x.dtype:
+            raise ValueError("a stream keeps its sample format")
+        s, W, yoff, y_next = stream_window(self.plan, self.x_total, self.y_done, n)
+        h = self.x_total - s
+        if h > (0 if self.hist is None else self.hist.shape[1]):
+            raise RuntimeError(f"stream window needs {h} samples of history")
+        win = x if h == 0 else np.concatenate([self.hist[:, self.hist.shape[1] - h:], x], axis=1)
+        win = np.ascontiguousarray(win)
+        c = _hip.ctx()
+        if freq_offsets is not None:
+            from tetraear.signal.processor import mixer_coefficient
+            fo = np.broadcast_to(np.asarray(freq_offsets, np.float64), (self.C,))
+            mc = np.array([mixer_coefficient(f) for f in fo], np.float64)
+            mixed = np.empty((self.C, W), np.complex64)
+            c.check(c.lib.tetra_etsi_mix(c.handle, _hip.ptr(win), self.C, W, W, _hip.ptr(mc), float(self.sample_rate),
+                                         int(s), _hip.ptr(mixed)), "tetra_etsi_mix")
+            dwin = mixed
+        else:
+            dwin = win
+        _, M2, sm = lengths(self.plan, W)
+        smax = max(sm + 1, 2)
+        sym = np.zeros((self.C, smax), np.complex64)
+        soft = np.zeros((self.C, 2 * smax), np.int8)
+        hard = np.zeros((self.C, smax), np.uint8)
+        ns = np.zeros(self.C, np.int32)
+        diag = np.zeros((self.C, 4), np.float32)
+        c.check(c.lib.tetra_demod_etsi_stream(c.handle, self.plan, _hip.ptr(dwin), fmt, self.C, W, W, int(yoff),
+                                              _hip.ptr(self.track), _hip.ptr(sym), _hip.ptr(soft), _hip.ptr(hard),
+                                              _hip.ptr(ns), smax, smax, _hip.ptr(diag)), "tetra_demod_etsi_stream")
+        keep = min(self.HIST, win.shape[1])
+        self.hist = np.ascontiguousarray(win[:, win.shape[1] - keep:])
+        self.x_total += n
+        self.y_done = y_next
+        self.diag = diag
+        return hard, soft, sym, ns
+
+
 class EtsiReceiver:
     def __init__(self, sample_rate=2.4e6):
         self.sample_rate = sample_rate
         self.plan = etsi_plan(sample_rate)
         self.diag = None
+        self._stream = None
+
+    def reset(self):
+        """process() starts a new capture (a retune): timing is acquired afresh on the next chunk."""
+        self._stream = None
 
     def demod_batch(self, iq):
         """[C, N] complex, or [C, N, 2] int16 SC16 capture samples (scaled 1/32768 in the channel
@@ -141,9 +245,28 @@ class EtsiReceiver:
         self.diag = diag
         return hard, soft, sym, ns
 
-    def process(self, samples, freq_offset=0):
-        """One chunk -> (SoftSymbols hard dibits, complex64 symbol-rate samples)."""
+    def process(self, samples, freq_offset=0, stream=True):
+        """One chunk -> (SoftSymbols hard dibits, complex64 symbol-rate samples).
+
+        ``stream`` (default): the chunk continues the capture the previous process() calls fed
+        (the reference's callers stream one capture chunk by chunk, modern.py:1901-1919): an
+        EtsiStream of one channel carries the filter history, the timing loop and the mixer phase,
+        so the symbols continue across the seam -- the returned symbols then start with the
+        previous chunk's last one and the dibits with the one across the seam (len(hard) ==
+        len(symbols) - 1 either way).  reset() starts a new capture.  ``stream=False``: the chunk on
+        its own (demod_batch)."""
         x = np.ascontiguousarray(samples, np.complex64)
+        if stream:
+            x = x[:len(x) - len(x) % 2]
+            if len(x) == 0:
+                return SoftSymbols(np.zeros(0, np.uint8), np.zeros(0, np.int8)), np.zeros(0, np.complex64)
+            if self._stream is None:
+                self._stream = EtsiStream(self.sample_rate, 1)
+            hard, soft, sym, ns = self._stream.demod(x[None, :], [freq_offset] if freq_offset else None)
+            self.diag = self._stream.diag
+            n = int(ns[0])
+            nd = max(0, n - 1)
+            return SoftSymbols(hard[0, :nd].copy(), soft[0, :2 * nd].copy()), sym[0, :n].copy()
         if freq_offset and len(x):   # AFC mixer on the GPU (same kernel as frequency_shift)
             from tetraear.signal.processor import mixer_coefficient
             out = np.empty(len(x), np.complex128)
@@ -229,6 +352,12 @@ def synth(C, N, fs=2.4e6, seed=1, snr_db=None, cfo_max=600.0, device_arrays=None
     return iq, cells, kinds, payload, t0
 
 
+def _on_stream(c):
+    """torch ops enqueued on library context c's stream (ordered with its kernels)."""
+    import torch
+    return torch.cuda.stream(torch.cuda.ExternalStream(c.lib.tetra_get_stream(c.handle)))
+
+
 class BenchStep:
     """bench.py workload: device-resident synthetic capture -> fused demod -> lower MAC."""
 
@@ -250,16 +379,38 @@ class BenchStep:
         self.plan = etsi_plan(fs)
         _, self.M2, self.smax = lengths(self.plan, N)
         # chunks > 1: every channel is one continuous capture of chunks x N samples, resident in HBM
-        # as `chunks` consecutive [C, N] batches; step k decodes batch k mod chunks, so the state the
-        # acquiring lower MAC carries into a step comes from the channel's earlier chunks -- a
-        # receiver streaming 128 Ki chunks (modern.py:1919) with the cell state of protocol.py:479-485
+        # as [C, chunks N] rows, and decoded as ONE stream (streaming receiver: step k demodulates
+        # chunk k's window -- the previous chunk's last samples re-read in place, tetra_etsi_stream_window
+        # -- with every channel's timing loop carried, and the lower MAC resumes each channel's burst
+        # scan on the dibits the previous step left unconsumed, tetra_lmac_etsi_stream), the cell
+        # state of protocol.py:479-485 kept as a receiver streaming 128 Ki chunks (modern.py:1919)
+        # does.  A run longer than the capture starts it again as a new capture (stream_resets).
         self.chunks = max(1, int(chunks))
+        self.stream = self.chunks > 1
+        if self.stream and demod != "fused":
+            raise ValueError("the streaming bench runs the fused demod")
         NT = N * self.chunks
         nb = c.lib.tetra_synth_bursts_per_channel(NT, fs)
         self.cells = torch.empty(C, dtype=torch.int32, device=device)
         self.kinds = torch.empty((C, nb), dtype=torch.int32, device=device)
         self.payload = torch.empty((C, nb, 2, 268), dtype=torch.uint8, device=device)
-        if self.chunks == 1:
+        if self.stream:
+            # synthesised straight into the capture rows, in channel slices (SC16: through a float slice)
+            sc16 = self.fmt == _hip.TETRA_SC16
+            self.cap = torch.empty((C, NT, 2), dtype=torch.int16 if sc16 else torch.float32, device=device)
+            S = max(1, min(C, (1 << 30) // NT))
+            for s0 in range(0, C, S):
+                n = min(S, C - s0)
+                dst = torch.empty((n, NT, 2), dtype=torch.float32, device=device) if sc16 else self.cap[s0:s0 + n]
+                c.check(c.lib.tetra_synth_etsi(c.handle, n, NT, fs, seed + 7919 * (s0 // S), snr_db, 600.0,
+                                               _hip.ptr(dst), _hip.ptr(self.cells[s0:]), _hip.ptr(self.kinds[s0:]),
+                                               _hip.ptr(self.payload[s0:]), None), "synth")
+                if sc16:
+                    c.synchronize()
+                    self.cap[s0:s0 + n].copy_(torch.round(dst * 32768).clamp_(-32768, 32767).to(torch.int16))
+                    del dst
+            self.iqs = [self.cap]
+        elif self.chunks == 1:
             self.iqs = [torch.empty((C, N, 2), dtype=torch.float32, device=device)]
             c.check(c.lib.tetra_synth_etsi(c.handle, C, N, fs, seed, snr_db, 600.0, _hip.ptr(self.iqs[0]),
                                            _hip.ptr(self.cells), _hip.ptr(self.kinds), _hip.ptr(self.payload), None),
@@ -282,15 +433,28 @@ class BenchStep:
         c.synchronize()   # the synthesised batches are read by torch's ops below (SC16 conversion)
         from tetraear.core.etsi import UNKNOWN_CELL
         self.cell_state = torch.full((C,), UNKNOWN_CELL, dtype=torch.int32, device=device)
-        if self.fmt == _hip.TETRA_SC16:   # the synth output is on the SC16 grid: exact
+        if self.fmt == _hip.TETRA_SC16 and not self.stream:   # the synth output is on the SC16 grid: exact
             self.iqs = [torch.round(x * 32768).clamp_(-32768, 32767).to(torch.int16) for x in self.iqs]
         self.iq = self.iqs[0]
         self.kchunk = 0
+        if self.stream:
+            # output rows: TETRA_ETSI_RESERVE dibits for the carried tail, then a window's symbols
+            # (a window is the chunk + < 1600 samples of the previous one)
+            _, self.M2, sm1 = lengths(self.plan, N + 4096)
+            self.smax = sm1 + 1
+            self.stride = RESERVE + self.smax
+            self.track = torch.zeros((C, TRACK.itemsize // 4), dtype=torch.int32, device=device)
+            self.lead = torch.full((C,), 2 * RESERVE, dtype=torch.int32, device=device)
+            self.x_total = self.y_done = 0
+            self.resets = 0
+            self.bufs = [self._stream_bufs(device) for _ in range(2)]
+            self.sym, self.soft, self.hard, self.nsym = self.bufs[0]
         sm = self.smax
-        self.sym = torch.empty((C, sm, 2), dtype=torch.float32, device=device)
-        self.soft = torch.empty((C, 2 * sm), dtype=torch.int8, device=device)
-        self.hard = torch.empty((C, sm), dtype=torch.uint8, device=device)
-        self.nsym = torch.empty(C, dtype=torch.int32, device=device)
+        if not self.stream:
+            self.sym = torch.empty((C, sm, 2), dtype=torch.float32, device=device)
+            self.soft = torch.empty((C, 2 * sm), dtype=torch.int8, device=device)
+            self.hard = torch.empty((C, sm), dtype=torch.uint8, device=device)
+            self.nsym = torch.empty(C, dtype=torch.int32, device=device)
         self.nburst = torch.empty(C, dtype=torch.int32, device=device)
         self.bursts = torch.empty((C, _hip.ETSI_MAXB, 2), dtype=torch.int32, device=device)
         self.nblock = torch.empty(C, dtype=torch.int32, device=device)
@@ -303,6 +467,14 @@ class BenchStep:
         # stream -- a Context() of its own runs on a non-blocking stream that does not wait for torch's
         c.synchronize()
         torch.cuda.current_stream(device).synchronize()
+
+    def _stream_bufs(self, device):
+        import torch
+        C, st = self.C, self.stride
+        return (torch.zeros((C, st, 2), dtype=torch.float32, device=device),
+                torch.zeros((C, 2 * st), dtype=torch.int8, device=device),
+                torch.zeros((C, st), dtype=torch.uint8, device=device),
+                torch.zeros(C, dtype=torch.int32, device=device))
 
     def pipeline(self):
         """Stream the batches through a two-stage software pipeline: the fused demod (HBM-bound
@@ -318,8 +490,9 @@ class BenchStep:
         self.back.check(self.back.lib.tetra_set_stream(self.back.handle, ctypes.c_void_p(self.s_back.cuda_stream)),
                         "set_stream")
         self.back.check(self.back.lib.tetra_etsi_set_cells(self.back.handle, _hip.ptr(self.cells), self.C), "set_cells")
-        self.bufs = [(self.sym, self.soft, self.hard, self.nsym),
-                     tuple(torch.empty_like(t) for t in (self.sym, self.soft, self.hard, self.nsym))]
+        if not self.stream:
+            self.bufs = [(self.sym, self.soft, self.hard, self.nsym),
+                         tuple(torch.empty_like(t) for t in (self.sym, self.soft, self.hard, self.nsym))]
         if self.demod_mode == "split":   # y is what crosses the streams; the symbol buffers stay on the back one
             self.y.append(torch.empty_like(self.y[0]))
         self.ev_front = [torch.cuda.Event() for _ in range(2)]
@@ -383,6 +556,9 @@ class BenchStep:
         return self.dbuf[i]
 
     def _demod(self, c, sym, soft, hard, nsym):
+        if self.stream:
+            self._demod_stream(c, sym, soft, hard, nsym)
+            return
         x = self._input()
         c.check(c.lib.tetra_demod_etsi_fmt(c.handle, self.plan, _hip.ptr(x), self.fmt, self.C, self.N,
                                            _hip.ptr(sym), _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(nsym), self.smax,
@@ -391,7 +567,42 @@ class BenchStep:
             ev, st = self._used
             ev.record(st)
 
+    def _demod_stream(self, c, sym, soft, hard, nsym):
+        """Chunk kchunk of every channel's capture: its window in place in the capture rows."""
+        k = self.kchunk % self.chunks
+        if self.kchunk and k == 0:   # past the capture's end: the same rows again, as a new capture
+            self.x_total = self.y_done = 0
+            with _on_stream(c):
+                self.track.zero_()
+            self._reset_lead = True
+            self.resets += 1
+        self.kchunk += 1
+        s, W, yoff, y_next = stream_window(self.plan, self.x_total, self.y_done, self.N)
+        bps = 4 if self.fmt == _hip.TETRA_SC16 else 8
+        _, _, sm = lengths(self.plan, W)
+        c.check(c.lib.tetra_demod_etsi_stream(
+            c.handle, self.plan, ctypes.c_void_p(self.cap.data_ptr() + bps * s), self.fmt, self.C,
+            self.N * self.chunks, W, int(yoff), _hip.ptr(self.track), ctypes.c_void_p(sym.data_ptr() + 8 * RESERVE),
+            ctypes.c_void_p(soft.data_ptr() + 2 * RESERVE), ctypes.c_void_p(hard.data_ptr() + RESERVE),
+            _hip.ptr(nsym), min(sm + 1, self.smax), self.stride, None), "demod_etsi_stream")
+        self.x_total += self.N
+        self.y_done = y_next
+
     def _lmac(self, c, soft, hard, nsym):
+        if self.stream:
+            i = [b[2].data_ptr() for b in self.bufs].index(hard.data_ptr())
+            nsoft, nhard = self.bufs[i ^ 1][1], self.bufs[i ^ 1][2]
+            if getattr(self, "_reset_lead", False):   # a new capture: no carried dibits
+                with _on_stream(c):
+                    self.lead.fill_(2 * RESERVE)
+                self._reset_lead = False
+            acq = self.cells_mode == "acquire"
+            c.check(c.lib.tetra_lmac_etsi_stream(c.handle, _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(nsym), self.C,
+                                                 self.stride, _hip.ptr(self.lead), _hip.ptr(nsoft), _hip.ptr(nhard),
+                                                 _hip.ptr(self.cell_state) if acq else None, _hip.ptr(self.nburst),
+                                                 _hip.ptr(self.bursts), _hip.ptr(self.nblock), _hip.ptr(self.blocks),
+                                                 _hip.ptr(self.type1)), "lmac_etsi_stream")
+            return
         if self.cells_mode == "acquire":
             c.check(c.lib.tetra_lmac_etsi_acquire(c.handle, _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(nsym), self.C,
                                                   self.smax, _hip.ptr(self.cell_state), _hip.ptr(self.nburst),
@@ -421,6 +632,11 @@ class BenchStep:
             if split:
                 self._chanfilt(self.c, self.y[0])
                 self._timing(self.c, self.y[0])
+            elif self.stream:   # the rows alternate: a chunk's lower MAC puts its tail in front of the next's
+                sym, soft, hard, nsym = self.bufs[self.kchunk & 1]
+                self._demod(self.c, sym, soft, hard, nsym)
+                self._lmac(self.c, soft, hard, nsym)
+                return
             else:
                 self._demod(self.c, self.sym, self.soft, self.hard, self.nsym)
             self._lmac(self.c, self.soft, self.hard, self.nsym)
@@ -470,11 +686,17 @@ class BenchStep:
         """bench.py's read floor over this batch: one row per channel at the demod kernel's own LDS
         footprint (so as many workgroups per CU as the kernel gets)."""
         row = self.N * (4 if self.fmt == _hip.TETRA_SC16 else 8)
+        if self.stream:   # rows of the resident capture are chunks N apart: the floor reads one chunk
+            x = self.cap[:, :self.N].contiguous() if not hasattr(self, "_floor_x") else self._floor_x
+            self._floor_x = x
+            return _hip.ptr(x), self.C, row, self.kernel_info()[1]
         return _hip.ptr(self.iq), self.C, row, self.kernel_info()[1]
 
     def quality(self):
         """Decoded-block statistics of the last step (device results, checked on the host); with
-        cell acquisition also how many channels hold the synthesised cell."""
+        cell acquisition also how many channels hold the synthesised cell.  Streaming: the bursts the
+        step decoded per channel against the slots on air in one chunk (N / 34000 at 2.4 MSps: a
+        255-symbol slot is 34000 samples) -- the fraction of the transmitted bursts decoded."""
         nb = self.nblock.cpu().numpy()
         blocks = self.blocks.cpu().numpy()
         ok = sum(int(blocks[i, :nb[i], 1].sum()) for i in range(self.C))
@@ -482,6 +704,13 @@ class BenchStep:
                  crc_ok_frac=round(ok / max(1, int(nb.sum())), 5))
         if self.chunks > 1:
             q["chunk"] = (self.kchunk - 1) % self.chunks   # the batch the last step decoded
+        if self.stream:
+            on_air = self.N * 18000.0 / 255.0 / self.fs
+            q["stream"] = True
+            q["bursts_per_channel_chunk"] = round(q["bursts"] / self.C, 4)
+            q["on_air_per_channel_chunk"] = round(on_air, 4)
+            q["decoded_frac"] = round(q["bursts"] / self.C / on_air, 4)
+            q["stream_resets"] = self.resets
         if self.cells_mode == "acquire":
             q["cells_acquired"] = int((self.cell_state == self.cells).sum().item())
         return q

@@ -99,6 +99,29 @@ def _fill(arr, vals):
 DECIMATORS = {"auto": 0, "sequential": _hip.COMPAT_SEQUENTIAL, "blocked": _hip.COMPAT_BLOCKED}
 
 
+def default_decimator():
+    """The compat decimator form of a SignalProcessor built without one: $TETRAEAR_COMPAT_DECIMATOR
+    (an operator's opt-in to the latency mode for unchanged callers, modern.py:1886), else "auto"
+    (= scipy's sequential order, bit-identical to the reference)."""
+    d = os.environ.get("TETRAEAR_COMPAT_DECIMATOR", "auto")
+    if d not in DECIMATORS:
+        raise ValueError(f"TETRAEAR_COMPAT_DECIMATOR must be one of {sorted(DECIMATORS)}, not {d!r}")
+    return d
+
+
+def compat_forms(plan, C, N):
+    """The kernels tetra_demod_compat runs for `plan` on a [C, N] batch (host-only query):
+    {"decimate": "blocked"|"sequential", "filtfilt": ..., "power_prepass": bool}."""
+    import ctypes
+    f = ctypes.c_int32(0)
+    if _hip.lib().tetra_compat_forms(plan, int(C), int(N), ctypes.byref(f)) != 0:
+        raise ValueError("tetra_compat_forms: invalid plan")
+    v = f.value
+    return {"decimate": "blocked" if v & _hip.FORM_DEC_BLOCKED else "sequential",
+            "filtfilt": "blocked" if v & _hip.FORM_LF_BLOCKED else "sequential",
+            "power_prepass": bool(v & _hip.FORM_POW_PREPASS)}
+
+
 _PLANS = {}   # compat_plan results of the warning-free cases (the GUI's repeated chunk shape)
 
 
@@ -107,10 +130,12 @@ def compat_plan(sample_rate, n, fmt, bandwidth=25000, decimator="auto", real=Fal
     Plans of calls that log nothing are cached by their arguments (~40 us of filter design per
     chunk otherwise); the plan is read-only to the library.
 
-    ``decimator`` picks the form of decimate's sosfiltfilt (include/tetra_hip.h, TETRA_COMPAT_*):
-    "sequential" is scipy's operation order, bit-identical to the reference; "blocked" recurses
-    256-sample tiles in parallel (latency mode, within the filter's fp32 noise of scipy); "auto"
-    lets tetra_demod_compat take the blocked form for batches of <= 64 channels at q <= 16.
+    ``decimator`` picks the form of decimate's sosfiltfilt and of filtfilt (include/tetra_hip.h,
+    TETRA_COMPAT_*): "sequential" (and "auto", the default) is scipy's operation order, bit-identical
+    to the reference; "blocked" is the opt-in latency mode -- 256-/128-sample tiles recursed in
+    parallel, ~40x lower latency for one chunk, but only within the cheby1 filter's fp32 noise of
+    scipy (up to ~1.5e-5 on .symbols near the chunk start; a decision with a ~1e-6 rad margin can
+    flip), so it is never chosen for the caller.
     ``real``: the samples are real (decimate's initial state in the real dtype).  ``cache=False``
     returns a private plan the caller may modify."""
     key = (float(sample_rate), int(n), int(fmt), bandwidth, decimator, bool(real))
@@ -171,16 +196,17 @@ def mixer_coefficient(freq_offset):
 class SignalProcessor:
     """Processes raw IQ samples for TETRA demodulation (processor.py:18)."""
 
-    def __init__(self, sample_rate=2.4e6, mode=None, decimator="auto"):
+    def __init__(self, sample_rate=2.4e6, mode=None, decimator=None):
         self.sample_rate = sample_rate
         self.symbol_rate = SYMBOL_RATE
         self.samples_per_symbol = int(sample_rate / self.symbol_rate)
         self.symbols = None
         self.mode = demod_mode(mode)
+        decimator = default_decimator() if decimator is None else decimator
         if decimator not in DECIMATORS:
             raise ValueError(f"decimator must be one of {sorted(DECIMATORS)}, not {decimator!r}")
-        # compat process(): the decimator form (compat_plan); "auto" serves a single chunk with the
-        # time-blocked (latency) form, a large batch with the scipy-exact sequential one
+        # compat process(): the decimator form (compat_plan); "auto"/"sequential" is scipy's exact
+        # order for every batch size, "blocked" the opt-in latency mode (not bit-exact)
         self.decimator = decimator
         self._etsi = None
 
@@ -401,28 +427,31 @@ class SignalProcessor:
             fo = np.zeros(C) if freq_offsets is None else np.asarray(freq_offsets, np.float64)
             mc = np.array([mixer_coefficient(f) if f != 0 else 0.0 for f in fo], np.float64)
             mo = (fo != 0).astype(np.uint8)
+        split = False
         if not plan.filt:
             # a chunk too short for filtfilt (processor.py:81-83 returns it unfiltered): the library
             # takes such a batch only with the mixer on for all channels or for none, so a mixed
             # batch runs as those two batches
             on = (mo.cpu().numpy() if hasattr(mo, "data_ptr") else mo).astype(bool)
             if on.any() and not on.all():
+                split = True
                 mc_h = mc.cpu().numpy() if hasattr(mc, "data_ptr") else mc
                 for rows in (np.flatnonzero(on), np.flatnonzero(~on)):
                     h, s, n = self._compat_rows(plan, xc, fmt, rows, mc_h[rows], on[rows], smax)
                     hard[rows], soft[rows], ns[rows] = h, s, n
-                if gate is not None:
-                    self.gate = {k: v.cpu().numpy() for k, v in gate.items()}
-                return hard, soft, ns
-        c.check(c.lib.tetra_demod_compat(c.handle, plan, _hip.ptr(xc), fmt, C, N, _hip.ptr(mc), _hip.ptr(mo),
-                                         _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(ns), smax, f32),
-                "tetra_demod_compat")
-        if f32.value:   # unfiltered cf32 without the mixer: complex64 symbols, rows smax apart
-            soft = soft.reshape(-1).view(np.complex64)[:C * smax].reshape(C, smax).astype(np.complex128)
-        if real_in and not (afc or dev_offsets):
-            # real rows without the mixer keep real symbols in the reference: decide them as process() does
+        if not split:
+            c.check(c.lib.tetra_demod_compat(c.handle, plan, _hip.ptr(xc), fmt, C, N, _hip.ptr(mc), _hip.ptr(mo),
+                                             _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(ns), smax, f32),
+                    "tetra_demod_compat")
+            if f32.value:   # unfiltered cf32 without the mixer: complex64 symbols, rows smax apart
+                soft = soft.reshape(-1).view(np.complex64)[:C * smax].reshape(C, smax).astype(np.complex128)
+        if real_in:
+            # real rows whose mixer stays off keep real symbols in the reference: decide them as
+            # process() does (real arithmetic), whichever way the offsets came -- host Hz, a device
+            # tensor or the AFC gate -- and whether or not the batch was split above
+            off = (mo.cpu().numpy() if hasattr(mo, "data_ptr") else np.asarray(mo)).astype(bool) == 0
             rt = np.float32 if (not plan.filt and fmt == _hip.TETRA_CF32) else np.float64
-            for r in np.flatnonzero(mo == 0):
+            for r in np.flatnonzero(off):
                 if ns[r] >= 2:
                     hard[r, :ns[r] - 1] = self.demodulate_dqpsk(soft[r, :ns[r]].real.astype(rt))
         if gate is not None:

@@ -4,7 +4,8 @@ call, then decode) -- the per-chunk latency against the chunk's 54.6 ms of air a
 
 Times, per chunk (median of --reps calls after warm-up):
   * etsi:   SignalProcessor(mode="etsi").process(x) + TetraDecoder(mode="etsi").decode(hard)
-  * compat: SignalProcessor().process(x, f) + TetraDecoder().decode(hard)   (the reference's semantics)
+  * compat: SignalProcessor().process(x, f) + TetraDecoder().decode(hard)   (the reference's semantics,
+            the default scipy-exact form); compat_blocked: the opt-in latency mode's process()
   * batch:  EtsiReceiver.demod_batch + EtsiLowerMac.decode_batch over C host channels at once
 Host buffers in and out (H2D / D2H included): this is the drop-in's latency, not the HBM-resident
 throughput bench.py reports.  usage: python tools/latency_c2.py [--reps 50]
@@ -60,6 +61,8 @@ def main():
     out["compat_process_ms"] = med_ms(lambda: pc.process(x, 1171.875), a.reps)
     hc = pc.process(x, 1171.875)
     out["compat_decode_ms"] = med_ms(lambda: dc.decode(hc), a.reps)
+    pb = SignalProcessor(fs, decimator="blocked")   # the opt-in latency mode (not bit-exact)
+    out["compat_blocked_process_ms"] = med_ms(lambda: pb.process(x, 1171.875), a.reps)
 
     rx, mac = EtsiReceiver(), EtsiLowerMac()
     for C in (1, 8, 64):

@@ -25,11 +25,31 @@ usage: pmc_summary.py TRACE_DIR FETCH_DIR WRITE_DIR OUT_JSON [workload] [--timed
 import collections
 import csv
 import glob
+import hashlib
 import json
+import os
 import re
 import sys
 
 MARK = "k_region_mark"
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tetraear-bladerf_amd", "csrc")
+
+
+def kernel_source(short_name, csrc=CSRC):
+    """Provenance of a kernel's code: {"file": <csrc file defining it>, "sha256": <hash of that file
+    and common.h>} or None.  pmc_summary records it per kernel; bench.py accepts a summary's bytes
+    only while the kernel's source still hashes the same, so a summary of older code is never cited
+    (VERDICT r5 item 4).  No git needed: the GPU box gets the tree without .git."""
+    pat = re.compile(r"\bvoid\s+" + re.escape(short_name) + r"\s*\(")
+    common = os.path.join(csrc, "common.h")
+    for f in sorted(glob.glob(os.path.join(csrc, "*.hip"))):
+        text = open(f, "rb").read()
+        if pat.search(text.decode("utf-8", "replace")):
+            h = hashlib.sha256(text)
+            if os.path.isfile(common):
+                h.update(open(common, "rb").read())
+            return {"file": os.path.basename(f), "sha256": h.hexdigest()}
+    return None
 FETCH_CORRECTION = 2   # calibrated at 4, 8 and 16 B per lane (docstring)
 # kernels that take their streamed input as `const void *`: element bytes per lane load
 WIDTH_OVERRIDE = {"k_waterfall": 8, "k_chanfilt_g": 8}
@@ -139,6 +159,9 @@ def main():
                      timed_max_ns=max(dur))
         wdt = load_width(k)
         e["load_bytes_per_lane"] = wdt
+        src = kernel_source(e["short"])
+        if src:
+            e["source"] = src
         if k in pmc:
             f = [v for _, v in in_window(pmc[k].get((fetch, "FETCH_SIZE"), []), pmc_win[fetch])]
             w = [v for _, v in in_window(pmc[k].get((write, "WRITE_SIZE"), []), pmc_win[write])]
