@@ -420,13 +420,17 @@ class Stream:
     (base, delta, last symbol) carried, and the lower MAC's greedy burst scan resumed at the bit it
     stopped at with the unconsumed dibits of the previous chunk in front of the new ones.
 
-    The window of a chunk: with P = q1 down input samples per `up` outputs, s = P floor((y_done -
-    MARGIN) / up) (0 for the first chunk), window = capture[s, x_total), yoff = y_done - up s / P."""
+    The window of a chunk: with P = q1 down input samples per `up` outputs (doubled when odd, so
+    windows hold whole sample pairs; then 2 up outputs), s = P floor((y_done - MARGIN) / (outputs per
+    P)) (0 for the first chunk), window = capture[s, x_total), yoff = y_done - up s / (q1 down)."""
 
     def __init__(self, fs=FS_NOMINAL, cell_init=None):
         self.rx = Receiver(fs)
         d = self.rx.d
-        self.P, self.up = d["q1"] * d["down"], d["up"]
+        # windows start at multiples of P input samples: q1 down carry `up` outputs; an even P keeps
+        # the window an even number of samples (the kernels read sample pairs)
+        self.Pb, self.up = d["q1"] * d["down"], d["up"]
+        self.P = self.Pb * (2 if self.Pb % 2 else 1)
         self.buf = np.zeros(0, np.complex64)
         self.x_total = self.y_done = 0
         self.trk = np.zeros(1, TRACK)
@@ -434,13 +438,15 @@ class Stream:
         self.tail_soft = np.zeros(0, np.int8)
         self.phase = 0
         self.acquire = cell_init is None
-        self.cell = 0 if cell_init is None else int(cell_init)
+        # before a BSCH is decoded: colour code 0 (init 3), what every receiver descrambles with
+        self.cell = scramble_init(0, 0, 0) if cell_init is None else int(cell_init)
 
     def window(self, n):
         """(s, W, yoff, y_start) of the next chunk of n samples (global sample / y indices)."""
-        s = self.P * ((self.y_done - MARGIN) // self.up) if self.y_done > 0 else 0
+        ups = self.up * self.P // self.Pb   # outputs per P input samples
+        s = self.P * ((self.y_done - MARGIN) // ups) if self.y_done > 0 else 0
         s = max(s, 0)
-        y_start = self.up * s // self.P
+        y_start = self.up * s // self.Pb
         return s, self.x_total + n - s, self.y_done - y_start, y_start
 
     def push(self, x):

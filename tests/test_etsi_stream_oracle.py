@@ -147,13 +147,14 @@ def test_product_window_arithmetic_equals_the_oracle():
     """tetra_etsi_stream_window (host code of the product, no GPU) gives the oracle's windows for
     every supported rate and chunk pattern, the first chunk, tiny chunks and chunks of one sample pair."""
     from tetraear.signal.etsi import etsi_plan, stream_window
-    for fs in (2.4e6, 1.8e6, 1.9e6, 2.1e6, 2.3e6):
+    for fs in (2.4e6, 1.8e6, 1.9e6, 2.0e6, 2.1e6, 2.2e6, 2.3e6):
         plan = etsi_plan(fs)
         st = E.Stream(fs)
         for n in (131072, 2, 40, 1200, 131072, 50002, 8, 131072):
             want = st.window(n)
             s, W, yoff, y_next = stream_window(plan, st.x_total, st.y_done, n)
             assert (s, W, yoff) == want[:3], (fs, n)
+            assert W % 2 == 0 and s % 2 == 0, (fs, n, s, W)   # whole sample pairs (the kernels' loads)
             st.x_total += n
             st.y_done = max(st.y_done, E.stream_lengths(st.rx.d, st.x_total)[1])
             assert y_next == st.y_done

@@ -843,11 +843,12 @@ def test_c5_full_shard_8192x131072():
 
 
 def test_acquire_streaming_chunks():
-    """bench.py --cells acquire: each channel is one continuous capture of 8 chunks, step k decodes
-    chunk k mod 8 with the cell state the earlier steps left (no cell configured).  After one pass
-    over the chunks every channel whose capture holds a CRC-good sync burst has acquired its cell,
-    and the next pass decodes >= 97 % of the blocks, each a transmitted payload, with the same bits
-    as the cell-given lower MAC on the same batch."""
+    """bench.py --cells acquire: each channel is one continuous capture of 8 chunks decoded as one
+    stream (timing loops carried, the lower MAC resuming on the previous chunk's unconsumed dibits),
+    with no cell configured.  By the last chunk every channel whose capture holds a CRC-good sync
+    burst has acquired its cell; the last step decodes >= 99 % of the bursts on air and >= 97 % of its
+    blocks pass the CRC, each a transmitted payload, with the same bits as the cell-given stream over
+    the same capture.  One step past the capture's end restarts it as a new capture (stream_resets)."""
     import torch
     from tetraear import _hip
     from tetraear.signal.etsi import BenchStep
@@ -855,24 +856,29 @@ def test_acquire_streaming_chunks():
     c = _hip.ctx()
     C, N, K = 1024, 131072, 8
     acq = BenchStep(c, C, N, 2.4e6, seed=55, device=dev, cells="acquire", chunks=K)
-    for _ in range(K + 3):
+    for _ in range(K):
         acq()
     torch.cuda.synchronize(dev)
     q = acq.quality()
-    assert q["chunk"] == (K + 2) % K and q["crc_ok_frac"] >= 0.97, q
+    assert q["chunk"] == K - 1 and q["crc_ok_frac"] >= 0.97 and q["stream_resets"] == 0, q
+    assert q["decoded_frac"] >= 0.99, q
     nblk, nok = _check_blocks_transmitted(acq, C)
     assert nok / nblk >= 0.97
     assert q["cells_acquired"] >= int(0.98 * C), q
-    # the same chunk through the cell-given lower MAC: identical blocks on every acquired channel
-    blocks_a, t1_a = acq.blocks.cpu().numpy(), acq.type1.cpu().numpy()
+    blocks_a, t1_a, nk_a = acq.blocks.cpu().numpy(), acq.type1.cpu().numpy(), acq.nblock.cpu().numpy()
     got = acq.cell_state.cpu().numpy() == acq.cells.cpu().numpy()
-    acq.cells_mode = "given"
-    acq.kchunk = K + 2
-    acq()
+    acq()   # past the end: a new capture from chunk 0
     torch.cuda.synchronize(dev)
-    nk, blocks_g, t1_g = acq.nblock.cpu().numpy(), acq.blocks.cpu().numpy(), acq.type1.cpu().numpy()
+    assert acq.quality()["stream_resets"] == 1
+    del acq
+    giv = BenchStep(c, C, N, 2.4e6, seed=55, device=dev, cells="given", chunks=K)
+    for _ in range(K):
+        giv()
+    torch.cuda.synchronize(dev)
+    nk, blocks_g, t1_g = giv.nblock.cpu().numpy(), giv.blocks.cpu().numpy(), giv.type1.cpu().numpy()
     for ch in np.nonzero(got)[0]:
         k = int(nk[ch])
+        assert k == int(nk_a[ch]), ch
         assert np.array_equal(blocks_a[ch, :k], blocks_g[ch, :k]) and np.array_equal(t1_a[ch, :k], t1_g[ch, :k]), ch
 
 

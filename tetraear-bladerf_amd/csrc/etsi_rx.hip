@@ -1703,6 +1703,39 @@ struct SyncLds {
     unsigned long long block_old;
 };
 
+// Streaming: the dibits (and their soft bits) the scan left unconsumed -- from row dibit td0, T of
+// them -- go in front of column R of the next rows, and lead[c] to their first unexamined bit (one
+// wave).  Into other rows straight from k_etsi_sync; into these rows (tinfo) by k_etsi_tail, after
+// the trellis has read them.
+__device__ __forceinline__ void tail_move(const uint8_t *hard, const int8_t *soft, int stride, int ch, int td0, int T,
+                                          int ph, int R, uint8_t *nhard, int8_t *nsoft, int32_t *lead, int lane) {
+    const uint8_t *hrow = hard + (size_t)ch * stride;
+    const int8_t *srow = soft + (size_t)ch * 2 * stride;
+    uint8_t hv[4];
+    int8_t s0[4], s1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = lane + 64 * u;
+        hv[u] = i < T ? hrow[td0 + i] : 0;
+        s0[u] = i < T ? srow[2 * (td0 + i)] : 0;
+        s1[u] = i < T ? srow[2 * (td0 + i) + 1] : 0;
+    }
+    __builtin_amdgcn_s_waitcnt(0);   // every read done before a write (the rows may be these rows)
+    __builtin_amdgcn_wave_barrier();
+    uint8_t *nh = nhard + (size_t)ch * stride;
+    int8_t *ns = nsoft + (size_t)ch * 2 * stride;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = lane + 64 * u;
+        if (i < T) {
+            nh[R - T + i] = hv[u];
+            ns[2 * (R - T + i)] = s0[u];
+            ns[2 * (R - T + i) + 1] = s1[u];
+        }
+    }
+    if (lane == 0) lead[ch] = 2 * (R - T) + ph;
+}
+
 // Streaming (lead != null, tetra_lmac_etsi_stream): row c holds the previous chunk's unconsumed
 // dibits in front of column R and this chunk's from R; the scan starts at row bit lead[c] and
 // afterwards the dibits from the first bit not examined move in front of column R of the next rows
@@ -1711,7 +1744,8 @@ __device__ __forceinline__ void sync_group(SyncLds &L, int grp, const uint8_t *_
                                            const int32_t *__restrict__ nsym, int smax, int32_t *__restrict__ nburst,
                                            int32_t *__restrict__ bursts, int32_t *__restrict__ nblock,
                                            unsigned long long *__restrict__ jcount, Job *__restrict__ jobs, int C,
-                                           const int8_t *soft, int32_t *lead, int R, int8_t *nsoft, uint8_t *nhard) {
+                                           int32_t *lead, int R, int32_t *tinfo, const int8_t *soft, uint8_t *nhard,
+                                           int8_t *nsoft) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ch = grp * SYNC_WAVES + wv;
     auto &words_all = L.words_all;
@@ -1798,36 +1832,17 @@ __device__ __forceinline__ void sync_group(SyncLds &L, int grp, const uint8_t *_
             nextpos = min(cur, nbits - 509);
         }
     }
-    if (lead && ch < C) {   // the unconsumed tail in front of the next rows' column R
+    if (lead && ch < C) {   // the unconsumed tail
         int td0 = d0 + (nextpos >> 1), ph = nextpos & 1;
         int T = R + nd - td0;
         if (T > R) { td0 = nd; T = R; ph = 0; }   // (past ETSI_MAXB bursts only) keep the last R dibits
         if (T < 0) { td0 = R + nd; T = 0; ph = 0; }
-        const uint8_t *hrow = hard + (size_t)ch * smax;
-        const int8_t *srow = soft + (size_t)ch * 2 * smax;
-        uint8_t hv[4];
-        int8_t s0[4], s1[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = lane + 64 * u;
-            hv[u] = i < T ? hrow[td0 + i] : 0;
-            s0[u] = i < T ? srow[2 * (td0 + i)] : 0;
-            s1[u] = i < T ? srow[2 * (td0 + i) + 1] : 0;
+        if (nhard) {   // other rows (double-buffered): moved here, the trellis reads only these rows
+            tail_move(hard, soft, smax, ch, td0, T, ph, R, nhard, nsoft, lead, lane);
+        } else if (lane == 0) {   // these rows: k_etsi_tail moves it after the trellis has read them
+            tinfo[2 * ch] = td0;
+            tinfo[2 * ch + 1] = (T << 1) | ph;
         }
-        __builtin_amdgcn_s_waitcnt(0);   // every read done before a write (the rows may be these rows)
-        __builtin_amdgcn_wave_barrier();
-        uint8_t *nh = nhard + (size_t)ch * smax;
-        int8_t *ns = nsoft + (size_t)ch * 2 * smax;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = lane + 64 * u;
-            if (i < T) {
-                nh[R - T + i] = hv[u];
-                ns[2 * (R - T + i)] = s0[u];
-                ns[2 * (R - T + i) + 1] = s1[u];
-            }
-        }
-        if (lane == 0) lead[ch] = 2 * (R - T) + ph;
     }
     __syncthreads();
     int per[3] = {0, 0, 0};
@@ -1880,14 +1895,24 @@ __global__ __launch_bounds__(64 * SYNC_WAVES) void k_etsi_sync(const uint8_t *__
                                                   int smax, int32_t *__restrict__ nburst, int32_t *__restrict__ bursts,
                                                   int32_t *__restrict__ nblock,
                                                   unsigned long long *__restrict__ jcount, Job *__restrict__ jobs,
-                                                  int C, const int8_t *soft, int32_t *lead, int R, int8_t *nsoft,
-                                                  uint8_t *nhard) {
+                                                  int C, int32_t *lead, int R, int32_t *tinfo, const int8_t *soft,
+                                                  uint8_t *nhard, int8_t *nsoft) {
     __shared__ SyncLds L;
     const int ng = (C + SYNC_WAVES - 1) / SYNC_WAVES;
     for (int g = blockIdx.x; g < ng; g += gridDim.x) {
-        sync_group(L, g, hard, nsym, smax, nburst, bursts, nblock, jcount, jobs, C, soft, lead, R, nsoft, nhard);
+        sync_group(L, g, hard, nsym, smax, nburst, bursts, nblock, jcount, jobs, C, lead, R, tinfo, soft, nhard,
+                   nsoft);
         __syncthreads();   // L is reused by the next group
     }
+}
+
+__global__ __launch_bounds__(64) void k_etsi_tail(const uint8_t *__restrict__ hard, const int8_t *__restrict__ soft,
+                                                  int stride, int C, const int32_t *__restrict__ tinfo, int R,
+                                                  uint8_t *nhard, int8_t *nsoft, int32_t *__restrict__ lead) {
+    const int ch = blockIdx.x;
+    if (ch >= C) return;
+    tail_move(hard, soft, stride, ch, tinfo[2 * ch], tinfo[2 * ch + 1] >> 1, tinfo[2 * ch + 1] & 1, R, nhard, nsoft,
+              lead, threadIdx.x);
 }
 
 // --------------------------------------------------------------------------- E4 Viterbi
@@ -2621,20 +2646,22 @@ int tetra_etsi_stream_window(const tetra_etsi_plan *P, int64_t x_total, int64_t 
     if (!P || !s || !W || !yoff || !y_done_next || x_total < 0 || y_done < 0 || n < 0 || P->q1 < 1 || P->up < 1 ||
         P->down < 1)
         return TETRA_E_INVALID;
-    // P = q1 down input samples carry `up` outputs: a window starting at a multiple of P has the
-    // polyphase phases of a run over the whole capture, its output m is global output m + up s / P
-    const int64_t per = (int64_t)P->q1 * P->down;
+    // pb = q1 down input samples carry `up` outputs: a window starting at a multiple of pb has the
+    // polyphase phases of a run over the whole capture, its output m is global output m + up s / pb.
+    // Windows start at multiples of per = pb, doubled when odd (whole sample pairs: the kernels load
+    // two samples at a time), which carry ups outputs.
+    const int64_t pb = (int64_t)P->q1 * P->down, per = pb % 2 ? 2 * pb : pb, ups = P->up * (per / pb);
     int64_t st = 0;
     if (y_done > 0) {
         const int64_t a = y_done - TETRA_ETSI_MARGIN;
-        st = per * (a >= 0 ? a / P->up : -((-a + P->up - 1) / P->up));   // floor division
+        st = per * (a >= 0 ? a / ups : -((-a + ups - 1) / ups));   // floor division
         if (st < 0) st = 0;
     }
     int64_t m1, m2, sm;
     tetra_etsi_lengths(P, (size_t)(x_total + n), &m1, &m2, &sm);
     *s = st;
     *W = x_total + n - st;
-    *yoff = y_done - P->up * (st / per);
+    *yoff = y_done - P->up * (st / pb);
     *y_done_next = m2 > y_done ? m2 : y_done;
     return TETRA_OK;
 }
@@ -2795,11 +2822,12 @@ static int lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard
     const size_t jtot = 32 * C;   // the three job regions (job_base / job_cap)
     // workspace: [job counters per kind (16 B)] [jobs] [survivors: 36 groups x jtot x 4 lanes x 32 bits
     // (SCH/F: 288 steps / 8; allocated as 288 x jtot dwords)]
-    char *w = (char *)ws(ctx, S_W7, 16 + jtot * sizeof(Job) + 288 * jtot * 4);
+    char *w = (char *)ws(ctx, S_W7, 16 + jtot * sizeof(Job) + 288 * jtot * 4 + (lead ? 8 * C : 0));
     if ((cell_init && !ci) || !sb || !hd || !ns || !nbo || !bo || !nko || !ko || !to || !w) return st.finish();
     unsigned long long *jcount = (unsigned long long *)w;
     Job *jobs = (Job *)(w + 16);
     uint32_t *surv = (uint32_t *)(w + 16 + jtot * sizeof(Job));
+    int32_t *tinfo = lead ? (int32_t *)(w + 16 + jtot * sizeof(Job) + 288 * jtot * 4) : nullptr;   // streaming
     if (cell_init && ctx->cells != C) {   // acquisition on a new channel count: an empty table
         std::vector<uint8_t> bsch(432);
         scramble_seq(3u, 432, bsch.data());
@@ -2817,19 +2845,26 @@ static int lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard
         PROF(ctx, "etsi_sync");
         HIP_TRY(ctx, hipMemsetAsync(jcount, 0, 16, ctx->stream));
         const unsigned ngrp = (unsigned)((C + SYNC_WAVES - 1) / SYNC_WAVES);
+        // double-buffered rows: the sync kernel moves the tails itself (no k_etsi_tail launch)
+        const bool other = lead && nhd != hd;
         hipLaunchKernelGGL(k_etsi_sync, dim3(ngrp), dim3(64 * SYNC_WAVES), 0,
-                           ctx->stream, hd, ns, (int)smax, nbo, bo, nko, jcount, jobs, (int)C, sb, ld_,
-                           lead ? TETRA_ETSI_RESERVE : 0, nsb, nhd);
+                           ctx->stream, hd, ns, (int)smax, nbo, bo, nko, jcount, jobs, (int)C, ld_,
+                           lead ? TETRA_ETSI_RESERVE : 0, tinfo, sb, other ? nhd : nullptr, other ? nsb : nullptr);
     }
     // grids: the waves each kind's job capacity needs (16 blocks per trellis wave, 64 per traceback wave)
+    // (TETRA_LMAC_GRID_CAP: at most that many trellis workgroups, a quarter as many traceback ones --
+    // the kernels walk their jobs with a grid stride; 0 = the capacity)
+    static const long gcap = getenv("TETRA_LMAC_GRID_CAP") ? atol(getenv("TETRA_LMAC_GRID_CAP")) : 0;
     auto vgrid = [&](int m) {
         size_t g = 0;
         for (int k = 0; k < 3; ++k) g += (m >> k) & 1 ? (job_cap(k, C) + 15) / 16 : 0;
+        if (gcap > 0 && g > (size_t)gcap) g = (size_t)gcap;
         return dim3((unsigned)g);
     };
     auto tgrid = [&](int m) {
         size_t g = 0;
         for (int k = 0; k < 3; ++k) g += (m >> k) & 1 ? (job_cap(k, C) + 63) / 64 : 0;
+        if (gcap > 0 && g > (size_t)(gcap / 4 + 1)) g = (size_t)(gcap / 4 + 1);
         return dim3((unsigned)g);
     };
     int mask = 7;
@@ -2851,6 +2886,11 @@ static int lmac_etsi(tetra_ctx *ctx, const int8_t *softbits, const uint8_t *hard
         PROF(ctx, "etsi_traceback");
         hipLaunchKernelGGL(k_etsi_traceback, tgrid(mask), dim3(64), 0, ctx->stream, jobs, jcount, (int)C, surv, ko, to,
                            mask);
+    }
+    if (lead && nhd == hd) {   // these rows: the tails after the trellis has read them
+        PROF(ctx, "etsi_tail");
+        hipLaunchKernelGGL(k_etsi_tail, dim3((unsigned)C), dim3(64), 0, ctx->stream, hd, sb, (int)smax, (int)C, tinfo,
+                           TETRA_ETSI_RESERVE, nhd, nsb, ld_);
     }
     return st.finish();
 }

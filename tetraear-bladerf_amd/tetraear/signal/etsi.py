@@ -355,7 +355,8 @@ def synth(C, N, fs=2.4e6, seed=1, snr_db=None, cfo_max=600.0, device_arrays=None
 def _on_stream(c):
     """torch ops enqueued on library context c's stream (ordered with its kernels)."""
     import torch
-    return torch.cuda.stream(torch.cuda.ExternalStream(c.lib.tetra_get_stream(c.handle)))
+    ptr = c.lib.tetra_get_stream(c.handle)
+    return torch.cuda.stream(torch.cuda.ExternalStream(ptr) if ptr else torch.cuda.default_stream())
 
 
 class BenchStep:
@@ -447,6 +448,7 @@ class BenchStep:
             self.lead = torch.full((C,), 2 * RESERVE, dtype=torch.int32, device=device)
             self.x_total = self.y_done = 0
             self.resets = 0
+            self._next_k, self._origin = 0, 0   # the chunk the stream continues into; its capture's start
             self.bufs = [self._stream_bufs(device) for _ in range(2)]
             self.sym, self.soft, self.hard, self.nsym = self.bufs[0]
         sm = self.smax
@@ -570,18 +572,25 @@ class BenchStep:
     def _demod_stream(self, c, sym, soft, hard, nsym):
         """Chunk kchunk of every channel's capture: its window in place in the capture rows."""
         k = self.kchunk % self.chunks
-        if self.kchunk and k == 0:   # past the capture's end: the same rows again, as a new capture
+        # the stream continues only into the chunk after the last one; anything else -- past the
+        # capture's end, or a caller that moved kchunk -- starts a new capture at chunk k (the
+        # windows never leave the resident capture)
+        if k != self._next_k:
             self.x_total = self.y_done = 0
             with _on_stream(c):
                 self.track.zero_()
             self._reset_lead = True
             self.resets += 1
+            self._origin = k * self.N
+        self._next_k = k + 1
         self.kchunk += 1
         s, W, yoff, y_next = stream_window(self.plan, self.x_total, self.y_done, self.N)
         bps = 4 if self.fmt == _hip.TETRA_SC16 else 8
         _, _, sm = lengths(self.plan, W)
+        off = self._origin + s
+        assert off + W <= self.N * self.chunks, (off, W)
         c.check(c.lib.tetra_demod_etsi_stream(
-            c.handle, self.plan, ctypes.c_void_p(self.cap.data_ptr() + bps * s), self.fmt, self.C,
+            c.handle, self.plan, ctypes.c_void_p(self.cap.data_ptr() + bps * off), self.fmt, self.C,
             self.N * self.chunks, W, int(yoff), _hip.ptr(self.track), ctypes.c_void_p(sym.data_ptr() + 8 * RESERVE),
             ctypes.c_void_p(soft.data_ptr() + 2 * RESERVE), ctypes.c_void_p(hard.data_ptr() + RESERVE),
             _hip.ptr(nsym), min(sm + 1, self.smax), self.stride, None), "demod_etsi_stream")
