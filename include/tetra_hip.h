@@ -93,7 +93,7 @@ typedef struct tetra_compat_plan {
     int32_t ntaps;        /* butter(4) -> 5 */
     int32_t sps;          /* int(rate/18000) (processor.py:183) */
     int32_t phase_step;   /* max(1, sps//8) (processor.py:194) */
-    int32_t flags;        /* TETRA_COMPAT_*: decimator form (0: automatic) */
+    int32_t flags;        /* TETRA_COMPAT_*: 0 = scipy's sequential order (bit-exact), BLOCKED = latency mode */
     int32_t reserved;
     double fs_dec;        /* sample rate after decimation: time base of frequency_shift */
     float sos_f32[24];    /* cheby1(8, 0.05, 0.8/q) SOS [4][6] as complex64 real parts */
