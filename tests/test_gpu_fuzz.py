@@ -11,7 +11,7 @@ outside that band (test_spectrum.py); the channeliser within Y_TOL (test_wideban
 Covered: the default compat process() against the sequential (reference-order) oracle, compat
 batches (latency and throughput kernels) and the direct SignalProcessor methods,
 compat decoder streams, the ETSI chain with its lower MAC (cell given and acquired) and its component
-methods, the scanner detector, the AFC gate, the wideband channeliser, device-tensor batches.  Each
+methods, the streaming ETSI receiver over random chunk patterns (round 6), the scanner detector, the AFC gate, the wideband channeliser, device-tensor batches.  Each
 host-side bug the sweep found keeps its case here ("sweep").
 """
 import numpy as np
@@ -160,6 +160,63 @@ def test_etsi_random_geometry_vs_oracle(seed):
         for f, (_, _, dec) in zip(res[ch], want):
             for b, (kind, bits, ok) in zip(f["blocks"], dec):
                 assert b["crc_ok"] == ok and np.array_equal(b["bits"], bits), case + (ch,)
+
+
+@pytest.mark.parametrize("seed", range(14 * SCALE))
+def test_etsi_stream_random_chunks_vs_oracle(seed):
+    """The streaming receiver (round 6) over chunk sequences nobody chose: every CLI rate, 1-4
+    channels, chunk patterns mixing tiny chunks (a few samples: windows too short for the filter,
+    k_track_skip), odd-sized and full ones, cf32 / SC16, cell given or acquired -- per chunk the
+    symbols, soft bits, dibits, bursts (negative positions across seams), decoded bits, CRC flags and
+    acquired cells equal the oracle Stream's (tests/test_gpu_stream.py's bar)."""
+    from tetraear.signal.etsi import EtsiStream, synth
+    from tetraear.core.etsi import EtsiLowerMac
+    rng = np.random.default_rng(5000 + seed)
+    fs = ETSI_RATES[seed % len(ETSI_RATES)]
+    C = int(rng.integers(1, 5))
+    n1 = int(131072 * fs / 2.4e6)
+    pattern = []
+    for _ in range(int(rng.integers(0, 4))):
+        u = rng.uniform()
+        pattern.append(int(rng.integers(2, 60)) if u < 0.35 else int(rng.integers(60, 5000)) if u < 0.7
+                       else int(rng.integers(5000, n1 + 1)))
+    pattern.insert(int(rng.integers(0, len(pattern) + 1)), int(rng.integers(20000, n1 + 1)))   # bounds the chunk count
+    total = int(rng.integers(2 * n1, 4 * n1))
+    sc16 = bool(rng.integers(0, 2))
+    acquire = bool(rng.integers(0, 2))
+    snr = float(rng.uniform(8.0, 24.0))
+    iq, cells = synth(C, total, fs=fs, seed=6000 + seed, snr_db=snr, cfo_max=float(rng.uniform(0, 600)))[:2]
+    inp = iq
+    if sc16:
+        inp = np.stack([np.rint(iq.real * 32768), np.rint(iq.imag * 32768)], -1).clip(-32768, 32767).astype(np.int16)
+        iq = (inp[..., 0].astype(np.float32) / 32768 + 1j * (inp[..., 1].astype(np.float32) / 32768)).astype(np.complex64)
+    streams = [E.Stream(fs, cell_init=None if acquire else int(cells[ch])) for ch in range(C)]
+    st, lm = EtsiStream(fs, C), EtsiLowerMac()
+    at, k = 0, 0
+    case = (seed, fs, C, pattern, total, "sc16" if sc16 else "cf32", "acquire" if acquire else "given")
+    while at < total:
+        n = min(pattern[k % len(pattern)], total - at)
+        n -= n % 2
+        if n == 0:
+            break
+        hard, soft, sym, ns = st.demod(inp[:, at:at + n])
+        frames = lm.decode_stream(soft, hard, ns, None if acquire else cells)
+        for ch in range(C):
+            w = streams[ch].push(iq[ch, at:at + n])
+            m = int(ns[ch])
+            where = case + (k, at, n, ch)
+            assert m == len(w["symbols"]), where
+            assert np.array_equal(sym[ch, :m], w["symbols"]), where
+            assert np.array_equal(hard[ch, :max(m - 1, 0)], w["hard"]), where
+            assert np.array_equal(soft[ch, :2 * max(m - 1, 0)], w["soft"]), where
+            assert [(f["position"], f["burst_kind"]) for f in frames[ch]] == [(p, kd) for p, kd, _ in w["bursts"]], where
+            for f, (_, _, dec) in zip(frames[ch], w["bursts"]):
+                for b, (kind, bits, ok) in zip(f["blocks"], dec):
+                    assert b["crc_ok"] == ok and np.array_equal(b["bits"], bits), where
+            if acquire:
+                assert int(lm.cell_state[ch]) == w["cell"], where
+        at += n
+        k += 1
 
 
 def _crc_burst_data(rng, fixed_tail):
