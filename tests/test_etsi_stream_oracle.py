@@ -114,6 +114,29 @@ def test_stream_at_other_cli_rates(fs):
     assert len(found) >= int(n_total / fs * 18000 / 255) - 2
 
 
+@pytest.mark.parametrize("t0", [0.1, 0.5, 0.9])
+def test_retune_mid_stream_recovers_in_the_first_chunk(t0):
+    """The GUI retunes the capture without a new processor (modern.py:1903-1909, the loop then keeps
+    calling process()): the stream carries the old signal's timing into a new one with another symbol
+    phase, CFO and carrier phase.  The Gardner loop pulls in within the first chunk: from the second
+    chunk on every burst is found and CRC-good, as for a fresh stream on the new signal."""
+    L = 131072
+    xa, _, _, _ = _capture(7, 3 * L, cfo=120.0)
+    xb, cb, _, _ = _capture(8, 5 * L, cfo=-300.0)
+    rng = np.random.default_rng(9)
+    xb = E.modulate(E.burst_stream(rng, 40, E.scramble_seq(cb, 432))[0], 5 * L, t0=t0, phase0=2.0, cfo=-300.0,
+                    snr_db=18.0, rng=rng)
+    st = E.Stream(2.4e6, cell_init=cb)
+    for k in range(3):
+        st.push(xa[k * L:(k + 1) * L])
+    got = []
+    for k in range(5):
+        r = st.push(xb[k * L:(k + 1) * L])
+        got.append((len(r["bursts"]), sum(all(ok for _, _, ok in dec) for _, _, dec in r["bursts"])))
+    assert all(n >= 3 and ok == n for n, ok in got[1:]), got
+    assert got[0][1] >= 1, got
+
+
 def _sync_pdu(rng, mcc, mnc, cc):
     """60 BSCH type-1 bits carrying a cell: colour code at 4..9, MCC 31..40, MNC 41..54 (the fields
     bsch_cell_init reads), the rest random."""
