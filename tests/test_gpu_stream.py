@@ -117,6 +117,25 @@ def test_sc16_stream_equals_cf32_stream():
             assert np.array_equal(x, y), k
 
 
+def test_stream_mixed_formats_continue_in_cf32():
+    """Chunks of one stream in different formats -- SC16, then cf32, then SC16 with the AFC mixer on
+    (which takes cf32) -- decode as the all-cf32 stream of the same samples does (SC16 -> cf32 is
+    exact), instead of failing."""
+    from tetraear.signal.etsi import EtsiStream, synth
+    C, K = 2, 4
+    iq = synth(C, K * L, seed=45, snr_db=18.0)[0]
+    q = np.stack([np.rint(iq.real * 32768), np.rint(iq.imag * 32768)], -1).clip(-32768, 32767).astype(np.int16)
+    f = (q[..., 0].astype(np.float32) / 32768 + 1j * (q[..., 1].astype(np.float32) / 32768)).astype(np.complex64)
+    offs = [None, None, [100.0, -50.0], None]
+    a, b = EtsiStream(2.4e6, C), EtsiStream(2.4e6, C)
+    for k in range(K):
+        sl = slice(k * L, (k + 1) * L)
+        ra = a.demod(f[:, sl], offs[k])
+        rb = b.demod(f[:, sl] if k == 1 else q[:, sl], offs[k])
+        for x, y in zip(ra, rb):
+            assert np.array_equal(x, y), k
+
+
 @pytest.mark.parametrize("fs", [1.8e6, 2.1e6])
 def test_stream_other_rates_vs_oracle(fs):
     """The generic-rate chain (k_chanfilt_g + k_timing) streams the same way."""

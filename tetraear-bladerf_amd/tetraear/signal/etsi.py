@@ -116,6 +116,12 @@ def stream_window(plan, x_total, y_done, n):
     return tuple(x.value for x in v)
 
 
+def _sc16_to_cf32(x):
+    """[C, N, 2] int16 -> [C, N] complex64 scaled 1/32768 (capture.py:241-269; exact)."""
+    return ((x[..., 0].astype(np.float32) + 1j * x[..., 1].astype(np.float32)) / np.float32(32768)).astype(
+        np.complex64)
+
+
 class EtsiStream:
     """The demod half of the streaming receiver: consecutive chunks of C channels' continuous
     captures (the reference's capture loops, /root/reference/tetraear/ui/modern.py:1901-1919,
@@ -161,12 +167,14 @@ class EtsiStream:
         n = x.shape[1]
         if n % 2:
             raise ValueError("streaming chunks must hold an even number of samples")
-        if freq_offsets is not None and fmt == _hip.TETRA_SC16:   # the mixer takes cf32 (SC16 -> cf32 is exact)
-            x = ((x[..., 0].astype(np.float32) + 1j * x[..., 1].astype(np.float32)) / np.float32(32768)).astype(
-                np.complex64)
-            fmt = _hip.TETRA_CF32
-        if self.hist is not None and self.hist.dtype != x.dtype:
-            raise ValueError("a stream keeps its sample format")
+        # SC16 -> cf32 is exact (the SC16 kernels compute on the same scaled samples, bit for bit), so a
+        # stream whose chunks mix the formats -- or SC16 with the mixer on for some chunks, which takes
+        # cf32 -- continues in cf32
+        if fmt == _hip.TETRA_SC16 and (freq_offsets is not None or
+                                       (self.hist is not None and self.hist.dtype != np.int16)):
+            x, fmt = _sc16_to_cf32(x), _hip.TETRA_CF32
+        if self.hist is not None and self.hist.dtype == np.int16 and fmt == _hip.TETRA_CF32:
+            self.hist = _sc16_to_cf32(self.hist)
         s, W, yoff, y_next = stream_window(self.plan, self.x_total, self.y_done, n)
         h = self.x_total - s
         if h > (0 if self.hist is None else self.hist.shape[1]):
