@@ -425,6 +425,8 @@ def main():
         achieved = per_sample * units_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
         floor = read_floor(c, step) if hasattr(step, "floor_args") else None
         cpu = None if a.no_cpu else cpu_baseline(a, step)
+        traffic = traffic_from_profiles(ksym, step.workload_key() if hasattr(step, "workload_key") else
+                                        f"{C} channels x {N} {a.iq if a.chain == 'etsi' else 'cf32'}")
         out = {
             "metric": "IQ Msamples/s demod+Viterbi; real-time 25 kHz TETRA channels @1/2/4/8 GPU",
             "value": round(value, 3),
@@ -458,8 +460,10 @@ def main():
             "roofline": {
                 "bound": "hbm", "kernel": name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic_from_profiles(ksym, step.workload_key() if hasattr(step, "workload_key") else
-                                                 f"{C} channels x {N} {a.iq if a.chain == 'etsi' else 'cf32'}"),
+                # HBM bytes per launch from this round's PMC summary of the same sources (or null), and
+                # where that number came from (or why there is none)
+                "traffic": traffic["bytes"] if traffic else None,
+                "traffic_source": traffic,
                 "launch_ms": round(launch_ms, 4), "algorithmic_bytes_per_launch": per_sample * units_per_launch,
                 "kernel_symbol": ksym,
                 # the same HBM read pattern with no arithmetic (k_read_floor), measured in this run:
