@@ -33,6 +33,7 @@ enum Slot {
     S_W16,                                                 // compat time-blocked decimator: tile states, Phi table
     S_W17,                                                 // compat time-blocked filtfilt: tile states
     S_W18,                                                 // compat latency mode: extract_symbols' |y|^2 rows
+    S_W19,                                                 // compat, few channels: the mixed rows filtfilt reads
     S_COUNT
 };
 

@@ -2043,6 +2043,18 @@ int tetra_demod_dqpsk(tetra_ctx *ctx, const void *sym, int fmt, size_t C, size_t
     return st.finish();
 }
 
+// The sequential filtfilt takes its mixed input from a parallel k_mix pass (instead of the mixer
+// inside its recursion) for batches of up to PREMIX_MAXC channels whose rows are all mixed, when the
+// flags are host memory (no read-back).  Past that the batch's lanes hide the mixer's latency, and a
+// float64 row written and read again would cost more than it saves (the bench's 8192 channels).
+constexpr size_t PREMIX_MAXC = 64;
+static bool premix_fits(size_t C, const uint8_t *mix_on) {
+    if (C > PREMIX_MAXC || !mix_on || is_device_ptr(mix_on)) return false;
+    for (size_t c = 0; c < C; ++c)
+        if (!mix_on[c]) return false;
+    return true;
+}
+
 int tetra_demod_compat(tetra_ctx *ctx, const tetra_compat_plan *P, const void *iq, int fmt, size_t C, size_t N,
                        const double *mix_c, const uint8_t *mix_on, void *soft, uint8_t *hard, int32_t *nsym,
                        size_t smax, int32_t *soft_f32) {
@@ -2125,7 +2137,25 @@ int tetra_demod_compat(tetra_ctx *ctx, const tetra_compat_plan *P, const void *i
                                                                       grouped(M))
                                        : run_filtfilt_blocked<float>(ctx, P, (const float *)d, ld, (int)C, M, mc, mo, fb,
                                                                      grouped(M));
-            else
+            else if (premix_fits(C, mix_on)) {
+                // a few channels, every one mixed: frequency_shift's values for the whole chunk in
+                // parallel first (k_mix: the same mixed_val arithmetic, float64), then the sequential
+                // filtfilt on them -- with the mixer inside its recursion one lane computed every
+                // sample's float64 sincos in its dependent chain (3.98 of the 11.7 ms one-chunk call,
+                // DESIGN §5.8).  The same values and the same double extension: bit-identical.
+                double *pm = (double *)ws(ctx, S_W19, grouped_elems((int)C, M) * 8);
+                if (!pm) return TETRA_E_NOMEM;
+                {
+                    PROF(ctx, "compat_mix");
+                    if (fmt == TETRA_CF64)
+                        hipLaunchKernelGGL(k_mix<double>, dim3(grid_for(C * M, 256)), dim3(256), 0, ctx->stream,
+                                           (const double *)d, ld, (int)C, M, mc, mo, P->fs_dec, pm, grouped(M));
+                    else
+                        hipLaunchKernelGGL(k_mix<float>, dim3(grid_for(C * M, 256)), dim3(256), 0, ctx->stream,
+                                           (const float *)d, ld, (int)C, M, mc, mo, P->fs_dec, pm, grouped(M));
+                }
+                rc = run_filtfilt<double>(ctx, P, pm, grouped(M), (int)C, M, nullptr, nullptr, fb, grouped(M));
+            } else
                 rc = fmt == TETRA_CF64 ? run_filtfilt<double>(ctx, P, (const double *)d, ld, (int)C, M, mc, mo, fb,
                                                               grouped(M))
                                        : run_filtfilt<float>(ctx, P, (const float *)d, ld, (int)C, M, mc, mo, fb,
