@@ -240,6 +240,29 @@ def test_process_and_decode_stream_across_seams():
     assert nslots >= int((K - 1) * L / 34000)
 
 
+def test_process_odd_chunks_carry_the_last_sample():
+    """process() chunks of odd length: the stream takes whole sample pairs, so each odd chunk's last
+    sample goes in front of the next call's -- no sample is dropped and the stream stays the
+    capture's: each call equals the oracle stream pushed with the pieces the carry produces."""
+    from tetraear.signal.etsi import EtsiReceiver, synth
+    iq = synth(1, 4 * L, seed=63, snr_db=18.0)[0][0]
+    sizes = [65537, 65535, 131071, 131073, 3, 1, 50000]
+    rx, orc = EtsiReceiver(), E.Stream(2.4e6)
+    at, carry = 0, np.zeros(0, np.complex64)
+    for k, n in enumerate(sizes):
+        hard, sym = rx.process(iq[at:at + n])
+        piece = np.concatenate([carry, iq[at:at + n]])
+        carry = piece[len(piece) - len(piece) % 2:]
+        piece = piece[:len(piece) - len(piece) % 2]
+        at += n
+        if len(piece) == 0:
+            assert len(hard) == 0, k
+            continue
+        w = orc.push(piece)
+        assert np.array_equal(np.asarray(hard), w["hard"]) and np.array_equal(sym, w["symbols"]), k
+    assert orc.x_total == at - len(carry)
+
+
 def test_stream_mixer_phase_is_continuous():
     """With an AFC offset the mixer runs on each window at the capture's global sample index, so the
     stream with the offset decodes as the stream of the pre-shifted capture does (every slot after

@@ -216,10 +216,12 @@ class EtsiReceiver:
         self.plan = etsi_plan(sample_rate)
         self.diag = None
         self._stream = None
+        self._odd = None   # a streamed chunk's odd last sample, carried to the front of the next one
 
     def reset(self):
         """process() starts a new capture (a retune): timing is acquired afresh on the next chunk."""
         self._stream = None
+        self._odd = None
 
     def demod_batch(self, iq):
         """[C, N] complex, or [C, N, 2] int16 SC16 capture samples (scaled 1/32768 in the channel
@@ -261,11 +263,18 @@ class EtsiReceiver:
         EtsiStream of one channel carries the filter history, the timing loop and the mixer phase,
         so the symbols continue across the seam -- the returned symbols then start with the
         previous chunk's last one and the dibits with the one across the seam (len(hard) ==
-        len(symbols) - 1 either way).  reset() starts a new capture.  ``stream=False``: the chunk on
-        its own (demod_batch)."""
+        len(symbols) - 1 either way).  An odd chunk's last sample is carried into the next call.
+        reset() starts a new capture.  ``stream=False``: the chunk on its own (demod_batch)."""
         x = np.ascontiguousarray(samples, np.complex64)
         if stream:
-            x = x[:len(x) - len(x) % 2]
+            # the stream takes whole sample pairs (the kernels load two at a time): an odd chunk's last
+            # sample goes in front of the next chunk instead of being dropped, so no sample slips
+            if self._odd is not None:
+                x = np.concatenate([self._odd, x])
+                self._odd = None
+            if len(x) % 2:
+                self._odd = x[-1:].copy()
+                x = x[:-1]
             if len(x) == 0:
                 return SoftSymbols(np.zeros(0, np.uint8), np.zeros(0, np.int8)), np.zeros(0, np.complex64)
             if self._stream is None:
