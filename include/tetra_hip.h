@@ -332,6 +332,17 @@ int tetra_etsi_timing(tetra_ctx *ctx, const tetra_etsi_plan *plan, const void *y
 int tetra_etsi_timing_om(tetra_ctx *ctx, const tetra_etsi_plan *plan, const void *y, size_t C, size_t M2,
                          const void *om, size_t nchunk, size_t ngrp, int U, void *soft, int8_t *softbits,
                          uint8_t *hard, int32_t *nsym, size_t smax, float *diag);
+/* tetra_etsi_timing over overlapping chunks of M carrier rows y [M][rowlen]: output row k nchunk + c
+ * is the timing of y[k][c stride, min(c stride + len, rowlen)) (len > stride: consecutive chunks
+ * share len - stride samples, so a burst that straddles one chunk's end lies whole in it -- the
+ * wideband chain's seams lose no burst).  om: NULL (each chunk's own Oerder-Meyr pass over y) or
+ * the rows' resampler partials [M][ngrp] float4 as in tetra_etsi_timing_om (stride a multiple of 4,
+ * ngrp U >= rowlen).  smax >= len / 4 + 2.  Outputs as tetra_etsi_timing with C = M nchunk; a
+ * chunk's outputs are the oracle's timing of its samples (no reference counterpart: the reference
+ * demodulates one narrowband capture at a time, tetraear/signal/processor.py:253-331). */
+int tetra_etsi_timing_chunks(tetra_ctx *ctx, const tetra_etsi_plan *plan, const void *y, size_t M, size_t rowlen,
+                             size_t nchunk, size_t stride, size_t len, const void *om, size_t ngrp, int U, void *soft,
+                             int8_t *softbits, uint8_t *hard, int32_t *nsym, size_t smax, float *diag);
 /* Fused demod (chanfilt + timing) over a batch. */
 int tetra_demod_etsi(tetra_ctx *ctx, const tetra_etsi_plan *plan, const void *iq, size_t C, size_t N,
                      void *soft, int8_t *softbits, uint8_t *hard, int32_t *nsym, size_t smax, float *diag);

@@ -155,6 +155,69 @@ def test_timing_om_rejects_bad_geometry():
         assert rc != 0, (C, m2, nchunk, ngrp, U)
 
 
+@pytest.mark.parametrize("rowlen,nchunk,stride,length,U,grouped", [
+    (12000, 3, 3932, 5012, 36, True), (12000, 3, 3932, 5012, 36, False), (11879, 3, 3932, 5011, 36, True),
+    (5000, 4, 1000, 1999, 4, True), (3000, 5, 500, 1337, 64, True), (4100, 6, 640, 1000, 12, False),
+    (700, 3, 200, 360, 36, True), (100, 2, 40, 60, 36, True)])
+def test_timing_chunks_geometries_bit_exact(synth_small, rowlen, nchunk, stride, length, U, grouped):
+    """tetra_etsi_timing_chunks, apart from the resampler: chunk c of each row is row[c stride,
+    min(c stride + length, rowlen)) -- overlapping chunks, the last cut by the row's end, odd
+    lengths, chunk starts on and off the groups, the grouped class sums or the timing's own pass --
+    and every output equals the oracle's timing of the chunk's samples."""
+    from tetraear import _hip
+    from tetraear.signal.etsi import etsi_plan, lengths
+    iq = synth_small[0][:2]
+    plan = etsi_plan()
+    C0, N = iq.shape
+    _, M2, _ = lengths(plan, N)
+    c = _hip.ctx()
+    y0 = np.zeros((C0, M2), np.complex64)
+    c.check(c.lib.tetra_etsi_chanfilt(c.handle, plan, _hip.ptr(iq), C0, N, _hip.ptr(y0)))
+    rows = np.stack([np.resize(np.roll(y0[r % C0], 977 * r), rowlen) for r in range(3)]).astype(np.complex64)
+    ngrp = -(-rowlen // U)
+    om = np.stack([E.Receiver.om_group_partials(r, U) for r in rows]).astype(np.float32) if grouped else None
+    C, sm = 3 * nchunk, length // 4 + 2
+    sym = np.zeros((C, sm), np.complex64)
+    soft, hard, ns = np.zeros((C, 2 * sm), np.int8), np.zeros((C, sm), np.uint8), np.zeros(C, np.int32)
+    c.check(c.lib.tetra_etsi_timing_chunks(c.handle, plan, _hip.ptr(rows), 3, rowlen, nchunk, stride, length,
+                                           _hip.ptr(om), ngrp if grouped else 0, U, _hip.ptr(sym), _hip.ptr(soft),
+                                           _hip.ptr(hard), _hip.ptr(ns), sm, None), "etsi_timing_chunks")
+    ora = E.Receiver()
+    for r in range(3):
+        for ci in range(nchunk):
+            s0 = ci * stride
+            L = min(length, rowlen - s0)
+            A = E.Receiver.om_grouped(rows[r], s0, L, U, om[r]) if grouped else None
+            so, sbo, ho, _ = ora.timing(rows[r, s0:s0 + L], om=A)
+            ch = r * nchunk + ci
+            n = int(ns[ch])
+            assert n == len(so), (r, ci)
+            assert np.array_equal(sym[ch, :n], so) and np.array_equal(hard[ch, :n - 1], ho), (r, ci)
+            assert np.array_equal(soft[ch, :2 * (n - 1)], sbo), (r, ci)
+
+
+def test_timing_chunks_rejects_bad_geometry():
+    """tetra_etsi_timing_chunks returns an error code (no launch) for a chunk shorter than 16 samples
+    (length, or the last chunk cut by the row's end), smax < length / 4 + 2, and with partials a
+    stride not a multiple of 4, U not a multiple of 4 or > 64, or partials short of the row."""
+    from tetraear import _hip
+    from tetraear.signal.etsi import etsi_plan
+    plan = etsi_plan()
+    c = _hip.ctx()
+    y = np.zeros((2, 1000), np.complex64)
+    om = np.zeros((2, 40, 4), np.float32)
+    sym, soft = np.zeros((8, 200), np.complex64), np.zeros((8, 400), np.int8)
+    hard, ns = np.zeros((8, 200), np.uint8), np.zeros(8, np.int32)
+    for nchunk, stride, length, smax, U, ngrp in ((2, 400, 12, 200, 36, 40), (4, 330, 400, 200, 36, 40),
+                                                  (2, 400, 800, 150, 36, 40), (2, 402, 500, 200, 36, 40),
+                                                  (2, 400, 500, 200, 18, 40), (2, 400, 500, 200, 68, 40),
+                                                  (2, 400, 500, 200, 36, 20)):
+        rc = c.lib.tetra_etsi_timing_chunks(c.handle, plan, _hip.ptr(y), 2, 1000, nchunk, stride, length,
+                                            _hip.ptr(om), ngrp, U, _hip.ptr(sym), _hip.ptr(soft), _hip.ptr(hard),
+                                            _hip.ptr(ns), smax, None)
+        assert rc != 0, (nchunk, stride, length, smax, U, ngrp)
+
+
 def test_lower_mac_matches_oracle(synth_small):
     from tetraear.signal.etsi import EtsiReceiver
     from tetraear.core.etsi import EtsiLowerMac

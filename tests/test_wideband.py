@@ -46,6 +46,58 @@ def test_lengths_match_oracle():
         assert p.lengths(Nw) == W.lengths(d, Nw), Nw
 
 
+def test_chunking_layouts():
+    """Overlapping chunks cover every carrier row to its end (each chunk m2 + ov samples but the
+    last, which the row's end cuts and which is never longer); ov = 0 is the tiled layout."""
+    from tetraear.signal.wideband import BURST_SAMPLES, OV_CHUNK, chunking, wb_plan
+    p = wb_plan()
+    assert OV_CHUNK >= BURST_SAMPLES and OV_CHUNK % 4 == 0
+    for Nw in (1_120_000, 3_300_000, 10_000_000, 2_000_000, 60_000):
+        _, n72 = p.lengths(Nw)
+        ck = chunking(p, Nw)
+        assert ck.rowlen == n72 and ck.length == min(ck.stride + OV_CHUNK, n72)
+        last = n72 - (ck.nchunk - 1) * ck.stride
+        assert 16 <= last <= ck.length, Nw
+        assert ck.nchunk == 1 or n72 - (ck.nchunk - 2) * ck.stride > ck.length   # no chunk to spare
+        t = chunking(p, Nw, ov=0) if n72 >= ck.stride else None
+        if t is not None:
+            assert t.nchunk == n72 // t.stride and t.length == t.stride and t.rowlen == t.nchunk * t.stride
+
+
+def test_merge_chunks_keeps_each_burst_once():
+    """merge_chunks: a burst two overlapping chunks both decoded (positions within the timing phase)
+    is kept once, in row order; bursts a slot apart, or in other carriers, are all kept; the blocks
+    follow their bursts."""
+    from tetraear.signal.wideband import merge_chunks
+    M, nchunk, stride = 2, 3, 1000
+    C = M * nchunk
+    nb, bursts = np.zeros(C, np.int32), np.zeros((C, 8, 2), np.int32)
+    nk, blocks = np.zeros(C, np.int32), np.zeros((C, 16, 4), np.int32)
+    pos = {0: [10, 520], 1: [2, 512], 2: [0], 3: [10], 4: [], 5: [3, 513]}   # start bits per chunk
+    for ch, ps in pos.items():
+        nb[ch] = len(ps)
+        for j, b in enumerate(ps):
+            bursts[ch, j] = (b, j % 3)
+            blocks[ch, nk[ch]] = (0, 1, j, 0)
+            nk[ch] += 1
+    keep, kb = merge_chunks(nb, bursts, nk, blocks, M, nchunk, stride)
+    # carrier 0 in row order: 20, 1004 (chunk 1), 1040 (chunk 0: its copy), 2000 (chunk 2), 2024 (chunk 1:
+    # its copy); the first copy in row order stays
+    assert keep[0, :2].tolist() == [True, False] and keep[1, :2].tolist() == [True, False] and keep[2, 0]
+    assert keep[3, 0] and keep[5, :2].tolist() == [True, True]
+    rows = {}
+    for ch in range(C):
+        for j in range(nb[ch]):
+            if keep[ch, j]:
+                rows.setdefault(ch // nchunk, []).append((ch % nchunk) * stride + 2 * int(bursts[ch, j, 0]))
+    for k, r in rows.items():
+        r.sort()
+        assert all(b - a > 64 for a, b in zip(r, r[1:])), (k, r)
+    assert len(rows[0]) == 3 and len(rows[1]) == 3   # 20, ~1020, ~2024 / 20, 2006, ~3026
+    assert np.array_equal(kb, keep[np.arange(C)[:, None], np.clip(blocks[..., 2], 0, 7)] &
+                          (np.arange(16)[None, :] < nk[:, None]))
+
+
 @pytest.fixture(scope="module")
 def capture():
     from tetraear.signal.wideband import synth_wideband
@@ -130,16 +182,17 @@ def test_wideband_timing_bit_exact(capture, monkeypatch):
     oracle/etsi.py on the same y, carrier by carrier (TETRA_WB_OM=0: the timing's own Oerder-Meyr
     pass over y, the ETSI chain's order; the grouped form: test_wideband_timing_om_bit_exact)."""
     import etsi as E
-    from tetraear.signal.wideband import WidebandReceiver
+    from tetraear.signal.wideband import WidebandReceiver, chunking
     monkeypatch.setenv("TETRA_WB_OM", "0")
     x = capture[0]
     rx = WidebandReceiver()
     hard, soft, sym, ns = rx.demod(x)
-    nchunk = ns.shape[1]
-    y = rx.channelize(x, nchunk * rx.m2).reshape(rx.plan.M, nchunk, rx.m2)
+    ck = chunking(rx.plan, len(x), rx.m2)
+    assert ns.shape[1] == ck.nchunk == 1 and ck.length == ck.rowlen   # one chunk: the whole row
+    y = rx.channelize(x, ck.rowlen)
     ora = E.Receiver()
     for k in (0, 1, 399, 400, 401, 799):
-        so, sbo, ho, _ = ora.timing(y[k, 0])
+        so, sbo, ho, _ = ora.timing(y[k])
         n = int(ns[k, 0])
         assert n == len(so), k
         assert np.array_equal(sym[k, 0, :n], so) and np.array_equal(hard[k, 0, :n - 1], ho)
@@ -220,8 +273,7 @@ def test_resampler_om_partials_bit_exact(capture3):
     from tetraear.signal.wideband import WidebandReceiver, chunking
     x = capture3[0]
     rx = WidebandReceiver()
-    nchunk, m2 = chunking(rx.plan, len(x), rx.m2)
-    n_keep = nchunk * m2
+    n_keep = chunking(rx.plan, len(x), rx.m2).rowlen
     y, om = rx.channelize_om(x, n_keep)
     assert np.array_equal(y, rx.channelize(x, n_keep))
     U = rx.plan.c.up
@@ -232,28 +284,100 @@ def test_resampler_om_partials_bit_exact(capture3):
 
 
 @pytest.mark.gpu
-def test_wideband_timing_om_bit_exact(capture3):
-    """The wideband timing on the resampler's class sums (tetra_etsi_timing_om) equals the oracle's
-    timing with the grouped Oerder-Meyr order, chunk by chunk -- chunks whose start is not on a
-    resampler group (heads and tails) included -- and decodes as the pass-over-y form does."""
+@pytest.mark.parametrize("grouped", [True, False])
+def test_wideband_timing_om_bit_exact(capture3, grouped, monkeypatch):
+    """The wideband timing over overlapping chunks (tetra_etsi_timing_chunks) equals the oracle's
+    timing of each chunk's samples, chunk by chunk -- the last chunk (cut by the row's end) and
+    chunks whose start is not on a resampler group (heads and tails) included; grouped: the
+    Oerder-Meyr class sums from the resampler's partials in the grouped order, else the timing's own
+    pass over y."""
     import etsi as E
     from tetraear.signal.wideband import WidebandReceiver, chunking
+    monkeypatch.setenv("TETRA_WB_OM", "1" if grouped else "0")
     x = capture3[0]
     rx = WidebandReceiver()
-    assert rx.grouped_om()
-    nchunk, m2 = chunking(rx.plan, len(x), rx.m2)
-    assert nchunk == 3
+    assert rx.grouped_om() == grouped
+    ck = chunking(rx.plan, len(x), rx.m2)
+    assert ck.nchunk == 3 and ck.length > ck.stride and ck.rowlen - 2 * ck.stride < ck.length
     hard, soft, sym, ns = rx.demod(x)
-    y, _ = rx.channelize_om(x, nchunk * m2)
+    y, _ = rx.channelize_om(x, ck.rowlen)
     U = rx.plan.c.up
     ora = E.Receiver()
     for k in (0, 3, 399, 400, 798):
         P = E.Receiver.om_group_partials(y[k], U)
-        for ci in range(nchunk):
-            s = ci * m2
-            A = E.Receiver.om_grouped(y[k], s, m2, U, P)
-            so, sbo, ho, _ = ora.timing(y[k, s:s + m2], om=A)
+        for ci in range(ck.nchunk):
+            s = ci * ck.stride
+            L = min(ck.length, ck.rowlen - s)
+            A = E.Receiver.om_grouped(y[k], s, L, U, P) if grouped else None
+            so, sbo, ho, _ = ora.timing(y[k, s:s + L], om=A)
             n = int(ns[k, ci])
             assert n == len(so), (k, ci)
             assert np.array_equal(sym[k, ci, :n], so) and np.array_equal(hard[k, ci, :n - 1], ho), (k, ci)
             assert np.array_equal(soft[k, ci, :2 * (n - 1)], sbo), (k, ci)
+
+
+@pytest.mark.gpu
+def test_timing_om_is_tiled_chunks(capture3):
+    """tetra_etsi_timing_om (chunks tiling the rows) is tetra_etsi_timing_chunks with stride = len."""
+    from tetraear import _hip
+    from tetraear.signal.wideband import WidebandReceiver, chunking
+    x = capture3[0]
+    rx = WidebandReceiver()
+    ck = chunking(rx.plan, len(x), rx.m2, ov=0)
+    y, om = rx.channelize_om(x, ck.rowlen)
+    M, U, sm = rx.plan.M, rx.plan.c.up, ck.length // 4 + 2
+    C = M * ck.nchunk
+    c = _hip.ctx()
+    outs = []
+    for form in ("om", "chunks"):
+        o = [np.zeros((C, sm), np.complex64), np.zeros((C, 2 * sm), np.int8), np.zeros((C, sm), np.uint8),
+             np.zeros(C, np.int32)]
+        if form == "om":
+            c.check(c.lib.tetra_etsi_timing_om(c.handle, rx.etsi, _hip.ptr(y), C, ck.length, _hip.ptr(om), ck.nchunk,
+                                               om.shape[1], U, *[_hip.ptr(a) for a in o], sm, None), "timing_om")
+        else:
+            c.check(c.lib.tetra_etsi_timing_chunks(c.handle, rx.etsi, _hip.ptr(y), M, ck.rowlen, ck.nchunk, ck.stride,
+                                                   ck.length, _hip.ptr(om), om.shape[1], U,
+                                                   *[_hip.ptr(a) for a in o], sm, None), "timing_chunks")
+        outs.append(o)
+    ns = outs[0][3]
+    assert np.array_equal(ns, outs[1][3]) and ns.min() > 0
+    for ch in range(C):
+        n = int(ns[ch])
+        assert np.array_equal(outs[0][0][ch, :n], outs[1][0][ch, :n])
+        assert np.array_equal(outs[0][1][ch, :2 * (n - 1)], outs[1][1][ch, :2 * (n - 1)])
+        assert np.array_equal(outs[0][2][ch, :n - 1], outs[1][2][ch, :n - 1])
+
+
+@pytest.mark.gpu
+def test_wideband_overlap_decodes_every_burst(capture3):
+    """Overlapping chunks lose no burst at a chunk seam: every burst wholly inside a carrier's row is
+    decoded once (WidebandReceiver.decode merges the copies two chunks share), its CRC-good blocks are
+    ones the carrier sent, and the tiled layout (ov = 0, rounds 1-6) decodes fewer."""
+    from tetraear.signal import wideband as WB
+    x, cells, kinds, payload, t0 = capture3
+    rx = WB.WidebandReceiver()
+    ck = WB.chunking(rx.plan, len(x), rx.m2)
+    frames = rx.decode(x, cells)
+    whole = ck.rowlen // WB.BURST_SAMPLES - 1   # slots wholly inside the row, whatever the phase
+    nb = nok = 0
+    for k, fr in enumerate(frames):
+        samples = [f["sample"] for f in fr]
+        assert samples == sorted(samples) and np.all(np.diff(samples) >= WB.BURST_SAMPLES - 16), k
+        assert len(fr) >= whole, (k, len(fr))
+        sent = {tuple(p) for bb in payload[k] for p in bb}
+        for f in fr:
+            for b in f["blocks"]:
+                nb += 1
+                if b["crc_ok"]:
+                    nok += 1
+                    assert tuple(np.pad(b["bits"], (0, 268 - len(b["bits"])))) in sent
+    assert nok / nb > 0.97, (nok, nb)
+    tiled = WB.WidebandReceiver()
+    orig = WB.OV_CHUNK
+    try:
+        WB.OV_CHUNK = 0
+        ft = tiled.decode(x, cells)
+    finally:
+        WB.OV_CHUNK = orig
+    assert sum(map(len, ft)) < sum(map(len, frames)) - rx.plan.M   # >= 1 burst per carrier lost at the seams

@@ -604,17 +604,13 @@ __device__ __forceinline__ void timing_wave(const float2 *y, int M2, float gain,
     }
 }
 
-// The Oerder-Meyr class sums of chunk ch in the wideband grouped order (oracle eo_om_grouped): the
-// chunk is row[s, s + M2) of its carrier's row of nchunk chunks, s = (ch mod nchunk) M2; om holds the
-// row's resampler group partials (ngrp float4 per carrier, U outputs per group).  Lane l sums the
-// whole groups g0 + l, g0 + l + 64, ... then a wave butterfly; the head [s, U g0) and the tail
-// [U g1, s + M2) (each < U <= 64 samples, one per lane) are summed class by class in ascending n.
-__device__ __forceinline__ float4 om_grouped(const float2 *__restrict__ yall, const float4 *__restrict__ om, int ch,
-                                             int M2, int nchunk, int ngrp, int U, int lane) {
-    const int k = ch / nchunk;
-    const long s = (long)(ch - k * nchunk) * M2, e = s + M2;
-    const float2 *row = yall + (size_t)k * nchunk * M2;
-    const float4 *P = om + (size_t)k * ngrp;
+// The Oerder-Meyr class sums of the chunk row[s, e) in the wideband grouped order (oracle
+// eo_om_grouped): P holds the carrier row's resampler group partials (U outputs per group, s a
+// multiple of 4).  Lane l sums the whole groups g0 + l, g0 + l + 64, ... then a wave butterfly; the
+// head [s, U g0) and the tail [U g1, e) (each < U <= 64 samples, one per lane) are summed class by
+// class in ascending n.
+__device__ __forceinline__ float4 om_grouped(const float2 *__restrict__ row, const float4 *__restrict__ P, long s,
+                                             long e, int U, int lane) {
     const long g0 = (s + U - 1) / U, g1 = e / U;
     const long hend = min((long)U * g0, e), tbeg = max((long)U * g1, hend);
     // head and tail samples first (their loads in flight with the partials')
@@ -639,24 +635,38 @@ __device__ __forceinline__ float4 om_grouped(const float2 *__restrict__ yall, co
     return make_float4((h[0] + v.x) + t[0], (h[1] + v.y) + t[1], (h[2] + v.z) + t[2], (h[3] + v.w) + t[3]);
 }
 
-// OMG (tetra_etsi_timing_om): the Oerder-Meyr class sums from the resampler's group partials
+// Chunked rows (cstride > 0: tetra_etsi_timing_chunks / _om): block ch is chunk c = ch mod nchunk of
+// carrier k = ch / nchunk, the samples yall[k rowlen + c cstride, ...) up to M2 of them or the row's
+// end (chunks may overlap); cstride = 0: block ch is yall[ch M2, (ch + 1) M2).
+// OMG (the _om forms): the Oerder-Meyr class sums from the resampler's group partials (om: ngrp
+// float4 per carrier row)
 template <int RING, bool LEAN, bool OMG = false>
 __global__ __launch_bounds__(64) void k_timing(const float2 *__restrict__ yall, int M2, float gain, float soft_scale,
                                                float2 *__restrict__ sym, float2 *__restrict__ dscr,
                                                int8_t *__restrict__ softbits, uint8_t *__restrict__ hard,
                                                int32_t *__restrict__ nsym, int smax, float4 *__restrict__ diag,
                                                int probe, const float4 *__restrict__ om, int nchunk, int ngrp, int U,
-                                               tetra_etsi_track *__restrict__ trk, int yoff, int ostride) {
+                                               tetra_etsi_track *__restrict__ trk, int yoff, int ostride, int cstride,
+                                               long rowlen) {
     __shared__ float2 ring[RING ? TRING : 1];
     const int ch = blockIdx.x;
     uint32_t *clk = probe && diag ? reinterpret_cast<uint32_t *>(diag + ch) : nullptr;
+    const float2 *y = yall + (size_t)ch * M2;
+    int L = M2;
     float4 omc = float4{};
-    if constexpr (OMG) {
-        if (clk && threadIdx.x == 0) clk[0] = (uint32_t)wall_clock64();
-        omc = om_grouped(yall, om, ch, M2, nchunk, ngrp, U, threadIdx.x);
+    if (cstride > 0) {
+        const int k = ch / nchunk;
+        const long s = (long)(ch - k * nchunk) * cstride;
+        L = (int)min((long)M2, rowlen - s);
+        const float2 *row = yall + (size_t)k * rowlen;
+        y = row + s;
+        if constexpr (OMG) {
+            if (clk && threadIdx.x == 0) clk[0] = (uint32_t)wall_clock64();
+            omc = om_grouped(row, om + (size_t)k * ngrp, s, s + L, U, threadIdx.x);
+        }
     }
     const size_t os = ostride ? (size_t)ostride : (size_t)smax;   // output rows (streaming: reserve + smax)
-    timing_wave<RING, LEAN, OMG>(yall + (size_t)ch * M2, M2, gain, soft_scale, sym + (size_t)ch * os,
+    timing_wave<RING, LEAN, OMG>(y, L, gain, soft_scale, sym + (size_t)ch * os,
                                  dscr ? dscr + (size_t)ch * smax : nullptr, softbits + (size_t)ch * 2 * os,
                                  hard + (size_t)ch * os, nsym + ch, diag ? diag + ch : nullptr, smax, threadIdx.x, ring,
                                  clk, omc, trk ? trk + ch : nullptr, yoff);
@@ -666,7 +676,7 @@ __global__ __launch_bounds__(64) void k_timing(const float2 *__restrict__ yall, 
 // quarter for the Oerder-Meyr pass and the d_j round trip through dscr (default 1: om_all, d_j
 // recomputed from the symbols)
 using timing_fn = void (*)(const float2 *, int, float, float, float2 *, float2 *, int8_t *, uint8_t *, int32_t *, int,
-                           float4 *, int, const float4 *, int, int, int, tetra_etsi_track *, int, int);
+                           float4 *, int, const float4 *, int, int, int, tetra_etsi_track *, int, int, int, long);
 // TETRA_TIMING_PROBE=1: with a diag buffer, each chunk's diag entry holds four 32-bit wall-clock stamps
 // (start, Oerder-Meyr done, Gardner done, end) instead of the diagnostics -- a latency probe
 static int timing_probe() {
@@ -2558,7 +2568,34 @@ int tetra_etsi_timing(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *y, s
         PROF(ctx, "etsi_timing");
         hipLaunchKernelGGL(timing_kernel(M2, smax), dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yd, (int)M2, P->gain,
                            P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg, timing_probe(),
-                           nullptr, 0, 0, 0, nullptr, 0, 0);
+                           nullptr, 0, 0, 0, nullptr, 0, 0, 0, 0);
+    }
+    return st.finish();
+}
+
+// The chunked timing both wideband entry points launch (cstride = the chunk stride, rowlen = the
+// carrier rows' length): tetra_etsi_timing_om's chunks tile the rows, tetra_etsi_timing_chunks' overlap.
+static int launch_timing_chunks(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *y, size_t M, size_t rowlen,
+                                size_t nchunk, size_t stride, size_t len, const void *om, size_t ngrp, int U,
+                                void *soft, int8_t *softbits, uint8_t *hard, int32_t *nsym, size_t smax, float *diag) {
+    const size_t C = M * nchunk;
+    Staging st(ctx);
+    const void *yd = st.in(y, M * rowlen * 8);
+    const void *omd = om ? st.in(om, M * ngrp * 16) : nullptr;
+    void *so = st.out(soft, C * smax * 8);
+    int8_t *sbo = (int8_t *)st.out(softbits, C * smax * 2);
+    uint8_t *ho = (uint8_t *)st.out(hard, C * smax);
+    int32_t *no = (int32_t *)st.out(nsym, C * 4);
+    float *dg = diag ? (float *)st.out(diag, C * 16) : nullptr;
+    // the grouped form needs no d_j scratch: the LEAN form recomputes d_j from the stored symbols
+    float2 *dscr = om ? nullptr : (float2 *)ws(ctx, S_W4, C * smax * 8);
+    if (!yd || (om && !omd) || !so || !sbo || !ho || !no || (!om && !dscr)) return st.finish();
+    {
+        PROF(ctx, "etsi_timing");
+        hipLaunchKernelGGL(timing_kernel(len, smax, om != nullptr), dim3((unsigned)C), dim3(64), 0, ctx->stream,
+                           (const float2 *)yd, (int)len, P->gain, P->soft_scale, (float2 *)so, dscr, sbo, ho, no,
+                           (int)smax, (float4 *)dg, timing_probe(), (const float4 *)omd, (int)nchunk, (int)ngrp, U,
+                           nullptr, 0, 0, (int)stride, (long)rowlen);
     }
     return st.finish();
 }
@@ -2571,24 +2608,23 @@ int tetra_etsi_timing_om(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *y
         M2 < 16 || nchunk * M2 * 8 >= ((size_t)1 << 31))
         return tetra_fail(ctx, TETRA_E_INVALID, "timing_om: C a multiple of nchunk, M2 >= 16 a multiple of 4, "
                                                 "4 <= U <= 64 a multiple of 4, ngrp U >= nchunk M2");
-    Staging st(ctx);
-    const void *yd = st.in(y, C * M2 * 8);
-    const void *omd = st.in(om, C / nchunk * ngrp * 16);
-    void *so = st.out(soft, C * smax * 8);
-    int8_t *sbo = (int8_t *)st.out(softbits, C * smax * 2);
-    uint8_t *ho = (uint8_t *)st.out(hard, C * smax);
-    int32_t *no = (int32_t *)st.out(nsym, C * 4);
-    float *dg = diag ? (float *)st.out(diag, C * 16) : nullptr;
-    if (!yd || !omd || !so || !sbo || !ho || !no) return st.finish();
-    {
-        PROF(ctx, "etsi_timing");
-        hipLaunchKernelGGL(timing_kernel(M2, smax, true), dim3((unsigned)C), dim3(64), 0, ctx->stream,
-                           // no d_j scratch: the LEAN form recomputes d_j from the stored symbols
-                           (const float2 *)yd, (int)M2, P->gain, P->soft_scale, (float2 *)so, nullptr, sbo, ho, no,
-                           (int)smax, (float4 *)dg, timing_probe(), (const float4 *)omd, (int)nchunk, (int)ngrp, U,
-                           nullptr, 0, 0);
-    }
-    return st.finish();
+    return launch_timing_chunks(ctx, P, y, C / nchunk, nchunk * M2, nchunk, M2, M2, om, ngrp, U, soft, softbits, hard,
+                                nsym, smax, diag);
+}
+
+int tetra_etsi_timing_chunks(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *y, size_t M, size_t rowlen,
+                             size_t nchunk, size_t stride, size_t len, const void *om, size_t ngrp, int U, void *soft,
+                             int8_t *softbits, uint8_t *hard, int32_t *nsym, size_t smax, float *diag) {
+    if (!ctx || !P || M == 0) return TETRA_E_INVALID;
+    if (nchunk == 0 || stride == 0 || len < 16 || (nchunk - 1) * stride + 16 > rowlen ||
+        rowlen * 8 >= ((size_t)1 << 31) || M * nchunk > INT32_MAX || smax < len / 4 + 2)
+        return tetra_fail(ctx, TETRA_E_INVALID, "timing_chunks: nchunk >= 1, stride >= 1, len >= 16, every chunk "
+                                                ">= 16 samples of the row, rows < 2^28 samples, smax >= len / 4 + 2");
+    if (om && (stride % 4 || U < 4 || U > 64 || U % 4 || ngrp * (size_t)U < rowlen))
+        return tetra_fail(ctx, TETRA_E_INVALID, "timing_chunks with om: stride a multiple of 4, 4 <= U <= 64 a "
+                                                "multiple of 4, ngrp U >= rowlen");
+    return launch_timing_chunks(ctx, P, y, M, rowlen, nchunk, stride, len, om, ngrp, U, soft, softbits, hard, nsym,
+                                smax, diag);
 }
 
 int tetra_demod_etsi(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *iq, size_t C, size_t N, void *soft,
@@ -2636,7 +2672,7 @@ int tetra_demod_etsi_fmt(tetra_ctx *ctx, const tetra_etsi_plan *P, const void *i
         PROF(ctx, "etsi_timing");
         hipLaunchKernelGGL(timing_kernel(M2, smax), dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yb, (int)M2, P->gain,
                            P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg, timing_probe(),
-                           nullptr, 0, 0, 0, nullptr, 0, 0);
+                           nullptr, 0, 0, 0, nullptr, 0, 0, 0, 0);
     }
     return st.finish();
 }
@@ -2720,7 +2756,7 @@ int tetra_demod_etsi_stream(tetra_ctx *ctx, const tetra_etsi_plan *P, const void
         PROF(ctx, "etsi_timing");
         hipLaunchKernelGGL(timing_kernel(M2, smax), dim3((unsigned)C), dim3(64), 0, ctx->stream, (const float2 *)yb,
                            (int)M2, P->gain, P->soft_scale, (float2 *)so, dscr, sbo, ho, no, (int)smax, (float4 *)dg,
-                           timing_probe(), nullptr, 0, 0, 0, tr, yoff, (int)ostride);
+                           timing_probe(), nullptr, 0, 0, 0, tr, yoff, (int)ostride, 0, 0);
     }
     return st.finish();
 }

@@ -114,7 +114,9 @@ def _bind(L):
         "tetra_etsi_timing": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _sz, _sz, _vp, _vp, _vp, _vp, _sz, _vp]),
         "tetra_etsi_timing_om": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _sz, _sz, _vp, _sz, _sz, ctypes.c_int, _vp,
                                         _vp, _vp, _vp, _sz, _vp]),
-        "tetra_demod_etsi": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _sz, _sz, _vp, _vp, _vp, _vp, _sz, _vp]),
+        "tetra_etsi_timing_chunks": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _sz, _sz, _sz, _sz, _sz, _vp, _sz,
+                                            ctypes.c_int, _vp, _vp, _vp, _vp, _sz, _vp]),
+        "tetra_demod_etsi":(_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _sz, _sz, _vp, _vp, _vp, _vp, _sz, _vp]),
         "tetra_etsi_chanfilt_fmt": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _i32, _sz, _sz, _vp]),
         "tetra_demod_etsi_fmt": (_i32, [_vp, ctypes.POINTER(EtsiPlan), _vp, _i32, _sz, _sz, _vp, _vp, _vp, _vp, _sz,
                                         _vp]),

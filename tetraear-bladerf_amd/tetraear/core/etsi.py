@@ -172,7 +172,8 @@ class EtsiLowerMac:
         self._run_stream(_hip.ctx(), C, nb, bursts, nk, blocks, t1, cells, (srow, hrow, nsym, stride, lead))
         return self._frames(C, nb, bursts, nk, blocks, t1)
 
-    def _frames(self, C, nb, bursts, nk, blocks, t1):
+    @staticmethod
+    def _frames(C, nb, bursts, nk, blocks, t1):
         out = []
         for ch in range(C):
             frames = []

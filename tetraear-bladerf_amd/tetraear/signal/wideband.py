@@ -10,6 +10,7 @@ is exactly the sample stream the ETSI timing stage takes (4 samples per symbol, 
 followed by the ETSI lower MAC.  This module designs the filters and moves arrays;
 oracle/wideband.py is the float64 specification the tests hold it to.
 """
+import collections
 import ctypes
 import functools
 import os
@@ -23,6 +24,11 @@ from tetraear.signal.etsi import etsi_plan, rrc
 FS_WB = 20e6
 M_WB = 800
 M2_CHUNK = 3932     # 72 kHz samples per timing chunk (as a 128 Ki chunk at 2.4 MSps)
+# samples consecutive timing chunks share: a whole burst (255 symbols = 1020 samples at 72 kHz) plus
+# 15 symbols, so a burst that starts in one chunk ends in it too (TETRA_WB_OVERLAP=0: chunks tile the
+# row, the round-1..6 form that loses the burst across every seam -- A/B only)
+OV_CHUNK = int(os.environ.get("TETRA_WB_OVERLAP", "1080"))
+BURST_SAMPLES = 1020   # one 255-symbol slot at 72 kHz
 # Two filter-bank designs (the carrier's output rate fs / D and what it implies):
 #   oversample 2 (default): D = M / 2 -> 50 kHz carriers.  A carrier's band aliases onto itself from
 #     37.5 kHz, so the prototype is 5 branches long (cut-off 25 kHz, Kaiser 8: 0.003 dB ripple over
@@ -78,13 +84,54 @@ def wb_plan(fs=FS_WB, M=M_WB, oversample=None):
     return WbPlan(fs, M, oversample)
 
 
-def chunking(plan, Nw, m2=M2_CHUNK):
-    """(nchunk, M2): each carrier's 72 kHz row is cut into nchunk timing chunks of M2 samples."""
+Chunks = collections.namedtuple("Chunks", "nchunk stride length rowlen")
+
+
+def chunking(plan, Nw, m2=M2_CHUNK, ov=None):
+    """Each carrier's 72 kHz row (rowlen samples kept) is cut into nchunk timing chunks: chunk c is
+    row[c m2, min(c m2 + length, rowlen)), length = m2 + ov, so consecutive chunks share ov samples
+    and the last one runs to the row's end (tetra_etsi_timing_chunks).  ov = 0: nchunk = n72 // m2
+    chunks tiling the first nchunk m2 samples (tetra_etsi_timing_om's layout)."""
+    ov = OV_CHUNK if ov is None else ov
     _, n72 = plan.lengths(Nw)
-    nchunk = n72 // m2
-    if nchunk < 1:
-        raise ValueError(f"{Nw} wideband samples give {n72} samples per carrier, less than one chunk of {m2}")
-    return nchunk, m2
+    if ov == 0:
+        nchunk = n72 // m2
+        if nchunk < 1:
+            raise ValueError(f"{Nw} wideband samples give {n72} samples per carrier, less than one chunk of {m2}")
+        return Chunks(nchunk, m2, m2, nchunk * m2)
+    if ov < 0 or ov % 4 or n72 < 16:
+        raise ValueError(f"overlap {ov} (a multiple of 4 >= 0) over {n72} samples per carrier")
+    nchunk = max(1, -(-(n72 - ov) // m2))
+    return Chunks(nchunk, m2, min(m2 + ov, n72), n72)
+
+
+def merge_chunks(nburst, bursts, nblock, blocks, M, nchunk, stride, tol=64):
+    """The lower MAC's bursts per (carrier, chunk) -> each burst once.  A burst in the ov samples two
+    chunks share is found by both; its position in the carrier row (chunk start + 2 x start bit, to
+    within the timing phase) tells the copies apart from the next burst (>= BURST_SAMPLES later).
+    Returns (keep [C, MAXB] bool: the first copy of every burst, in row order; keep_blocks [C, MAXJ]
+    bool: the blocks of kept bursts).  nburst [C], bursts [C][MAXB][2], nblock [C], blocks
+    [C][MAXJ][4] as tetra_lmac_etsi leaves them (host arrays)."""
+    nburst, bursts = np.asarray(nburst), np.asarray(bursts)
+    nblock, blocks = np.asarray(nblock), np.asarray(blocks)
+    C, maxb = bursts.shape[:2]
+    valid = np.arange(maxb)[None, :] < nburst[:, None]
+    ch = np.broadcast_to(np.arange(C)[:, None], (C, maxb))
+    pos = (ch % nchunk) * stride + 2 * bursts[..., 0].astype(np.int64)
+    car = ch // nchunk
+    ci, ji = np.nonzero(valid)
+    order = np.lexsort((ci, pos[ci, ji], car[ci, ji]))   # by carrier, row position, then chunk
+    ci, ji = ci[order], ji[order]
+    pc, cc = pos[ci, ji], car[ci, ji]
+    first = np.ones(len(ci), bool)
+    first[1:] = (cc[1:] != cc[:-1]) | (pc[1:] - pc[:-1] > tol)
+    keep = np.zeros((C, maxb), bool)
+    keep[ci[first], ji[first]] = True
+    maxj = blocks.shape[1]
+    jv = np.arange(maxj)[None, :] < nblock[:, None]
+    bi = np.clip(blocks[..., 2], 0, maxb - 1)
+    keep_blocks = jv & keep[np.arange(C)[:, None], bi]
+    return keep, keep_blocks
 
 
 def grouped_om(plan, m2=M2_CHUNK):
@@ -136,31 +183,63 @@ class WidebandReceiver:
         return grouped_om(self.plan, self.m2)
 
     def demod(self, x):
-        """x [Nw] -> (hard, soft_bits, sym, nsym) per (carrier, chunk): [M, nchunk, smax] uint8,
-        [M, nchunk, 2 smax] int8, [M, nchunk, smax] complex64, [M, nchunk] int32."""
-        nchunk, m2 = chunking(self.plan, len(x), self.m2)
+        """x [Nw] -> (hard, soft_bits, sym, nsym) per (carrier, chunk) of chunking(): [M, nchunk,
+        smax] uint8, [M, nchunk, 2 smax] int8, [M, nchunk, smax] complex64, [M, nchunk] int32."""
+        ck = chunking(self.plan, len(x), self.m2)
         om = None
         if self.grouped_om():
-            y, om = self.channelize_om(x, nchunk * m2)
+            y, om = self.channelize_om(x, ck.rowlen)
         else:
-            y = self.channelize(x, nchunk * m2)
+            y = self.channelize(x, ck.rowlen)
         c = _hip.ctx()
-        C = self.plan.M * nchunk
-        sm = m2 // 4 + 2
+        M = self.plan.M
+        C = M * ck.nchunk
+        sm = ck.length // 4 + 2
         sym = np.empty((C, sm), np.complex64)
         soft = np.empty((C, 2 * sm), np.int8)
         hard = np.empty((C, sm), np.uint8)
         ns = np.empty(C, np.int32)
-        if om is not None:
-            c.check(c.lib.tetra_etsi_timing_om(c.handle, self.etsi, _hip.ptr(y), C, m2, _hip.ptr(om), nchunk,
-                                               om.shape[1], self.plan.c.up, _hip.ptr(sym), _hip.ptr(soft),
-                                               _hip.ptr(hard), _hip.ptr(ns), sm, None), "etsi_timing_om")
-        else:
-            c.check(c.lib.tetra_etsi_timing(c.handle, self.etsi, _hip.ptr(y), C, m2, _hip.ptr(sym), _hip.ptr(soft),
-                                            _hip.ptr(hard), _hip.ptr(ns), sm, None), "etsi_timing")
-        M = self.plan.M
-        return (hard.reshape(M, nchunk, sm), soft.reshape(M, nchunk, 2 * sm), sym.reshape(M, nchunk, sm),
-                ns.reshape(M, nchunk))
+        c.check(c.lib.tetra_etsi_timing_chunks(c.handle, self.etsi, _hip.ptr(y), M, ck.rowlen, ck.nchunk, ck.stride,
+                                               ck.length, _hip.ptr(om) if om is not None else None,
+                                               om.shape[1] if om is not None else 0, self.plan.c.up, _hip.ptr(sym),
+                                               _hip.ptr(soft), _hip.ptr(hard), _hip.ptr(ns), sm, None),
+                "etsi_timing_chunks")
+        return (hard.reshape(M, ck.nchunk, sm), soft.reshape(M, ck.nchunk, 2 * sm), sym.reshape(M, ck.nchunk, sm),
+                ns.reshape(M, ck.nchunk))
+
+
+    def decode(self, x, cells):
+        """x [Nw] -> per carrier the frames decoded from it, each burst once (merge_chunks), in row
+        order: demod, then the ETSI lower MAC on every (carrier, chunk) with carrier k's scrambling
+        init cells[k].  A frame is the lower MAC's dict (core/etsi.py) plus "chunk" and "sample" (its
+        start in the carrier's 72 kHz row, to within the timing phase)."""
+        from tetraear.core.etsi import EtsiLowerMac
+        hard, soft, _, ns = self.demod(x)
+        M, nchunk, sm = hard.shape
+        C = M * nchunk
+        nb = np.zeros(C, np.int32)
+        bursts = np.zeros((C, _hip.ETSI_MAXB, 2), np.int32)
+        nk = np.zeros(C, np.int32)
+        blocks = np.zeros((C, _hip.ETSI_MAXJ, 4), np.int32)
+        t1 = np.zeros((C, _hip.ETSI_MAXJ, 268), np.uint8)
+        c = _hip.ctx()
+        cc = np.ascontiguousarray(np.repeat(np.asarray(cells, np.uint32), nchunk))
+        c.check(c.lib.tetra_etsi_set_cells(c.handle, _hip.ptr(cc), C), "tetra_etsi_set_cells")
+        c.check(c.lib.tetra_lmac_etsi(c.handle, _hip.ptr(soft.reshape(C, -1)), _hip.ptr(hard.reshape(C, -1)),
+                                      _hip.ptr(ns.reshape(-1)), C, sm, _hip.ptr(nb), _hip.ptr(bursts), _hip.ptr(nk),
+                                      _hip.ptr(blocks), _hip.ptr(t1)), "tetra_lmac_etsi")
+        keep, _ = merge_chunks(nb, bursts, nk, blocks, M, nchunk, self.m2)
+        frames = EtsiLowerMac._frames(C, nb, bursts, nk, blocks, t1)
+        out = [[] for _ in range(M)]
+        for ch in range(C):
+            for b, f in enumerate(frames[ch]):
+                if keep[ch, b]:
+                    f["chunk"] = ch % nchunk
+                    f["sample"] = (ch % nchunk) * self.m2 + 2 * f["position"]
+                    out[ch // nchunk].append(f)
+        for fr in out:
+            fr.sort(key=lambda f: f["sample"])
+        return out
 
 
 def synth_wideband(Nw, seed=1, snr_db=30.0, cfo_max=300.0, fs=FS_WB, M=M_WB, oversample=None):
@@ -191,9 +270,10 @@ class BenchStep:
         self.c, self.Nw, self.fs = c, Nw, fs
         self.plan = wb_plan(fs, M)
         self.etsi = etsi_plan(2.4e6)
-        self.nchunk, self.m2 = chunking(self.plan, Nw)
+        self.ck = chunking(self.plan, Nw)
+        self.nchunk, self.m2 = self.ck.nchunk, self.ck.stride
         self.C = M * self.nchunk
-        self.sm = self.m2 // 4 + 2
+        self.sm = self.ck.length // 4 + 2
         nbb = Nw // self.plan.D + 1
         nb = c.lib.tetra_synth_bursts_per_channel(nbb, fs / self.plan.D)
         self.x = torch.empty((Nw, 2), dtype=torch.float32, device=device)
@@ -208,10 +288,10 @@ class BenchStep:
         self.cells = cells.repeat_interleave(self.nchunk).contiguous()
         torch.cuda.current_stream(device).synchronize()
         c.check(c.lib.tetra_etsi_set_cells(c.handle, _hip.ptr(self.cells), self.C), "set_cells")
-        self.y = torch.empty((M, self.nchunk * self.m2, 2), dtype=torch.float32, device=device)
+        self.y = torch.empty((M, self.ck.rowlen, 2), dtype=torch.float32, device=device)
         # the timing's Oerder-Meyr class sums from the resampler (grouped_om): its group partials
         self.om_grouped = grouped_om(self.plan, self.m2)
-        self.ngrp = -(-self.nchunk * self.m2 // self.plan.c.up)
+        self.ngrp = -(-self.ck.rowlen // self.plan.c.up)
         self.om = torch.empty((M, self.ngrp, 4), dtype=torch.float32, device=device) if self.om_grouped else None
         self.sym = torch.empty((self.C, self.sm, 2), dtype=torch.float32, device=device)
         self.soft = torch.empty((self.C, 2 * self.sm), dtype=torch.int8, device=device)
@@ -290,21 +370,18 @@ class BenchStep:
             self._waterfall(c)
         if om is not None:
             c.check(c.lib.tetra_channelize_om(c.handle, self.plan.c, _hip.ptr(self.x), self.Nw, _hip.ptr(y),
-                                              self.nchunk * self.m2, _hip.ptr(om)), "channelize_om")
+                                              self.ck.rowlen, _hip.ptr(om)), "channelize_om")
         else:
             c.check(c.lib.tetra_channelize(c.handle, self.plan.c, _hip.ptr(self.x), self.Nw, _hip.ptr(y),
-                                           self.nchunk * self.m2), "channelize")
+                                           self.ck.rowlen), "channelize")
 
     def _timing(self, c, y, om):
-        if om is not None:
-            c.check(c.lib.tetra_etsi_timing_om(c.handle, self.etsi, _hip.ptr(y), self.C, self.m2, _hip.ptr(om),
-                                               self.nchunk, self.ngrp, self.plan.c.up, _hip.ptr(self.sym),
-                                               _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.sm,
-                                               None), "etsi_timing_om")
-        else:
-            c.check(c.lib.tetra_etsi_timing(c.handle, self.etsi, _hip.ptr(y), self.C, self.m2, _hip.ptr(self.sym),
-                                            _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.sm,
-                                            None), "etsi_timing")
+        ck = self.ck
+        c.check(c.lib.tetra_etsi_timing_chunks(c.handle, self.etsi, _hip.ptr(y), self.plan.M, ck.rowlen, ck.nchunk,
+                                               ck.stride, ck.length, _hip.ptr(om), self.ngrp if om is not None else 0,
+                                               self.plan.c.up, _hip.ptr(self.sym), _hip.ptr(self.soft),
+                                               _hip.ptr(self.hard), _hip.ptr(self.nsym), self.sm, None),
+                "etsi_timing_chunks")
 
     def _lmac(self, c):
         c.check(c.lib.tetra_lmac_etsi(c.handle, _hip.ptr(self.soft), _hip.ptr(self.hard), _hip.ptr(self.nsym), self.C,
@@ -350,9 +427,11 @@ class BenchStep:
         """Algorithmic bytes per wideband input sample of each timed stage (cf32 = 8 B):
         the fused analysis (M = 800) and the fold read x and write Y (M per D samples), the FFT reads and writes Y, the resampler reads
         Y and writes y (M carriers at 72 kHz), the timing stage reads y and writes per symbol an
-        8 B symbol, 2 soft bits and a hard dibit.  bench.py reports the slowest of them."""
-        M, D, fs = self.plan.M, self.plan.D, self.fs
+        8 B symbol, 2 soft bits and a hard dibit -- the samples two chunks share twice (cover =
+        the chunks' total length over the row's).  bench.py reports the slowest of them."""
+        M, D, fs, ck = self.plan.M, self.plan.D, self.fs, self.ck
         yb = 8.0 * M * 72000.0 / fs
+        cover = ((ck.nchunk - 1) * ck.length + ck.rowlen - (ck.nchunk - 1) * ck.stride) / ck.rowlen
         ana = "k_pfb_analysis2" if os.environ.get("TETRA_WB_ANALYSIS") == "2" else \
             ("k_pfb_analysis1" if self.plan.oversample == 2 else "k_pfb_analysis")
         return {"waterfall": (12.0 * self.nfr * 2048 / self.Nw, "k_waterfall"),
@@ -360,13 +439,15 @@ class BenchStep:
                 "wb_fold": (8.0 + 8.0 * M / D, "k_pfb_fold"), "wb_fft": (2 * 8.0 * M / D, None),
                 "wb_resamp": (8.0 * M / D + yb + (yb * 2.0 / self.plan.c.up if self.om_grouped else 0.0),
                               "k_pfb_resamp_fix"),
-                "etsi_timing": (yb + 11.0 * M * 18000.0 / fs, "k_timing")}
+                "etsi_timing": (cover * (yb + 11.0 * M * 18000.0 / fs), "k_timing")}
 
     def config(self, world):
         return {"workload": f"C3: {self.Nw} samples of a {self.fs / 1e6:g} MSps capture per GPU, "
-                            f"{self.plan.M} carriers x {self.nchunk} timing chunks of {self.m2}",
+                            f"{self.plan.M} carriers x {self.nchunk} timing chunks of {self.ck.length} "
+                            f"every {self.m2}",
                 "wideband_samples_per_gpu": self.Nw, "sample_rate": self.fs, "carriers": self.plan.M,
-                "timing_chunks_per_carrier": self.nchunk, "parallelism": f"capture-sharded x{world}",
+                "timing_chunks_per_carrier": self.nchunk, "timing_chunk_overlap": self.ck.length - self.m2,
+                "parallelism": f"capture-sharded x{world}",
                 "filter_bank": f"D = M / {self.plan.oversample} ({self.fs / self.plan.D / 1e3:g} kHz carriers)",
                 "pipeline": self.pipelined}
 
@@ -377,7 +458,13 @@ class BenchStep:
         return f"C3: {self.Nw} samples"   # a substring of config()["workload"]
 
     def quality(self):
-        nb = self.nblock.cpu().numpy()
-        blocks = self.blocks.cpu().numpy()
-        ok = sum(int(blocks[i, :nb[i], 1].sum()) for i in range(self.C))
-        return dict(blocks=int(nb.sum()), crc_ok=ok, bursts=int(self.nburst.sum().item()))
+        """The last step's decoded work, each burst once (merge_chunks): bursts, blocks, CRC-good
+        blocks, and decoded_frac = bursts / the slots on air (M rows of rowlen samples, 1020 per
+        slot; a slot cut by the capture's start or end cannot be decoded, so ~0.97-0.99 is whole)."""
+        nb, bursts = self.nburst.cpu().numpy(), self.bursts.cpu().numpy()
+        nk, blocks = self.nblock.cpu().numpy(), self.blocks.cpu().numpy()
+        keep, kb = merge_chunks(nb, bursts, nk, blocks, self.plan.M, self.nchunk, self.m2)
+        slots = self.plan.M * self.ck.rowlen / BURST_SAMPLES
+        return dict(blocks=int(kb.sum()), crc_ok=int((blocks[..., 1].astype(bool) & kb).sum()),
+                    bursts=int(keep.sum()), decoded_frac=round(float(keep.sum()) / slots, 4),
+                    per_chunk=dict(bursts=int(nb.sum()), blocks=int(nk.sum())))

@@ -115,18 +115,22 @@ def etsi_rate(x, cells, seconds, threads=None):
 
 def wideband_rate(step, seconds):
     """C3 (wideband) on the host: the float64 channeliser restatement (oracle/wideband.py) over one
-    timing chunk per carrier, then the ETSI C oracle's timing + lower MAC per carrier (a sample of
-    carriers, extrapolated to all), one thread."""
+    timing chunk per carrier (the GPU's chunk length: stride m2 plus the overlap two chunks share),
+    then the ETSI C oracle's timing + lower MAC per carrier (a sample of carriers, extrapolated to
+    all), one thread.  Rated per stride: the channeliser's time scaled to m2 of the chunk's samples
+    (a host chain channelises each sample once), the timing's whole (it re-reads the overlap as the
+    GPU does)."""
     import numpy as np
     _paths()
     import etsi as E
     import wideband as W
     from tetraear.signal.wideband import DOWN, P_WB, UP
     d = W.design(step.fs, step.plan.M)
-    nw = (step.m2 * DOWN) // UP * step.plan.D + step.plan.M * P_WB + 64 * step.plan.D   # one chunk per carrier
+    L, m2 = step.ck.length, step.m2
+    nw = (L * DOWN) // UP * step.plan.D + step.plan.M * P_WB + 64 * step.plan.D   # one chunk per carrier
     x = step.x[:nw].cpu().numpy().view(np.complex64)[:, 0]
     t0 = time.perf_counter()
-    y = W.channelize(x.astype(np.complex128), d, step.m2).astype(np.complex64)
+    y = W.channelize(x.astype(np.complex128), d, L).astype(np.complex64)
     t_ch = time.perf_counter() - t0
     cells = step.cells[::step.nchunk].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
     rx = E.Receiver()
@@ -137,11 +141,13 @@ def wideband_rate(step, seconds):
         rx.lower_mac(soft, hard, int(cells[k]))
         k += 1
     t_c = (time.perf_counter() - t1) / k
-    total = t_ch + step.plan.M * t_c
-    return dict(value=nw / total / 1e6, unit="Msamples/s", cores=1, kind="port",
-                sample=f"{nw} samples @{step.fs / 1e6:g} MSps: numpy float64 channeliser ({t_ch:.2f} s) + C "
-                       f"oracle timing+lower MAC on {k} of {step.plan.M} carriers (x{step.plan.M / k:.1f} "
-                       f"extrapolated), 1 thread")
+    total = t_ch * m2 / L + step.plan.M * t_c
+    ns = m2 * step.fs / 72000.0   # wideband samples per stride
+    return dict(value=ns / total / 1e6, unit="Msamples/s", cores=1, kind="port",
+                sample=f"{nw} samples @{step.fs / 1e6:g} MSps: numpy float64 channeliser ({t_ch:.2f} s, rated for "
+                       f"{m2} of {L} samples) + C oracle timing+lower MAC on chunks of {L} samples on {k} of "
+                       f"{step.plan.M} carriers (x{step.plan.M / k:.1f} extrapolated), rated per {m2}-sample "
+                       f"stride, 1 thread")
 
 
 def main():
