@@ -27,7 +27,7 @@ for part in "$@"; do
       bash tools/profile_bench.sh r06_etsi_sc16_$V --iq sc16 && cp_summ r06_etsi_sc16_$V
       bash tools/profile_bench.sh r06_wideband_$V --chain wideband && cp_summ r06_wideband_$V ;;
     bench)
-      for a in "etsi:" "sc16:--iq sc16 --no-cpu" "wb:--chain wideband --no-cpu" "compat:--chain compat --no-cpu"; do
+      for a in "etsi:" "sc16:--iq sc16 --no-cpu" "wb:--chain wideband" "compat:--chain compat --no-cpu"; do
         n=${a%%:*}; args=${a#*:}
         timeout -k 10 400 python -u bench.py $args > $O/r06_bench_${n}_$V.log 2>&1
         tail -1 $O/r06_bench_${n}_$V.log | cut -c1-400
