@@ -177,20 +177,6 @@ def test_one_block_analysis_forms_bit_identical(monkeypatch):
 
 
 @pytest.mark.gpu
-def test_resampler_xcd_order_bit_identical(capture3, monkeypatch):
-    """TETRA_WB_RESAMP_XCD=1 only reorders the resampler's workgroups over the XCDs: y and the
-    Oerder-Meyr partials are bit-identical to the default order."""
-    from tetraear.signal.wideband import WidebandReceiver
-    x = capture3[0]
-    rx = WidebandReceiver()
-    outs = []
-    for v in ("0", "1"):
-        monkeypatch.setenv("TETRA_WB_RESAMP_XCD", v)
-        outs.append(rx.channelize_om(x))
-    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
-
-
-@pytest.mark.gpu
 def test_wideband_timing_bit_exact(capture, monkeypatch):
     """From y on the chain is the ETSI one: the GPU timing on the channeliser's own output equals
     oracle/etsi.py on the same y, carrier by carrier (TETRA_WB_OM=0: the timing's own Oerder-Meyr

@@ -838,17 +838,6 @@ struct ResampUse {
     }
 };
 
-// Block order by XCD (MI355X_MICROARCH.md, workgroup dispatch): blocks are dealt round-robin over the
-// eight XCDs, so block id b runs beside b + 8 on one L2.  Logical block xcd_block(b, n) gives each XCD
-// a contiguous run of logical blocks (bijective for any n; speed only, never correctness).
-__device__ __forceinline__ int xcd_block(int b, int n) {
-    const int q = n >> 3, r = n & 7, x = b & 7;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
-}
-
-// XCD (TETRA_WB_RESAMP_XCD): the groups of one carrier tile run in time order on one XCD, so the
-// 22 rows a workgroup shares with the next one in time are read once into that L2 (without it the
-// two are 13 block ids apart: different XCDs, every shared row fetched twice).
 // PRB (timing-only build, TETRA_WB_RESAMP_PROBE=1): no y stores -- what the write-out costs.
 // OM (tetra_channelize_om; UP a multiple of 4): each lane also leaves its group's Oerder-Meyr class
 // partials om[k][m] = (P0, P1, P2, P3), P_c = sum over o = c mod 4, ascending, of |y[UP m + o]|^2 --
@@ -858,7 +847,7 @@ template <int UP, int DOWN, int Q, bool ROT, int PRB = 0, bool OM = false>
 __global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict__ Y, int M, int nblk,
                                                         const float *__restrict__ gU, float2 *__restrict__ y,
                                                         int n_keep, float4 *__restrict__ om = nullptr,
-                                                        int ngrp = 0, int xcd = 0) {
+                                                        int ngrp = 0) {
     using U = ResampUse<UP, DOWN, Q>;
     constexpr U use{};
     constexpr int ROWS = U::ROWS;                       // rows of one output group
@@ -878,14 +867,8 @@ __global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     for (int e = tid; e < use.n; e += 256) tapP[e] = gU[e];
-    int bx = blockIdx.x, by = blockIdx.y;               // (carrier tile, time tile)
-    if (xcd) {
-        const int gy = gridDim.y, lb = xcd_block(by * gridDim.x + bx, gridDim.x * gy);
-        bx = lb / gy;
-        by = lb - bx * gy;
-    }
-    const int k = min(bx * RS_C + lane, M - 1);
-    const int m = by * 4 + wv;                          // output group: outputs UP m .. UP m + UP - 1
+    const int k = min(blockIdx.x * RS_C + lane, M - 1);
+    const int m = blockIdx.y * 4 + wv;                  // output group: outputs UP m .. UP m + UP - 1
     const int r0 = DOWN * m;                            // wave-uniform: row offsets are scalar
     // rows r0 .. r0 + ROWS - 1; a group reaching past nblk (the last ones) clamps its row index --
     // clamped rows only feed outputs n >= n_keep, which are not stored
@@ -927,7 +910,7 @@ __global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict
     for (int o = 0; o < UP; ++o) tile[lane * (OT + 1) + wv * UP + o] = make_float2(acc[o].x, acc[o].y);
     if constexpr (OM) {
         static_assert(UP % 4 == 0, "class partials need whole classes per group");
-        if (bx * RS_C + lane < M && m * UP < n_keep) {
+        if (blockIdx.x * RS_C + lane < M && m * UP < n_keep) {
             float p[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int o = 0; o < UP; ++o) p[o & 3] = p[o & 3] + fmaf(acc[o].x, acc[o].x, acc[o].y * acc[o].y);
@@ -935,7 +918,7 @@ __global__ __launch_bounds__(256) void k_pfb_resamp_fix(const float2 *__restrict
         }
     }
     __syncthreads();
-    const int k0 = bx * RS_C, n0 = by * OT;
+    const int k0 = blockIdx.x * RS_C, n0 = blockIdx.y * OT;
     for (int e = tid; e < RS_C * OT; e += 256) {
         const int c = e / OT, o = e - c * OT, kk = k0 + c, n = n0 + o;
         if constexpr (PRB == 1) {
@@ -1169,23 +1152,22 @@ int channelize(tetra_ctx *ctx, const tetra_wb_plan *P, const void *x, size_t Nw,
         const dim3 gr((unsigned)((M + RS_C - 1) / RS_C), (unsigned)((n_keep + 4 * P->up - 1) / (4 * P->up)));
         const float *gu = taps + L + P->up * RS_QP;
         // TETRA_WB_RESAMP_PROBE=1 (timing-only, wrong y): the D = M / 2 resampler without its stores
-        const char *pe = getenv("TETRA_WB_RESAMP_PROBE"), *xe = getenv("TETRA_WB_RESAMP_XCD");
-        const int xcd = xe ? atoi(xe) : 0;
+        const char *pe = getenv("TETRA_WB_RESAMP_PROBE");
         if (fix36 && pe && atoi(pe) == 1)
             hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false, 1>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk,
-                               gu, yd, (int)n_keep, nullptr, 0, xcd);
+                               gu, yd, (int)n_keep);
         else if (fix36 && omd)   // + the Oerder-Meyr group partials
             hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false, 0, true>), gr, dim3(256), 0, ctx->stream, u, M,
-                               (int)nblk, gu, yd, (int)n_keep, omd, ngrp, xcd);
+                               (int)nblk, gu, yd, (int)n_keep, omd, ngrp);
         else if (fix36)   // D = M / 2: always the fused analysis, Y rotated there
             hipLaunchKernelGGL((k_pfb_resamp_fix<36, 25, 23, false>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk, gu,
-                               yd, (int)n_keep, nullptr, 0, xcd);
+                               yd, (int)n_keep);
         else if (fused)   // Y already carries the mixer rotation
             hipLaunchKernelGGL((k_pfb_resamp_fix<18, 25, 45, false>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk, gu,
-                               yd, (int)n_keep, nullptr, 0, xcd);
+                               yd, (int)n_keep);
         else
             hipLaunchKernelGGL((k_pfb_resamp_fix<18, 25, 45, true>), gr, dim3(256), 0, ctx->stream, u, M, (int)nblk, gu,
-                               yd, (int)n_keep, nullptr, 0, xcd);
+                               yd, (int)n_keep);
         HIP_TRY(ctx, hipGetLastError());
     } else {
         PROF(ctx, "wb_resamp");
