@@ -11,7 +11,7 @@ outside that band (test_spectrum.py); the channeliser within Y_TOL (test_wideban
 Covered: the default compat process() against the sequential (reference-order) oracle, compat
 batches (latency and throughput kernels) and the direct SignalProcessor methods,
 compat decoder streams, the ETSI chain with its lower MAC (cell given and acquired) and its component
-methods, the streaming ETSI receiver over random chunk patterns (round 6), the scanner detector, the AFC gate, the wideband channeliser, device-tensor batches.  Each
+methods, the streaming ETSI receiver over random chunk patterns (round 6), the scanner detector, the AFC gate, the wideband channeliser and its chunked timing (overlapping chunks, round 6), device-tensor batches.  Each
 host-side bug the sweep found keeps its case here ("sweep").
 """
 import numpy as np
@@ -474,6 +474,66 @@ def test_compat_device_tensor_batches_equal_host(seed):
     got = SignalProcessor(fs).process_batch(t, offs)
     for g, w in zip(got, want):
         assert np.array_equal(g, w), (seed, fs, C, N, x.dtype)
+
+
+@pytest.fixture(scope="module")
+def y72():
+    """72 kHz rows from the GPU channel filter of two synthetic 2.4 MSps channels (the timing's input)."""
+    from tetraear import _hip
+    from tetraear.signal.etsi import etsi_plan, lengths, synth
+    iq = synth(2, 262144, seed=31, snr_db=18.0)[0]
+    plan = etsi_plan()
+    _, M2, _ = lengths(plan, iq.shape[1])
+    y = np.zeros((2, M2), np.complex64)
+    c = _hip.ctx()
+    c.check(c.lib.tetra_etsi_chanfilt(c.handle, plan, _hip.ptr(iq), 2, iq.shape[1], _hip.ptr(y)), "chanfilt")
+    return y
+
+
+@pytest.mark.parametrize("seed", range(12 * SCALE))
+def test_timing_chunks_random_vs_oracle(seed, y72):
+    """tetra_etsi_timing_chunks (the wideband timing, round 6) at random geometries: rows, row length,
+    chunk stride and length (overlapping, tiling or with gaps), the last chunk cut by the row's end,
+    resampler group sizes, the grouped Oerder-Meyr sums or the timing's own pass -- every output of
+    every chunk bit-identical to the oracle's timing of the chunk's samples."""
+    from tetraear import _hip
+    from tetraear.signal.etsi import etsi_plan
+    rng = np.random.default_rng(12000 + seed)
+    M = int(rng.integers(1, 5))
+    rowlen = int(rng.integers(16, 3 * y72.shape[1]))
+    grouped = bool(rng.uniform() < 0.6)
+    U = 4 * int(rng.integers(1, 17))
+    stride = int(rng.integers(1, max(2, rowlen // 2)))
+    if grouped:
+        stride = max(4, stride - stride % 4)
+    length = int(rng.integers(16, max(17, min(rowlen, 3 * stride) + 1)))
+    nchunk = max(1, min((rowlen - 16) // stride + 1, int(rng.integers(1, 12))))
+    rows = np.stack([np.resize(np.roll(y72[r % 2], int(rng.integers(0, y72.shape[1]))), rowlen)
+                     for r in range(M)]).astype(np.complex64)
+    if rng.uniform() < 0.3:   # a noise row among them
+        rows[-1] = (rng.standard_normal(rowlen) + 1j * rng.standard_normal(rowlen)).astype(np.complex64)
+    ngrp = -(-rowlen // U)
+    om = np.stack([E.Receiver.om_group_partials(r, U) for r in rows]).astype(np.float32) if grouped else None
+    C, sm = M * nchunk, length // 4 + 2
+    sym = np.zeros((C, sm), np.complex64)
+    soft, hard, ns = np.zeros((C, 2 * sm), np.int8), np.zeros((C, sm), np.uint8), np.zeros(C, np.int32)
+    c = _hip.ctx()
+    c.check(c.lib.tetra_etsi_timing_chunks(c.handle, etsi_plan(), _hip.ptr(rows), M, rowlen, nchunk, stride, length,
+                                           _hip.ptr(om), ngrp if grouped else 0, U, _hip.ptr(sym), _hip.ptr(soft),
+                                           _hip.ptr(hard), _hip.ptr(ns), sm, None), "timing_chunks")
+    ora = E.Receiver()
+    case = (seed, M, rowlen, nchunk, stride, length, U, grouped)
+    for r in range(M):
+        for ci in range(nchunk):
+            s0 = ci * stride
+            L = min(length, rowlen - s0)
+            A = E.Receiver.om_grouped(rows[r], s0, L, U, om[r]) if grouped else None
+            so, sbo, ho, _ = ora.timing(rows[r, s0:s0 + L], om=A)
+            ch = r * nchunk + ci
+            n = int(ns[ch])
+            assert n == len(so), case + (r, ci)
+            assert np.array_equal(sym[ch, :n], so) and np.array_equal(hard[ch, :n - 1], ho), case + (r, ci)
+            assert np.array_equal(soft[ch, :2 * (n - 1)], sbo), case + (r, ci)
 
 
 @pytest.mark.parametrize("seed", range(12 * SCALE))
