@@ -76,6 +76,28 @@ struct Biquad {
     }
 };
 
+// fp32: the same operations, paired -- (b1 x, b2 x) and (a1 xn, a2 xn) are each one v_pk_mul_f32
+// (x and xn broadcast by op_sel_hi) and the two differences one v_pk_add_f32 (the product negated
+// by neg_lo/neg_hi: a - b and a + (-b) are the same IEEE operation), so a section's tick is 6 VALU
+// instead of 9.  Every product and sum is the scalar one, rounded once: bit-identical.
+typedef float pkf2 __attribute__((ext_vector_type(2)));
+template <>
+struct Biquad<float> {
+    pkf2 b12, a12;
+    float b0, z0, z1;
+    __device__ __forceinline__ Biquad(float b0_, float b1, float b2, float a1, float a2, float z0_, float z1_)
+        : b12{b1, b2}, a12{a1, a2}, b0(b0_), z0(z0_), z1(z1_) {}
+    __device__ __forceinline__ float step(float x) {
+        const float m0 = b0 * x;
+        const pkf2 p1 = b12 * pkf2{x, x};
+        const float xn = m0 + z0;
+        const pkf2 p3 = p1 - a12 * pkf2{xn, xn};
+        z0 = p3.x + z1;
+        z1 = p3.y;
+        return xn;
+    }
+};
+
 template <typename T>
 __device__ __forceinline__ Biquad<T> load_section(const T *sos, const T *zi, int s, T x0) {
     return Biquad<T>{sos[6 * s], sos[6 * s + 1], sos[6 * s + 2], sos[6 * s + 4], sos[6 * s + 5], zi[2 * s] * x0,
@@ -875,29 +897,83 @@ struct Lfilt {
     }
 };
 
+// The same lfilter with its four states spread over a quad of lanes (NT = 5: butter(4)): lane k holds
+// z_k; per sample every lane forms y = z_0 + b0 x from quad lane 0's state (DPP broadcast), and
+// z_k = (z_{k+1} + x b_{k+1}) - y a_{k+1} from lane k+1's (DPP shift; lane 3: x b_4 - y a_4).  The
+// operations and their order are Lfilt's; a sample is 5 float64 operations per wave instead of 17.
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double v) {
+    const long long b = __builtin_bit_cast(long long, v);
+    // quad_perm writes every lane: no `old` operand to materialise
+    const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffff), CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+struct Lfilt4 {
+    double b0, bk, ak, z;
+    bool last;
+    __device__ __forceinline__ void init(const double *b, const double *a, const double *zi, double x0) {
+        const int k = threadIdx.x & 3;
+        b0 = b[0];
+        bk = b[k + 1];
+        ak = a[k + 1];
+        z = zi[k] * x0;
+        last = k == 3;
+    }
+    __device__ __forceinline__ double step(double xn) {
+        const double z0 = dpp64<0x00>(z);   // quad_perm [0,0,0,0]: lane 0's z_0
+        const double zs = dpp64<0xF9>(z);   // quad_perm [1,2,3,3]: lane k+1's z_{k+1}
+        const double yn = z0 + b0 * xn;
+        const double t = xn * bk;
+        z = (last ? t : zs + t) - yn * ak;
+        return yn;
+    }
+};
+// Lanes per stream of the filtfilt kernels: 4 (Lfilt4) for a few channels, where one wave's issue
+// sets the time -- one 131072-sample chunk (C2): filtfilt 1.97 -> ~1.7 ms, process() 7.2 -> 7.0 ms --
+// and 1 (Lfilt) for batches, which are bound by the load path: at 8192 channels Lfilt4's four lanes
+// per stream make the two passes 1.04 + 0.75 -> 1.30 + 0.99 ms (profiles/r06_ab_compat_lf4.txt).
+// TETRA_COMPAT_LF=1 / 4 forces a form (same-box A/B).
+constexpr int LF4_MAXC = 64;
+static int lf_lanes(int C) {
+    const char *e = getenv("TETRA_COMPAT_LF");
+    if (e && (atoi(e) == 1 || atoi(e) == 4)) return atoi(e);
+    return C <= LF4_MAXC ? 4 : 1;
+}
+
 constexpr int LFB = 16;   // samples per load batch; batches double-buffered
 
 // Forward pass over the odd extension (filtfilt padlen 3*NT) of the (optionally mixed) input.
-template <typename TIn, int NT>
+// MIX = false (launched when no channel mixes, e.g. on k_mix's pre-mixed rows): the mixer's sincos
+// code leaves the loop -- with it inlined 16 times the kernel holds values in AGPRs across the
+// recursion; the same operations otherwise.
+// QL lanes per stream: 1 (Lfilt) or 4 (Lfilt4, NT = 5: the quad's four lanes hold the same y and all
+// store it -- one address, one value -- so no per-sample branch).
+template <typename TIn, int NT, bool MIX = true, int QL = 1>
 __global__ __launch_bounds__(64) void k_lf_fwd(const TIn *__restrict__ x, Lay lx, int C, long M, int pad,
                                                const double *__restrict__ b, const double *__restrict__ a,
                                                const double *__restrict__ zi, const double *__restrict__ mixc,
                                                const uint8_t *__restrict__ mixon, double fs,
                                                double *__restrict__ scr, Lay ls) {
+    static_assert(QL == 1 || (QL == 4 && NT == 5), "Lfilt4 holds butter(4)'s four states");
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-    const int ch = gid >> 1, comp = gid & 1;
-    if (ch >= C) return;
-    const bool mix = mixon && mixon[ch];
+    const int ch = (gid / QL) >> 1, comp = (gid / QL) & 1;
+    constexpr bool st = true;
+    if (ch >= C) return;   // whole quads
+    const bool mix = MIX && mixon && mixon[ch];
     const double c = mix ? mixc[ch] : 0.0;
     const TIn *xp = x + lx.off(ch, 0);
     const size_t sx = lx.s_n;
     const long L = M + 2 * pad;
-    Lfilt<NT> f;
+    typename std::conditional<QL == 4, Lfilt4, Lfilt<NT>>::type f;
     f.init(b, a, zi, lf_ext(xp, sx, M, pad, 0, comp, mix, c, fs));
     double *sp = scr + ls.off(ch, 0) + comp;
     const size_t ss = ls.s_n;
     long j = 0;
-    for (; j < pad; ++j) sp[(size_t)j * ss] = f.step(lf_ext(xp, sx, M, pad, j, comp, mix, c, fs));
+    for (; j < pad; ++j) {
+        const double yv = f.step(lf_ext(xp, sx, M, pad, j, comp, mix, c, fs));
+        if (st) sp[(size_t)j * ss] = yv;
+    }
     // body: a batch's 16 (re, im) loads issue together, one batch ahead of the recursion; the
     // mixer (a divergent sincos branch) runs between load and recursion
     using P2 = typename std::conditional<sizeof(TIn) == 4, float2, double2>::type;
@@ -913,7 +989,10 @@ __global__ __launch_bounds__(64) void k_lf_fwd(const TIn *__restrict__ x, Lay lx
 #pragma unroll
         for (int u = 0; u < LFB; ++u) xs[u] = mix_pair((double)r[u].x, (double)r[u].y, j0 + u - pad, comp, mix, c, fs);
 #pragma unroll
-        for (int u = 0; u < LFB; ++u) sp[(size_t)(j0 + u) * ss] = f.step(xs[u]);
+        for (int u = 0; u < LFB; ++u) {
+            const double yv = f.step(xs[u]);
+            if (st) sp[(size_t)(j0 + u) * ss] = yv;
+        }
     };
     if (M >= 2 * LFB) {
         ld(ra, j);
@@ -930,21 +1009,26 @@ __global__ __launch_bounds__(64) void k_lf_fwd(const TIn *__restrict__ x, Lay lx
         run(rb, j + LFB);
         j += 2 * LFB;
     }
-    for (; j < L; ++j) sp[(size_t)j * ss] = f.step(lf_ext(xp, sx, M, pad, j, comp, mix, c, fs));
+    for (; j < L; ++j) {
+        const double yv = f.step(lf_ext(xp, sx, M, pad, j, comp, mix, c, fs));
+        if (st) sp[(size_t)j * ss] = yv;
+    }
 }
 
 // Reverse pass: y[t] = output at ext index t + pad, t in [0, M).
-template <int NT>
+template <int NT, int QL = 1>
 __global__ __launch_bounds__(64) void k_lf_bwd(const double *__restrict__ scr, Lay ls, int C, long M, int pad,
                                                const double *__restrict__ b, const double *__restrict__ a,
                                                const double *__restrict__ zi, double *__restrict__ out, Lay lo) {
+    static_assert(QL == 1 || (QL == 4 && NT == 5), "Lfilt4 holds butter(4)'s four states");
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-    const int ch = gid >> 1, comp = gid & 1;
-    if (ch >= C) return;
+    const int ch = (gid / QL) >> 1, comp = (gid / QL) & 1;
+    constexpr bool st = true;
+    if (ch >= C) return;   // whole quads
     const double *sp = scr + ls.off(ch, 0) + comp;
     const size_t ss = ls.s_n;
     const long L = M + 2 * pad;
-    Lfilt<NT> f;
+    typename std::conditional<QL == 4, Lfilt4, Lfilt<NT>>::type f;
     f.init(b, a, zi, sp[(size_t)(L - 1) * ss]);
     double *op = out + lo.off(ch, 0) + comp;
     const size_t so = lo.s_n;
@@ -957,7 +1041,10 @@ __global__ __launch_bounds__(64) void k_lf_bwd(const double *__restrict__ scr, L
     };
     auto run = [&](double (&v)[LFB], long j0) __attribute__((always_inline)) {
 #pragma unroll
-        for (int u = 0; u < LFB; ++u) op[(size_t)(j0 - u - pad) * so] = f.step(v[u]);
+        for (int u = 0; u < LFB; ++u) {
+            const double yv = f.step(v[u]);
+            if (st) op[(size_t)(j0 - u - pad) * so] = yv;
+        }
     };
     if (j - 2 * LFB + 1 >= pad) {
         ld(xa, j);
@@ -976,7 +1063,7 @@ __global__ __launch_bounds__(64) void k_lf_bwd(const double *__restrict__ scr, L
     }
     for (; j >= 0; --j) {
         const double yn = f.step(sp[(size_t)j * ss]);
-        if (j >= pad) op[(size_t)(j - pad) * so] = yn;
+        if (st && j >= pad) op[(size_t)(j - pad) * so] = yn;
     }
 }
 
@@ -1786,15 +1873,33 @@ int run_filtfilt(tetra_ctx *ctx, const tetra_compat_plan *P, const TIn *x, Lay l
     for (int k = 0; k < nt - 1; ++k) hc[2 * MAXTAP + k] = P->lzi[k];
     HIP_TRY(ctx, hipMemcpyAsync(coef, hc, sizeof hc, hipMemcpyHostToDevice, ctx->stream));
     const unsigned blk = 64;
+    const int ql = lf_lanes(C);
     {
         PROF(ctx, "compat_filtfilt_fwd");
-        hipLaunchKernelGGL((k_lf_fwd<TIn, 5>), dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, x, lx, C, M,
-                           pad, coef, coef + MAXTAP, coef + 2 * MAXTAP, mixc, mixon, P->fs_dec, scr, grouped(L));
+        const dim3 g1(grid_for((size_t)2 * C, blk)), g4(grid_for((size_t)8 * C, blk));
+        const Lay ls = grouped(L);
+        const double *cb = coef, *ca = coef + MAXTAP, *cz = coef + 2 * MAXTAP;
+        if (ql == 4 && mixon)
+            hipLaunchKernelGGL((k_lf_fwd<TIn, 5, true, 4>), g4, dim3(blk), 0, ctx->stream, x, lx, C, M, pad, cb, ca, cz,
+                               mixc, mixon, P->fs_dec, scr, ls);
+        else if (ql == 4)
+            hipLaunchKernelGGL((k_lf_fwd<TIn, 5, false, 4>), g4, dim3(blk), 0, ctx->stream, x, lx, C, M, pad, cb, ca, cz,
+                               mixc, mixon, P->fs_dec, scr, ls);
+        else if (mixon)
+            hipLaunchKernelGGL((k_lf_fwd<TIn, 5>), g1, dim3(blk), 0, ctx->stream, x, lx, C, M, pad, cb, ca, cz, mixc,
+                               mixon, P->fs_dec, scr, ls);
+        else
+            hipLaunchKernelGGL((k_lf_fwd<TIn, 5, false>), g1, dim3(blk), 0, ctx->stream, x, lx, C, M, pad, cb, ca, cz,
+                               mixc, mixon, P->fs_dec, scr, ls);
     }
     {
         PROF(ctx, "compat_filtfilt_bwd");
-        hipLaunchKernelGGL(k_lf_bwd<5>, dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, scr, grouped(L), C,
-                           M, pad, coef, coef + MAXTAP, coef + 2 * MAXTAP, out, lo);
+        if (ql == 4)
+            hipLaunchKernelGGL((k_lf_bwd<5, 4>), dim3(grid_for((size_t)8 * C, blk)), dim3(blk), 0, ctx->stream, scr,
+                               grouped(L), C, M, pad, coef, coef + MAXTAP, coef + 2 * MAXTAP, out, lo);
+        else
+            hipLaunchKernelGGL(k_lf_bwd<5>, dim3(grid_for((size_t)2 * C, blk)), dim3(blk), 0, ctx->stream, scr,
+                               grouped(L), C, M, pad, coef, coef + MAXTAP, coef + 2 * MAXTAP, out, lo);
     }
     return TETRA_OK;
 }
