@@ -381,3 +381,50 @@ def test_wideband_overlap_decodes_every_burst(capture3):
     finally:
         WB.OV_CHUNK = orig
     assert sum(map(len, ft)) < sum(map(len, frames)) - rx.plan.M   # >= 1 burst per carrier lost at the seams
+
+
+@pytest.mark.gpu
+def test_wideband_stream_equals_whole_capture(capture3):
+    """WidebandStream over pieces of a capture (seams anywhere, one piece shorter than a chunk)
+    decodes the bursts the whole capture does: per carrier the same stream positions (within the
+    timing phase) and the same CRC-good bits -- none lost or doubled at the pieces' seams."""
+    from tetraear.signal import wideband as WB
+    x, cells = capture3[0], capture3[1]
+    whole = WB.WidebandReceiver().decode(x, cells)
+    st = WB.WidebandStream(cells)
+    got = [[] for _ in range(len(cells))]
+    for a, b in ((0, 1_234_567), (1_234_567, 1_300_001), (1_300_001, 2_711_113), (2_711_113, len(x))):
+        for k, fr in enumerate(st.decode(x[a:b])):
+            got[k].extend(fr)
+    nmatch = 0
+    for k in range(len(cells)):
+        ws = [f["sample"] for f in whole[k]]
+        gs = [f["stream_sample"] for f in got[k]]
+        assert len(gs) == len(ws) and all(abs(p - q) <= 16 for p, q in zip(gs, ws)), (k, ws, gs)
+        for fw, fg in zip(whole[k], got[k]):
+            bw = [tuple(b["bits"]) for b in fw["blocks"] if b["crc_ok"]]
+            bg = [tuple(b["bits"]) for b in fg["blocks"] if b["crc_ok"]]
+            assert bw == bg, (k, fw["sample"])
+            nmatch += len(bw)
+    assert nmatch > 2 * len(cells)
+
+
+@pytest.mark.gpu
+def test_channelize_period_shift_bit_exact(capture3):
+    """What WidebandStream's tail rests on: a capture cut a whole number of its periods in (whole
+    resampler periods and whole cycles of the filter bank's (-1)^(k j) mixer term) channelises to the
+    uncut capture's outputs, bit for bit; one resampler period (25 blocks, odd) negates the odd
+    carriers."""
+    from tetraear.signal.wideband import WidebandReceiver, WidebandStream
+    x, cells = capture3[0], capture3[1]
+    rx = WidebandReceiver()
+    st = WidebandStream(cells)
+    p = rx.plan
+    assert st.per == 2 * p.D * p.c.down and st.ups == 2 * p.c.up
+    y = rx.channelize(x)
+    for k in (1, 37, 65):
+        yk = rx.channelize(x[k * st.per:])
+        assert np.array_equal(yk, y[:, k * st.ups:k * st.ups + yk.shape[1]]), k
+    y1 = rx.channelize(x[p.D * p.c.down:])
+    ref = y[:, p.c.up:p.c.up + y1.shape[1]]
+    assert np.array_equal(y1[0::2], ref[0::2]) and np.array_equal(y1[1::2], -ref[1::2])

@@ -242,6 +242,52 @@ class WidebandReceiver:
         return out
 
 
+class WidebandStream:
+    """Consecutive pieces of one continuous wideband capture decoded as one stream (the C3 form of the
+    ETSI receiver's streaming, signal/etsi.py EtsiStream): each call channelises the new samples
+    behind a tail of the previous ones and WidebandReceiver.decode's frames are kept once per carrier
+    by their position in the carrier's whole 72 kHz stream, so a burst across the seam between two
+    pieces is decoded too.  The tail starts a whole number of resampler periods (D x down input
+    samples -> up outputs) into the buffer, so its outputs are the previous buffer's at the same
+    stream positions, bit for bit, and it holds the last CARRY_Y outputs' input: every burst that the
+    buffer's end cut is whole in the next one.  The period also holds the filter bank's mixer term
+    ((-1)^(k j) at D = M / 2, (-i)^(k j) at M / 4: whole cycles of it), else odd carriers would
+    come out negated."""
+    CARRY_Y = 2 * BURST_SAMPLES
+
+    def __init__(self, cells, fs=FS_WB, M=M_WB, m2=M2_CHUNK, oversample=None, tol=64):
+        self.rx = WidebandReceiver(fs, M, m2, oversample)
+        self.cells = np.ascontiguousarray(cells, np.uint32)
+        p = self.rx.plan
+        blocks = int(np.lcm(p.c.down, p.oversample))   # filter-bank blocks per period
+        self.per, self.ups, self.M, self.tol = p.D * blocks, p.c.up * blocks // p.c.down, p.M, tol
+        self.reset()
+
+    def reset(self):
+        self.tail = np.zeros(0, np.complex64)
+        self.y0 = 0                                    # stream position of the buffer's first output
+        self.last = np.full(self.M, -(1 << 62), np.int64)   # stream position of each carrier's last frame
+
+    def decode(self, x):
+        """x: the next samples of the capture -> per carrier the frames first decoded now, each with
+        "stream_sample" (its start in the carrier's 72 kHz stream)."""
+        buf = np.concatenate([self.tail, np.asarray(x, np.complex64)])
+        _, n72 = self.rx.plan.lengths(len(buf))
+        out = [[] for _ in range(self.M)]
+        if n72 >= 16:
+            for k, fr in enumerate(self.rx.decode(buf, self.cells)):
+                for f in fr:
+                    a = self.y0 + f["sample"]
+                    if a > self.last[k] + self.tol:
+                        f["stream_sample"] = int(a)
+                        out[k].append(f)
+                        self.last[k] = a
+        T = max(0, (n72 - self.CARRY_Y) // self.ups) * self.per   # the next buffer starts here
+        self.tail = buf[T:]
+        self.y0 += self.ups * (T // self.per)
+        return out
+
+
 def synth_wideband(Nw, seed=1, snr_db=30.0, cfo_max=300.0, fs=FS_WB, M=M_WB, oversample=None):
     """Synthetic capture (device-generated, copied to the host): x [Nw] complex64, cells [M],
     kinds [M][NB], payload [M][NB][2][268], t0 [M] (carrier k is FFT bin k, at +k fs/M)."""
