@@ -11,7 +11,7 @@ outside that band (test_spectrum.py); the channeliser within Y_TOL (test_wideban
 Covered: the default compat process() against the sequential (reference-order) oracle, compat
 batches (latency and throughput kernels) and the direct SignalProcessor methods,
 compat decoder streams, the ETSI chain with its lower MAC (cell given and acquired) and its component
-methods, the streaming ETSI receiver over random chunk patterns (round 6), the scanner detector, the AFC gate, the wideband channeliser and its chunked timing (overlapping chunks, round 6), device-tensor batches.  Each
+methods, the streaming ETSI receiver over random chunk patterns (round 6), the scanner detector, the AFC gate, the wideband channeliser, its chunked timing (overlapping chunks, round 6) and its stream over capture pieces, device-tensor batches.  Each
 host-side bug the sweep found keeps its case here ("sweep").
 """
 import numpy as np
@@ -534,6 +534,32 @@ def test_timing_chunks_random_vs_oracle(seed, y72):
             assert n == len(so), case + (r, ci)
             assert np.array_equal(sym[ch, :n], so) and np.array_equal(hard[ch, :n - 1], ho), case + (r, ci)
             assert np.array_equal(soft[ch, :2 * (n - 1)], sbo), case + (r, ci)
+
+
+@pytest.mark.parametrize("seed", range(4 * SCALE))
+def test_wideband_stream_random_pieces(seed):
+    """WidebandStream (round 6) over random cuts of a random-length capture at a random SNR: every
+    carrier's frames are the whole capture's -- stream positions within the timing phase, the same
+    CRC-good bits (test_wideband.py's equality, on pieces nobody chose)."""
+    from tetraear.signal import wideband as WB
+    rng = np.random.default_rng(13000 + seed)
+    Nw = int(rng.integers(600_000, 3_000_000))
+    x, cells = WB.synth_wideband(Nw, seed=13100 + seed, snr_db=float(rng.uniform(20, 30)))[:2]
+    whole = WB.WidebandReceiver().decode(x, cells)
+    cuts = np.sort(rng.choice(np.arange(1, Nw), size=int(rng.integers(1, 5)), replace=False))
+    st = WB.WidebandStream(cells)
+    got = [[] for _ in range(len(cells))]
+    for a, b in zip(np.r_[0, cuts], np.r_[cuts, Nw]):
+        for k, fr in enumerate(st.decode(x[a:b])):
+            got[k].extend(fr)
+    case = (seed, Nw, cuts.tolist())
+    for k in range(len(cells)):
+        ws = [f["sample"] for f in whole[k]]
+        gs = [f["stream_sample"] for f in got[k]]
+        assert len(gs) == len(ws) and all(abs(p - q) <= 16 for p, q in zip(gs, ws)), case + (k, ws, gs)
+        for fw, fg in zip(whole[k], got[k]):
+            assert [tuple(b["bits"]) for b in fw["blocks"] if b["crc_ok"]] == \
+                [tuple(b["bits"]) for b in fg["blocks"] if b["crc_ok"]], case + (k, fw["sample"])
 
 
 @pytest.mark.parametrize("seed", range(12 * SCALE))
