@@ -98,6 +98,50 @@ def test_merge_chunks_keeps_each_burst_once():
                           (np.arange(16)[None, :] < nk[:, None]))
 
 
+def test_wideband_stream_host_logic(monkeypatch):
+    """WidebandStream's host side on the CPU (decode stubbed): buffers start whole periods (20000
+    input samples -> 72 outputs) into the previous one, keep the last CARRY_Y outputs' input, and
+    a frame seen again from the next buffer (same stream position to within the tolerance) is
+    emitted once."""
+    from tetraear.signal import wideband as WB
+    st = None
+    p = WB.wb_plan()
+    calls = []
+
+    def fake_decode(self, x, cells):
+        _, n72 = p.lengths(len(x))
+        calls.append((len(x), n72))
+        y0 = st.y0
+        out = [[], []]
+        for k in range(2):   # a burst every 1020 stream outputs, carrier 1 offset by 500
+            a0 = (y0 - 500 * k + 1019) // 1020 * 1020 + 500 * k
+            for a in range(a0, y0 + n72 - 1020, 1020):
+                out[k].append({"sample": a - y0 + (3 if len(calls) % 2 else 0), "blocks": []})
+        return out
+
+    monkeypatch.setattr(WB.WidebandReceiver, "decode", fake_decode)
+    st = WB.WidebandStream(np.zeros(p.M, np.uint32))
+    st.M = 2
+    st.last = np.full(2, -(1 << 62), np.int64)
+    got = [[], []]
+    total = 0
+    for n in (700_000, 5_000, 1_300_000, 2_000_003, 999_999):
+        before = len(st.tail)
+        fr = st.decode(np.zeros(n, np.complex64))
+        total += n
+        assert (total - len(st.tail)) % st.per == 0                  # buffers start on whole periods
+        assert st.y0 == (total - len(st.tail)) // st.per * st.ups    # ... at that stream position
+        _, n72 = p.lengths(before + n)
+        if n72 > st.CARRY_Y:
+            assert p.lengths(len(st.tail))[1] >= st.CARRY_Y - st.ups   # the carried outputs
+        for k in range(2):
+            got[k].extend(f["stream_sample"] for f in fr[k])
+    n72 = p.lengths(total)[1]
+    for k in range(2):   # every burst of the stream once, at its position (to within the phase)
+        want = list(range(500 * k, n72 - 1020, 1020))
+        assert len(got[k]) == len(want) and all(0 <= g - w <= 3 for g, w in zip(got[k], want)), k
+
+
 @pytest.fixture(scope="module")
 def capture():
     from tetraear.signal.wideband import synth_wideband
