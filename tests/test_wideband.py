@@ -454,21 +454,25 @@ def test_wideband_stream_equals_whole_capture(capture3):
 
 
 @pytest.mark.gpu
-def test_channelize_period_shift_bit_exact(capture3):
+@pytest.mark.parametrize("oversample", [2, 4])
+def test_channelize_period_shift_bit_exact(capture3, oversample):
     """What WidebandStream's tail rests on: a capture cut a whole number of its periods in (whole
-    resampler periods and whole cycles of the filter bank's (-1)^(k j) mixer term) channelises to the
-    uncut capture's outputs, bit for bit; one resampler period (25 blocks, odd) negates the odd
-    carriers."""
-    from tetraear.signal.wideband import WidebandReceiver, WidebandStream
+    resampler periods and whole cycles of the filter bank's mixer term, (-1)^(k j) at D = M / 2,
+    (-i)^(k j) at M / 4) channelises to the uncut capture's outputs, bit for bit; at D = M / 2 one
+    resampler period (25 blocks, odd) negates the odd carriers."""
+    from tetraear.signal.wideband import WidebandReceiver, WidebandStream, synth_wideband
     x, cells = capture3[0], capture3[1]
-    rx = WidebandReceiver()
-    st = WidebandStream(cells)
+    if oversample == 4:
+        x = synth_wideband(2_000_000, seed=23, snr_db=25.0, oversample=4)[0]
+    rx = WidebandReceiver(oversample=oversample)
+    st = WidebandStream(cells, oversample=oversample)
     p = rx.plan
-    assert st.per == 2 * p.D * p.c.down and st.ups == 2 * p.c.up
+    assert st.per == 20000 and st.ups == 72 and st.per % (p.D * p.c.down) == 0
     y = rx.channelize(x)
     for k in (1, 37, 65):
         yk = rx.channelize(x[k * st.per:])
         assert np.array_equal(yk, y[:, k * st.ups:k * st.ups + yk.shape[1]]), k
-    y1 = rx.channelize(x[p.D * p.c.down:])
-    ref = y[:, p.c.up:p.c.up + y1.shape[1]]
-    assert np.array_equal(y1[0::2], ref[0::2]) and np.array_equal(y1[1::2], -ref[1::2])
+    if oversample == 2:
+        y1 = rx.channelize(x[p.D * p.c.down:])
+        ref = y[:, p.c.up:p.c.up + y1.shape[1]]
+        assert np.array_equal(y1[0::2], ref[0::2]) and np.array_equal(y1[1::2], -ref[1::2])
