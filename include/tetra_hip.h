@@ -481,7 +481,7 @@ int tetra_wb_lengths(const tetra_wb_plan *plan, size_t Nw, int64_t *nblk, int64_
 int tetra_channelize(tetra_ctx *ctx, const tetra_wb_plan *plan, const void *x, size_t Nw, void *y, size_t n_keep);
 /* tetra_channelize that also leaves om [M][ceil(n_keep / up)] float4: per carrier and group of up
  * consecutive outputs, the Oerder-Meyr class partials (sum over o = c mod 4 of |y[up g + o]|^2, o
- * ascending; oracle eo_om_group_partials) for tetra_etsi_timing_om.  D = M / 2 plan (up = 36) only. */
+ * ascending; oracle eo_om_group_partials) for tetra_etsi_timing_chunks (and _om).  D = M / 2 plan (up = 36) only. */
 int tetra_channelize_om(tetra_ctx *ctx, const tetra_wb_plan *plan, const void *x, size_t Nw, void *y, size_t n_keep,
                         void *om);
 /* Synthetic wideband capture: M carriers of tetra_synth_etsi bursts at fs/D, filter-bank
